@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Headline benchmark: samples/sec/node + step time of the reference model
+(src/model.py LeNet-5, "default" config) trained with DDP on 1/2/4/8 MI355X.
+
+BASELINE.json metric: "samples/sec/node + step time, src/model.py default, DDP
+1/2/4/8 MI355X"; the reference's published number is 892 samples/s (mean over 6
+epochs, batch 32).
+
+Each timed step is a FULL reference training step (src/trainer.py:180-197):
+sample a batch from the dataset (synthetic CIFAR-shaped uint8 data resident in
+HBM), RandomCrop(32, pad 4) + HFlip + Normalize (src/utils/functions.py:5-12),
+forward, softmax-cross-entropy, loss + accuracy accumulation (on device),
+backward, DDP gradient all-reduce (RCCL, W > 1) and the SGD(lr=1e-3,
+momentum=0.9) update -- random-init weights, fp32 compute.
+
+Scaling modes:
+  weak (default)  per-GPU batch fixed at --batch (32 = the reference's batch), global batch = 32*N
+  reference       global batch 32 split across ranks (src/trainer.py:62-64)
+
+Usage:  python bench.py --gpus N --steps K --warmup W
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+BASELINE_SAMPLES_PER_S = 892.0  # BASELINE.md headline (CPU, batch 32)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (weak) / global batch (reference)")
+    ap.add_argument("--scaling", choices=["weak", "reference"], default="weak")
+    ap.add_argument("--model", default="default", choices=["default", "tiny"])
+    ap.add_argument("--steps-per-graph", type=int, default=16)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dataset-size", type=int, default=50000)
+    ap.add_argument("--optimizer", default="sgd")
+    ap.add_argument("--seed", type=int, default=32)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.parallel.sampler import shard_indices
+    from ml_trainer_amd.utils.flat import FlatParams
+
+    torch.manual_seed(args.seed)
+    model = MLModel(args.model).to(dev)
+    flat = FlatParams(model.parameters())
+    if world > 1:
+        dist.broadcast(flat.data, src=0)  # DDP-style initial parameter broadcast
+    opt = build_optimizer(args.optimizer, model.parameters(), lr=1e-3, momentum=0.9, weight_decay=0.0, flat=flat)
+    per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
+    engine = LeNetStepEngine(model, flat, max_batch=per_gpu, optimizer=opt, world_size=world, seed=args.seed)
+
+    # Synthetic CIFAR-10-shaped dataset (uint8 HWC) resident in HBM; random labels.
+    N = args.dataset_size
+    g = torch.Generator(device=dev).manual_seed(1234)
+    data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    targets = torch.randint(0, 10, (N,), dtype=torch.int64, device=dev, generator=g)
+    engine.set_dataset(data, targets, batch_size=per_gpu, augment=True)
+
+    state = {"epoch": 0, "steps_left": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}
+
+    def new_epoch():
+        idx = shard_indices(N, world, rank, shuffle=True, seed=0, epoch=state["epoch"])
+        state["epoch"] += 1
+        state["shard_len"] = len(idx)
+        state["steps_per_epoch"] = math.ceil(len(idx) / per_gpu)
+        state["step_in_epoch"] = 0
+        engine.start_epoch(torch.as_tensor(idx, dtype=torch.int32))
+
+    def run(nsteps: int) -> int:
+        """Run nsteps training steps (crossing epochs as needed); return samples processed on this rank."""
+        samples = 0
+        while nsteps > 0:
+            if state["step_in_epoch"] >= state["steps_per_epoch"]:
+                new_epoch()
+            left = state["steps_per_epoch"] - state["step_in_epoch"]
+            full_left = left - (1 if state["shard_len"] % per_gpu else 0)
+            if full_left > 0:
+                k = min(nsteps, full_left)
+                engine.train_steps(per_gpu, k, use_graph=not args.no_graph, steps_per_graph=args.steps_per_graph)
+                samples += k * per_gpu
+            else:
+                k = 1
+                last = state["shard_len"] - (state["steps_per_epoch"] - 1) * per_gpu
+                engine.train_steps(last, 1, use_graph=not args.no_graph, steps_per_graph=1)
+                samples += last
+            state["step_in_epoch"] += k
+            nsteps -= k
+        return samples
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    samples = run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    tot = torch.tensor([elapsed, float(samples)], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = tot[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        s_sum = tot[1:2].clone()
+        dist.all_reduce(s_sum, op=dist.ReduceOp.SUM)
+        elapsed, total_samples = float(t_max.item()), float(s_sum.item())
+    else:
+        total_samples = float(samples)
+    # sanity: training actually ran (finite loss accumulated on device)
+    loss_sum = float(engine.stats[0].item())
+    value = total_samples / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    out = {
+        "metric": "samples/sec/node",
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak" if args.scaling == "weak" else "strong",
+        "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2),
+        "dtype": "fp32",
+        "data": "synthetic (CIFAR-10-shaped uint8 in HBM, on-GPU RandomCrop+HFlip+Normalize), random-init weights",
+        "config": {"model": f"src/model.py MLModel ({args.model} LeNet-5, 62,006 params)" if args.model == "default"
+                   else f"src/model.py MLModel ({args.model})",
+                   "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
+                   "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
+                   "hipgraph_steps": 0 if args.no_graph else args.steps_per_graph,
+                   "loss_finite": math.isfinite(loss_sum)},
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+"""In-tree build of the native extension ``ml_trainer_amd._C`` for gfx950.
+
+Why a hand-rolled build instead of ``torch.utils.cpp_extension``: the torch
+extension builder runs hipify over ``.hip``/``.cu`` sources; this framework is
+written for CDNA4 directly, so there is nothing to translate. The build is:
+
+* every ``csrc/kernels/*.hip`` file -> ``hipcc -c --offload-arch=gfx950 -O3``
+  (pure HIP, no torch headers: these recompile in seconds);
+* ``csrc/bindings.cpp`` and ``csrc/runtime/*.cpp`` (torch/pybind11 glue, the
+  graph executor, the pinned-host prefetcher, the RCCL communicator) ->
+  ``hipcc -c`` host-only objects with the torch include paths;
+* link with ``g++ -shared`` against *torch's own* ``libamdhip64``/``librccl``
+  (so exactly one HIP runtime is loaded per process) into
+  ``ml_trainer_amd/_C<ext_suffix>.so`` - in-tree, so it ships with the repo
+  snapshot to the GPU box and is visible to the round-end loaded-.so audit.
+
+Objects are cached under ``build/`` and rebuilt only when a source or any
+header under ``csrc/include`` is newer.
+
+Usage: ``python -m ml_trainer_amd.build [-j N] [--force] [--debug]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+import time
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(REPO_DIR, "build", "mlt")
+ARCH = os.environ.get("MLT_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, "_C" + suffix)
+
+
+def _torch_paths():
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    lib = os.path.join(tdir, "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "include", "*.h"))
+
+
+def _newer(src: str, obj: str, deps) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    if os.path.getmtime(src) > t:
+        return True
+    return any(os.path.getmtime(h) > t for h in deps)
+
+
+def _run(cmd):
+    t0 = time.time()
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if p.returncode != 0:
+        raise RuntimeError("build step failed:\n" + " ".join(cmd) + "\n" + p.stdout)
+    return time.time() - t0, p.stdout
+
+
+def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
+    import pybind11
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    tinc, tlib, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    common = ["-std=c++17", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-D__HIP_PLATFORM_AMD__=1",
+              f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    if debug:
+        common.append("-DMLT_DEBUG=1")
+    hdrs = _headers()
+
+    kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    host_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")) +
+                       glob.glob(os.path.join(CSRC, "comm", "*.cpp")) +
+                       [os.path.join(CSRC, "bindings.cpp")])
+    jobs_list = []
+    objs = []
+    for s in kernel_srcs:
+        o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(s, o, hdrs):
+            jobs_list.append([HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common,
+                              "-munsafe-fp-atomics", "-Wno-unused-result"])
+    for s in host_srcs:
+        o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(s, o, hdrs):
+            jobs_list.append([HIPCC, "-c", s, "-o", o, *opt, *common, "-DTORCH_EXTENSION_NAME=_C",
+                              "-DTORCH_API_INCLUDE_EXTENSION_H", f"-I{pyinc}",
+                              f"-I{pybind11.get_include()}", *[f"-isystem{i}" for i in tinc],
+                              "-I/opt/rocm/include", "-Wno-deprecated-declarations", "-Wno-unused-result"])
+    if jobs_list:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            futs = {ex.submit(_run, c): c for c in jobs_list}
+            for f in cf.as_completed(futs):
+                dt, _ = f.result()
+                if verbose:
+                    src = futs[f][2]
+                    print(f"[mlt-build] {os.path.relpath(src, REPO_DIR)}  {dt:.1f}s", flush=True)
+    out = ext_path()
+    if force or jobs_list or not os.path.exists(out):
+        link = ["g++", "-shared", "-o", out, *objs, f"-L{tlib}", f"-Wl,-rpath,{tlib}",
+                "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+                "-lamdhip64", "-lrccl", "-Wl,--no-as-needed"]
+        roctx = os.path.join(tlib, "libroctx64.so")
+        if os.path.exists(roctx):
+            link += ["-lroctx64"]
+        _run(link)
+        if verbose:
+            print(f"[mlt-build] linked {os.path.relpath(out, REPO_DIR)}", flush=True)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=int(os.environ.get("MAX_JOBS", "8")))
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    a = ap.parse_args(argv)
+    build(jobs=min(a.jobs, 16), force=a.force, debug=a.debug)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,402 @@
+// Python bindings of the native extension ml_trainer_amd._C.
+//
+// Every launcher validates dtype/device/contiguity/shape on the host BEFORE the
+// launch (a kernel that indexes past a buffer can take down the whole node), and
+// launches on torch's current HIP stream so it composes with torch ops and with
+// stream capture.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+#include <map>
+#include <memory>
+
+#include "mlt_kernels.h"
+#include "mlt_runtime.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace mlt {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA_T(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+
+static void check_dev(const Tensor& t, const char* name, at::ScalarType st, int64_t min_numel, int align = 16) {
+  TORCH_CHECK(t.defined(), name, " is undefined");
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.numel() >= min_numel, name, " too small: ", t.numel(), " < ", min_numel);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % align == 0, name, " must be ", align, "-byte aligned");
+}
+
+// ----------------------------------------------------------------------------
+// Flat optimizers
+// ----------------------------------------------------------------------------
+static OptHyper make_hyper(int kind, double lr, double momentum, double dampening, double wd, double beta1,
+                           double beta2, double eps, double lr_decay, double grad_scale, bool nesterov,
+                           bool maximize) {
+  OptHyper h;
+  h.kind = kind;
+  h.lr = (float)lr;
+  h.momentum = (float)momentum;
+  h.dampening = (float)dampening;
+  h.weight_decay = (float)wd;
+  h.beta1 = (float)beta1;
+  h.beta2 = (float)beta2;
+  h.eps = (float)eps;
+  h.lr_decay = (float)lr_decay;
+  h.grad_scale = (float)grad_scale;
+  h.nesterov = nesterov ? 1 : 0;
+  h.maximize = maximize ? 1 : 0;
+  return h;
+}
+
+void flat_optim(Tensor p, Tensor g, c10::optional<Tensor> s1, c10::optional<Tensor> s2, int kind, double lr,
+                double momentum, double dampening, double wd, double beta1, double beta2, double eps,
+                double lr_decay, double grad_scale, bool nesterov, bool maximize, c10::optional<Tensor> lr_t,
+                c10::optional<Tensor> lr_index, c10::optional<Tensor> step_t, double t_host,
+                c10::optional<Tensor> shadow, c10::optional<Tensor> coef) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
+  check_dev(p, "p", at::kFloat, n);
+  check_dev(g, "g", at::kFloat, n);
+  TORCH_CHECK(kind >= 0 && kind <= 4, "unknown optimizer kind");
+  const bool need_s2 = (kind == OPT_ADAM || kind == OPT_ADAMW || kind == OPT_ADAMAX);
+  const bool need_s1 = need_s2 || kind == OPT_ADAGRAD || (kind == OPT_SGD && momentum != 0.0);
+  float* s1p = nullptr;
+  float* s2p = nullptr;
+  if (need_s1) {
+    TORCH_CHECK(s1.has_value(), "optimizer state s1 required");
+    check_dev(*s1, "s1", at::kFloat, n);
+    s1p = s1->data_ptr<float>();
+  }
+  if (need_s2) {
+    TORCH_CHECK(s2.has_value(), "optimizer state s2 required");
+    check_dev(*s2, "s2", at::kFloat, n);
+    s2p = s2->data_ptr<float>();
+  }
+  const float* lrp = nullptr;
+  const int64_t* lidx = nullptr;
+  const int64_t* stp = nullptr;
+  uint16_t* sh = nullptr;
+  const float* cf = nullptr;
+  if (lr_t.has_value()) {
+    check_dev(*lr_t, "lr", at::kFloat, 1, 4);
+    lrp = lr_t->data_ptr<float>();
+  }
+  if (lr_index.has_value()) {
+    check_dev(*lr_index, "lr_index", at::kLong, 1, 8);
+    lidx = lr_index->data_ptr<int64_t>();
+  }
+  if (step_t.has_value()) {
+    check_dev(*step_t, "step", at::kLong, 1, 8);
+    stp = step_t->data_ptr<int64_t>();
+  }
+  if (shadow.has_value()) {
+    check_dev(*shadow, "shadow", at::kBFloat16, n);
+    sh = reinterpret_cast<uint16_t*>(shadow->data_ptr());
+  }
+  if (coef.has_value()) {
+    check_dev(*coef, "coef", at::kFloat, 1, 4);
+    cf = coef->data_ptr<float>();
+  }
+  const OptHyper h = make_hyper(kind, lr, momentum, dampening, wd, beta1, beta2, eps, lr_decay, grad_scale,
+                                nesterov, maximize);
+  launch_flat_optim(p.data_ptr<float>(), g.data_ptr<float>(), s1p, s2p, n, h, lrp, lidx, stp, (float)t_host, sh,
+                    cf, cur_stream());
+}
+
+void sq_norm(Tensor x, Tensor out) {
+  TORCH_CHECK(x.numel() % 4 == 0, "sq_norm needs numel % 4 == 0");
+  check_dev(x, "x", at::kFloat, x.numel());
+  check_dev(out, "out", at::kFloat, 1, 4);
+  launch_sq_norm(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream());
+}
+
+void clip_coef(Tensor sq, double max_norm, Tensor coef, Tensor total) {
+  check_dev(sq, "sq", at::kFloat, 1, 4);
+  check_dev(coef, "coef", at::kFloat, 1, 4);
+  check_dev(total, "total", at::kFloat, 1, 4);
+  launch_clip_coef(sq.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(), total.data_ptr<float>(),
+                   cur_stream());
+}
+
+void cast_bf16(Tensor x, Tensor y) {
+  TORCH_CHECK(x.numel() % 4 == 0 && x.numel() == y.numel(), "cast_bf16 shape");
+  check_dev(x, "x", at::kFloat, x.numel());
+  check_dev(y, "y", at::kBFloat16, x.numel());
+  launch_cast_bf16(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), cur_stream());
+}
+
+// ----------------------------------------------------------------------------
+// CIFAR device augmentation
+// ----------------------------------------------------------------------------
+static LeNetAug make_aug(const Tensor& data, const Tensor& perm, c10::optional<Tensor> ctrl, int64_t seed, int pad,
+                         int flip, int batch_stride, const std::vector<double>& mean,
+                         const std::vector<double>& stdv) {
+  TORCH_CHECK(data.dim() == 4 && data.size(1) == 32 && data.size(2) == 32 && data.size(3) == 3,
+              "data must be [N,32,32,3] uint8 (HWC)");
+  check_dev(data, "data", at::kByte, data.numel());
+  check_dev(perm, "perm", at::kInt, 1);
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean/std need 3 channels");
+  TORCH_CHECK(pad >= 0 && pad <= 16, "pad out of range");
+  LeNetAug A{};
+  A.data = data.data_ptr<uint8_t>();
+  A.perm = perm.data_ptr<int32_t>();
+  A.ctrl = nullptr;
+  if (ctrl.has_value()) {
+    check_dev(*ctrl, "ctrl", at::kLong, 2, 8);
+    A.ctrl = ctrl->data_ptr<int64_t>();
+  }
+  A.n = data.size(0);
+  A.perm_len = perm.numel();
+  A.seed = (uint64_t)seed;
+  A.pad = pad;
+  A.flip = flip;
+  A.batch_stride = batch_stride;
+  for (int c = 0; c < 3; ++c) {
+    A.mean[c] = (float)mean[c];
+    A.std[c] = (float)stdv[c];
+  }
+  return A;
+}
+
+void cifar_augment(Tensor data, Tensor perm, c10::optional<Tensor> ctrl, Tensor dtargets, Tensor out,
+                   Tensor targets_out, int64_t seed, int pad, int flip, int batch_stride, std::vector<double> mean,
+                   std::vector<double> stdv, int B) {
+  LeNetAug A = make_aug(data, perm, ctrl, seed, pad, flip, batch_stride, mean, stdv);
+  TORCH_CHECK(B > 0, "B must be positive");
+  check_dev(out, "out", at::kFloat, (int64_t)B * 3072);
+  check_dev(targets_out, "targets_out", at::kLong, B);
+  check_dev(dtargets, "dtargets", at::kLong, A.n);
+  launch_cifar_augment(A, B, out.data_ptr<float>(), targets_out.data_ptr<int64_t>(), dtargets.data_ptr<int64_t>(),
+                       cur_stream());
+}
+
+// ----------------------------------------------------------------------------
+// LeNet engine: holds every buffer pointer once, launches the fused step, and
+// captures multi-step hipGraphs.
+// ----------------------------------------------------------------------------
+class LeNetEngine {
+ public:
+  LeNetEngine(int cfg, int max_batch, py::dict bufs) : cfg_(cfg), max_b_(max_batch) {
+    TORCH_CHECK(cfg == LENET_DEFAULT || cfg == LENET_TINY, "unknown LeNet cfg");
+    TORCH_CHECK(max_batch > 0 && max_batch <= (1 << 20), "bad max_batch");
+    const int C1 = cfg == LENET_TINY ? 4 : 6, C2 = cfg == LENET_TINY ? 8 : 16;
+    const int F1 = cfg == LENET_TINY ? 64 : 120, F2 = cfg == LENET_TINY ? 32 : 84, NC = 10;
+    const int FLAT = C2 * 25;
+    const int64_t B = max_batch;
+    auto get = [&](const char* k, at::ScalarType st, int64_t n) -> Tensor {
+      TORCH_CHECK(bufs.contains(k), "missing engine buffer ", k);
+      Tensor t = bufs[k].cast<Tensor>();
+      check_dev(t, k, st, n);
+      keep_.push_back(t);
+      return t;
+    };
+    auto fp = [&](const char* k, int64_t n) { return get(k, at::kFloat, n).data_ptr<float>(); };
+    P_.w1 = fp("w1", C1 * 75);
+    P_.b1 = fp("b1", C1);
+    P_.w2 = fp("w2", C2 * C1 * 25);
+    P_.b2 = fp("b2", C2);
+    P_.w3 = fp("w3", (int64_t)F1 * FLAT);
+    P_.b3 = fp("b3", F1);
+    P_.w4 = fp("w4", F2 * F1);
+    P_.b4 = fp("b4", F2);
+    P_.w5 = fp("w5", NC * F2);
+    P_.b5 = fp("b5", NC);
+    P_.gw1 = fp("gw1", C1 * 75);
+    P_.gb1 = fp("gb1", C1);
+    P_.gw2 = fp("gw2", C2 * C1 * 25);
+    P_.gb2 = fp("gb2", C2);
+    P_.gw3 = fp("gw3", (int64_t)F1 * FLAT);
+    P_.gb3 = fp("gb3", F1);
+    P_.gw4 = fp("gw4", F2 * F1);
+    P_.gb4 = fp("gb4", F2);
+    P_.gw5 = fp("gw5", NC * F2);
+    P_.gb5 = fp("gb5", NC);
+    P_.x = fp("x", B * 3072);
+    P_.p1 = fp("p1", B * C1 * 196);
+    P_.p2 = fp("p2", B * FLAT);
+    P_.h1 = fp("h1", B * F1);
+    P_.h2 = fp("h2", B * F2);
+    P_.logits = fp("logits", B * NC);
+    P_.dlogits = fp("dlogits", B * NC);
+    P_.dh2 = fp("dh2", B * F2);
+    P_.dh1 = fp("dh1", B * F1);
+    P_.dflat = fp("dflat", B * FLAT);
+    P_.g1 = fp("g1", B * C1 * 196);
+    P_.slab1 = fp("slab1", B * C1 * 128);
+    P_.i1 = get("i1", at::kByte, B * C1 * 196).data_ptr<uint8_t>();
+    P_.i2 = get("i2", at::kByte, B * FLAT).data_ptr<uint8_t>();
+    P_.targets = get("targets", at::kLong, B).data_ptr<int64_t>();
+    P_.stats = get("stats", at::kDouble, 2).data_ptr<double>();  // 16B-aligned by get()
+    P_.counters = reinterpret_cast<unsigned*>(get("counters", at::kInt, C1 + 1).data_ptr<int32_t>());
+    P_.dtargets = nullptr;
+    A_ = LeNetAug{};
+    O_ = LeNetOpt{};
+  }
+
+  void set_aug(Tensor data, Tensor perm, Tensor ctrl, Tensor dtargets, int64_t seed, int pad, int flip,
+               int batch_stride, std::vector<double> mean, std::vector<double> stdv) {
+    A_ = make_aug(data, perm, ctrl, seed, pad, flip, batch_stride, mean, stdv);
+    TORCH_CHECK(A_.ctrl != nullptr, "ctrl required");
+    check_dev(dtargets, "dtargets", at::kLong, A_.n);
+    P_.dtargets = dtargets.data_ptr<int64_t>();
+    aug_keep_ = {data, perm, ctrl, dtargets};
+    graphs_.clear();
+  }
+
+  void clear_aug() {
+    A_.data = nullptr;
+    P_.dtargets = nullptr;
+    graphs_.clear();
+  }
+
+  void set_ctrl(Tensor ctrl) {
+    check_dev(ctrl, "ctrl", at::kLong, 2, 8);
+    A_.ctrl = ctrl.data_ptr<int64_t>();
+    ctrl_keep_ = ctrl;
+    graphs_.clear();
+  }
+
+  void set_opt(Tensor p, Tensor g, c10::optional<Tensor> s1, c10::optional<Tensor> s2, int kind, double lr,
+               double momentum, double dampening, double wd, double beta1, double beta2, double eps,
+               double lr_decay, double grad_scale, bool nesterov, bool maximize, c10::optional<Tensor> lr_t,
+               bool lr_table, std::vector<int64_t> offsets) {
+    const int64_t n = p.numel();
+    check_dev(p, "p", at::kFloat, n);
+    check_dev(g, "g", at::kFloat, n);
+    O_ = LeNetOpt{};
+    O_.p = p.data_ptr<float>();
+    O_.g = g.data_ptr<float>();
+    O_.n = n;
+    O_.s1 = s1.has_value() ? s1->data_ptr<float>() : nullptr;
+    O_.s2 = s2.has_value() ? s2->data_ptr<float>() : nullptr;
+    if (s1.has_value()) check_dev(*s1, "s1", at::kFloat, n);
+    if (s2.has_value()) check_dev(*s2, "s2", at::kFloat, n);
+    O_.h = make_hyper(kind, lr, momentum, dampening, wd, beta1, beta2, eps, lr_decay, grad_scale, nesterov,
+                      maximize);
+    O_.lr_ptr = nullptr;
+    O_.lr_table = lr_table ? 1 : 0;
+    if (lr_t.has_value()) {
+      check_dev(*lr_t, "lr", at::kFloat, 1, 4);
+      O_.lr_ptr = lr_t->data_ptr<float>();
+    }
+    TORCH_CHECK(!lr_table || O_.lr_ptr, "lr_table requires an lr tensor");
+    TORCH_CHECK(offsets.size() == 10, "need the flat offsets of the 10 LeNet tensors");
+    const int C1 = cfg_ == LENET_TINY ? 4 : 6, C2 = cfg_ == LENET_TINY ? 8 : 16;
+    const int F1 = cfg_ == LENET_TINY ? 64 : 120, F2 = cfg_ == LENET_TINY ? 32 : 84;
+    const int64_t sizes[10] = {C1 * 75, C1, C2 * C1 * 25, C2, (int64_t)F1 * C2 * 25, F1, F2 * F1, F2, 10 * F2, 10};
+    for (int i = 0; i < 10; ++i) {
+      TORCH_CHECK(offsets[i] >= 0 && offsets[i] % 4 == 0 && offsets[i] + sizes[i] <= n,
+                  "flat offset ", i, " out of range / misaligned");
+      O_.off[i] = offsets[i];
+    }
+    opt_keep_.clear();
+    opt_keep_.push_back(p);
+    opt_keep_.push_back(g);
+    if (s1.has_value()) opt_keep_.push_back(*s1);
+    if (s2.has_value()) opt_keep_.push_back(*s2);
+    if (lr_t.has_value()) opt_keep_.push_back(*lr_t);
+    graphs_.clear();
+  }
+
+  void check_mode(int mode, int B) const {
+    TORCH_CHECK(B > 0 && B <= max_b_, "batch ", B, " outside [1, ", max_b_, "]");
+    if (mode & (LENET_OPT | LENET_REDUCE)) TORCH_CHECK(O_.g != nullptr, "set_opt() first");
+    if (mode & LENET_OPT) TORCH_CHECK(A_.ctrl != nullptr, "ctrl required for the fused optimizer");
+    if ((mode & LENET_OPT) && O_.lr_table) TORCH_CHECK(A_.ctrl != nullptr, "lr table needs ctrl");
+  }
+
+  void run(int mode, int B) {
+    check_mode(mode, B);
+    launch_lenet(cfg_, mode, B, P_, A_, O_, cur_stream());
+  }
+
+  // Capture `nsteps` consecutive steps (the device step counter advances inside)
+  void capture(int mode, int B, int nsteps) {
+    check_mode(mode, B);
+    TORCH_CHECK(nsteps >= 1 && nsteps <= 4096, "nsteps");
+    TORCH_CHECK((mode & LENET_BWD) == 0 || A_.ctrl != nullptr || nsteps == 1,
+                "multi-step capture needs the device step counter");
+    auto g = std::make_unique<HipGraph>();
+    const LeNetPtrs P = P_;
+    const LeNetAug A = A_;
+    const LeNetOpt O = O_;
+    const int cfg = cfg_;
+    g->capture([&](hipStream_t s) {
+      for (int i = 0; i < nsteps; ++i) launch_lenet(cfg, mode, B, P, A, O, s);
+    });
+    graphs_[key(mode, B, nsteps)] = std::move(g);
+  }
+
+  bool has_graph(int mode, int B, int nsteps) const { return graphs_.count(key(mode, B, nsteps)) != 0; }
+
+  void replay(int mode, int B, int nsteps) {
+    auto it = graphs_.find(key(mode, B, nsteps));
+    TORCH_CHECK(it != graphs_.end(), "no captured graph for this (mode, B, nsteps)");
+    it->second->launch(cur_stream());
+  }
+
+  size_t graph_nodes(int mode, int B, int nsteps) const {
+    auto it = graphs_.find(key(mode, B, nsteps));
+    return it == graphs_.end() ? 0 : it->second->num_nodes();
+  }
+
+  void reset_graphs() { graphs_.clear(); }
+
+ private:
+  static int64_t key(int mode, int B, int nsteps) {
+    return ((int64_t)mode << 48) | ((int64_t)B << 16) | (int64_t)nsteps;
+  }
+  int cfg_;
+  int max_b_;
+  LeNetPtrs P_{};
+  LeNetAug A_{};
+  LeNetOpt O_{};
+  std::vector<Tensor> keep_, aug_keep_, opt_keep_;
+  Tensor ctrl_keep_;
+  std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
+};
+
+}  // namespace mlt
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  using namespace mlt;
+  m.doc() = "ml_trainer_amd native gfx950 kernels and runtime";
+  m.attr("ARCH") = "gfx950";
+  m.def("flat_optim", &flat_optim, py::arg("p"), py::arg("g"), py::arg("s1"), py::arg("s2"), py::arg("kind"),
+        py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("lr_decay"), py::arg("grad_scale"), py::arg("nesterov"),
+        py::arg("maximize"), py::arg("lr_t") = py::none(), py::arg("lr_index") = py::none(),
+        py::arg("step_t") = py::none(), py::arg("t_host") = 1.0, py::arg("shadow") = py::none(),
+        py::arg("coef") = py::none());
+  m.def("sq_norm", &sq_norm);
+  m.def("clip_coef", &clip_coef);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("cifar_augment", &cifar_augment);
+  py::class_<LeNetEngine>(m, "LeNetEngine")
+      .def(py::init<int, int, py::dict>())
+      .def("set_aug", &LeNetEngine::set_aug)
+      .def("clear_aug", &LeNetEngine::clear_aug)
+      .def("set_ctrl", &LeNetEngine::set_ctrl)
+      .def("set_opt", &LeNetEngine::set_opt)
+      .def("run", &LeNetEngine::run)
+      .def("capture", &LeNetEngine::capture)
+      .def("has_graph", &LeNetEngine::has_graph)
+      .def("replay", &LeNetEngine::replay)
+      .def("graph_nodes", &LeNetEngine::graph_nodes)
+      .def("reset_graphs", &LeNetEngine::reset_graphs);
+  m.attr("LENET_FWD") = (int)LENET_FWD;
+  m.attr("LENET_CE") = (int)LENET_CE;
+  m.attr("LENET_BWD") = (int)LENET_BWD;
+  m.attr("LENET_OPT") = (int)LENET_OPT;
+  m.attr("LENET_REDUCE") = (int)LENET_REDUCE;
+}

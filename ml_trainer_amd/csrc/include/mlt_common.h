@@ -1,0 +1,94 @@
+// Common device helpers for the gfx950 (CDNA4) kernels of ml_trainer_amd.
+//
+// Conventions used throughout csrc/kernels:
+//  * wave64 everywhere: lane = threadIdx.x & 63, reductions are 6 xor-shuffle steps;
+//  * block sizes are multiples of 64;
+//  * every launcher takes a hipStream_t and never synchronises (graph-capturable);
+//  * shape assumptions are validated on the host (bindings.cpp) before launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define MLT_WAVE 64
+
+#define MLT_HIP_CHECK(expr)                                                          \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorString(_e), __FILE__, \
+              __LINE__, #expr);                                                      \
+      abort();                                                                       \
+    }                                                                                \
+  } while (0)
+
+namespace mlt {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Segmented sum over aligned groups of G lanes (G power of two, <= 64).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum; `red` must hold >= blockDim.x/64 floats of LDS. Result broadcast to all threads.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];  // fixed order: deterministic
+  return s;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float s = -INFINITY;
+  for (int i = 0; i < nw; ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
+// Counter-based hash (splitmix64 finaliser): stateless per-sample RNG that is
+// identical under hipGraph replay as long as the counter lives in device memory.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 via the hardware convert (keeps NaN a NaN).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+// XCD-aware bijective block remap (gfx950: 8 XCDs, blocks dealt round-robin).
+// Makes consecutive logical tiles land on one XCD so they share its L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+}  // namespace mlt

@@ -1,0 +1,77 @@
+// Host-visible launcher interface of the gfx950 kernels (csrc/kernels/*.hip).
+// Pure HIP types only: the torch glue lives in csrc/bindings.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mlt_optim.h"
+
+namespace mlt {
+
+// ----------------------------------------------------------------------------
+// Flat optimizers (optim.hip)
+// ----------------------------------------------------------------------------
+// lr = lr_ptr ? lr_ptr[lr_index_ptr ? (*lr_index_ptr - 1) : 0] : h.lr
+// t  = step_ptr ? *step_ptr : t_host           (1-based step count)
+void launch_flat_optim(float* p, const float* g, float* s1, float* s2, int64_t n, const OptHyper& h,
+                       const float* lr_ptr, const int64_t* lr_index_ptr, const int64_t* step_ptr, float t_host,
+                       uint16_t* shadow_bf16, const float* coef_ptr, hipStream_t stream);
+void launch_sq_norm(const float* x, int64_t n, float* out, hipStream_t stream);
+void launch_clip_coef(const float* sq, float max_norm, float* coef, float* total_norm, hipStream_t stream);
+void launch_cast_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// LeNet-5 (reference src/model.py:7-24) fused forward/backward (lenet.hip)
+// ----------------------------------------------------------------------------
+enum LeNetCfg : int { LENET_DEFAULT = 0, LENET_TINY = 1 };
+enum LeNetMode : int {
+  LENET_FWD = 1,        // conv1 -> logits
+  LENET_CE = 2,         // softmax-CE loss + dlogits + loss/accuracy accumulation
+  LENET_BWD = 4,        // dlogits -> all parameter gradients
+  LENET_OPT = 8,        // fused optimizer update inside the weight-gradient kernel (single process only)
+  LENET_REDUCE = 16,    // (kept for API compatibility: the conv1 reduction always happens inside K5)
+};
+
+struct LeNetPtrs {
+  const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4, *w5, *b5;  // params (fp32)
+  float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3, *gw4, *gb4, *gw5, *gb5;  // grads (fp32)
+  float *x, *p1, *p2, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dflat, *g1, *slab1;
+  uint8_t *i1, *i2;
+  int64_t* targets;          // [B] class ids (written by conv1 in the augment path)
+  const int64_t* dtargets;   // dataset targets [N] (augment path)
+  double* stats;             // [2]: sum over batches of batch-mean loss, of batch accuracy
+  unsigned* counters;        // [>= C1+1] zero-initialised arrival counters (K5 last-arriver reductions)
+};
+
+struct LeNetAug {
+  const uint8_t* data;  // [N,32,32,3] HWC uint8; nullptr -> ptrs.x is the (normalised) input
+  const int32_t* perm;  // epoch sample order
+  int64_t* ctrl;        // ctrl[0]: global step (1-based after the step), ctrl[1]: step in epoch
+  int64_t n;            // dataset rows
+  int64_t perm_len;
+  uint64_t seed;
+  int pad;              // RandomCrop padding (0 = no crop)
+  int flip;             // RandomHorizontalFlip(p=0.5)
+  int batch_stride;     // samples per step (offset into perm = ctrl[1]*batch_stride)
+  float mean[3], std[3];
+};
+
+struct LeNetOpt {
+  float *p, *g, *s1, *s2;  // whole flat buffers (params / grads / state)
+  int64_t n;
+  OptHyper h;
+  const float* lr_ptr;     // device lr (table indexed by ctrl[1]-1 when lr_table)
+  int lr_table;
+  // flat-buffer offsets of the 10 LeNet tensors (w1,b1,w2,b2,w3,b3,w4,b4,w5,b5)
+  int64_t off[10];
+};
+
+void launch_lenet(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                  hipStream_t stream);
+
+// Standalone GPU augmentation (RandomCrop(32,pad) + HFlip + ToTensor + Normalize) for the
+// generic (non-LeNet) device data path: out [B,3,32,32] fp32.
+void launch_cifar_augment(const LeNetAug& A, int B, float* out, int64_t* targets_out, const int64_t* dtargets,
+                          hipStream_t stream);
+
+}  // namespace mlt

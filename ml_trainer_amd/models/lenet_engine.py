@@ -1,0 +1,208 @@
+"""Fused LeNet training-step engine (the Trainer's and bench.py's fast path).
+
+One training step of the reference hot loop (``src/trainer.py:180-197``:
+zero_grad -> H2D -> forward -> CE -> loss.item() -> backward (DDP all-reduce)
+-> optimizer.step -> metric) becomes:
+
+* W = 1: six kernels ``K1..K6`` (csrc/kernels/lenet.hip) -- augmentation of an
+  HBM-resident uint8 dataset, forward, softmax-CE + on-device loss/accuracy
+  accumulation, backward and the fused optimizer update -- captured as a
+  multi-step hipGraph, so the host submits one graph per ``steps_per_graph``
+  steps and never synchronises inside an epoch (B12: no ``loss.item()``, no
+  sklearn host round trip per batch);
+* W > 1: graph(K1..K5 + conv1 partial reduce) -> RCCL all-reduce (AVG) of the
+  flat gradient buffer (one 248 KB bucket; latency-bound, so a single
+  collective) -> fused flat optimizer launch that reads lr/step from device
+  memory.
+
+The device step counter ``ctrl`` (``[global_step, step_in_epoch]``) drives
+batch selection from the epoch permutation, the augmentation RNG, the lr table
+and Adam's bias correction, so every replay of a captured graph is a new step.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from ml_trainer_amd.models.lenet import MLModel, lenet_buffers, _param_names
+from ml_trainer_amd.ops._ext import require_native
+from ml_trainer_amd.utils.flat import FlatParams
+
+CIFAR_MEAN = (0.4914, 0.4822, 0.4465)
+CIFAR_STD = (0.2023, 0.1994, 0.2010)
+
+
+class LeNetStepEngine:
+    def __init__(self, model: MLModel, flat: FlatParams, max_batch: int, optimizer=None, process_group=None,
+                 world_size: int = 1, seed: int = 0):
+        C = require_native()
+        self.C = C
+        self.model = model
+        self.flat = flat
+        self.max_batch = int(max_batch)
+        self.device = flat.device
+        self.world_size = int(world_size)
+        self.pg = process_group
+        self.seed = int(seed)
+        params = model.param_list()
+        for p in params:
+            if id(p) not in flat._index:
+                raise ValueError("model parameters must live in the flat buffer")
+        bufs = lenet_buffers(model.cfg_id, self.max_batch, self.device)
+        for name, p in zip(_param_names(), params):
+            o, n = flat.segment(p)
+            bufs[name] = flat.data[o:o + n]
+            bufs["g" + name] = flat.grad[o:o + n]
+        self.bufs = bufs
+        self.stats = bufs["stats"]
+        self.ctrl = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.eng = C.LeNetEngine(model.cfg_id, self.max_batch, bufs)
+        self.eng.set_ctrl(self.ctrl)
+        self.offsets = [flat.segment(p)[0] for p in params]
+        self.optimizer = None
+        self.lr_table: Optional[torch.Tensor] = None
+        self._use_table = False
+        self.data = None
+        self.perm: Optional[torch.Tensor] = None
+        if optimizer is not None:
+            self.set_optimizer(optimizer)
+
+    # ------------------------------------------------------------------ setup
+    def set_optimizer(self, optimizer, lr_table_len: int = 0) -> None:
+        self.optimizer = optimizer
+        s1, s2 = optimizer.state_buffers(0)
+        h = optimizer.hyper(0)
+        lr_t = optimizer.lr_tensor(0)
+        self._use_table = lr_table_len > 0
+        if self._use_table:
+            if self.lr_table is None or self.lr_table.numel() < lr_table_len:
+                self.lr_table = torch.zeros(lr_table_len, dtype=torch.float32, device=self.device)
+            lr_t = self.lr_table
+        self._lr_arg = lr_t
+        self._hyper = h
+        self.eng.set_opt(self.flat.data, self.flat.grad, s1, s2, h["kind"], h["lr"], h["momentum"], h["dampening"],
+                         h["weight_decay"], h["beta1"], h["beta2"], h["eps"], h["lr_decay"], h["grad_scale"],
+                         h["nesterov"], h["maximize"], lr_t, self._use_table, self.offsets)
+
+    def set_dataset(self, data_u8: torch.Tensor, targets: torch.Tensor, batch_size: int, augment: bool = True,
+                    pad: int = 4, flip: bool = True, mean: Sequence[float] = CIFAR_MEAN,
+                    std: Sequence[float] = CIFAR_STD, perm_capacity: Optional[int] = None) -> None:
+        """Make an HBM-resident uint8 dataset [N,32,32,3] the engine's input."""
+        if data_u8.dtype != torch.uint8 or tuple(data_u8.shape[1:]) != (32, 32, 3):
+            raise ValueError("expected uint8 [N,32,32,3] data")
+        self.data = data_u8.to(self.device).contiguous()
+        self.targets = targets.to(self.device, torch.int64).contiguous()
+        cap = int(perm_capacity or self.data.shape[0])
+        self.perm = torch.zeros(max(cap, 1), dtype=torch.int32, device=self.device)
+        self.batch_size = int(batch_size)
+        self.eng.set_aug(self.data, self.perm, self.ctrl, self.targets, self.seed, pad if augment else 0,
+                         1 if (augment and flip) else 0, self.batch_size, list(mean), list(std))
+
+    def start_epoch(self, indices: torch.Tensor, lr_values: Optional[Sequence[float]] = None) -> None:
+        """Upload this epoch's sample order (and per-step lrs) and reset the in-epoch counter."""
+        n = indices.numel()
+        if n > self.perm.numel():
+            raise ValueError("epoch permutation larger than perm capacity")
+        self.perm[:n].copy_(indices.to(torch.int32), non_blocking=True)
+        self.ctrl[1:2].zero_()
+        if lr_values is not None:
+            if not self._use_table:
+                raise RuntimeError("engine not configured with an lr table")
+            vals = torch.tensor(list(lr_values), dtype=torch.float32)
+            self.lr_table[:vals.numel()].copy_(vals, non_blocking=False)
+        elif self.optimizer is not None:
+            self.optimizer.lr_tensor(0)  # sync group lr -> device scalar
+
+    def reset_stats(self) -> None:
+        self.stats.zero_()
+
+    def read_stats(self, n_batches: int):
+        s = self.stats.cpu().tolist()
+        return s[0] / max(n_batches, 1), s[1] / max(n_batches, 1)
+
+    # ------------------------------------------------------------------ steps
+    @property
+    def fused(self) -> bool:
+        return self.world_size == 1
+
+    def _train_mode(self) -> int:
+        C = self.C
+        base = C.LENET_FWD | C.LENET_CE | C.LENET_BWD
+        return base | (C.LENET_OPT if self.fused else 0)
+
+    def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8) -> None:
+        """Run ``n`` full training steps of batch ``B`` from the device dataset."""
+        mode = self._train_mode()
+        if self.fused:
+            if not use_graph:
+                for _ in range(n):
+                    self.eng.run(mode, B)
+                return
+            k = max(1, min(steps_per_graph, n))
+            full, rem = divmod(n, k)
+            if full and not self.eng.has_graph(mode, B, k):
+                self.eng.capture(mode, B, k)
+            for _ in range(full):
+                self.eng.replay(mode, B, k)
+            if rem:
+                if not self.eng.has_graph(mode, B, rem):
+                    self.eng.capture(mode, B, rem)
+                self.eng.replay(mode, B, rem)
+            return
+        for _ in range(n):
+            self._dist_step(mode, B, use_graph)
+
+    def _dist_step(self, mode: int, B: int, use_graph: bool) -> None:
+        import torch.distributed as dist
+        if use_graph:
+            if not self.eng.has_graph(mode, B, 1):
+                self.eng.capture(mode, B, 1)
+            self.eng.replay(mode, B, 1)
+        else:
+            self.eng.run(mode, B)
+        g = self.flat.grad
+        if self.pg is not None or dist.is_initialized():
+            if dist.get_backend(self.pg) == "nccl":
+                dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.pg)
+            else:
+                dist.all_reduce(g, group=self.pg)
+                g.mul_(1.0 / self.world_size)
+        h = self._hyper
+        s1, s2 = self.optimizer.state_buffers(0)
+        self.C.flat_optim(self.flat.data, g, s1, s2, h["kind"], h["lr"], h["momentum"], h["dampening"],
+                          h["weight_decay"], h["beta1"], h["beta2"], h["eps"], h["lr_decay"], h["grad_scale"],
+                          h["nesterov"], h["maximize"], self._lr_arg, self.ctrl[1:2] if self._use_table else None,
+                          self.ctrl[0:1], 1.0, None, None)
+
+    def eval_steps(self, B: int, n: int = 1) -> None:
+        """Forward + CE + accuracy only (validation / test)."""
+        C = self.C
+        for _ in range(n):
+            self.eng.run(C.LENET_FWD | C.LENET_CE, B)
+            self._advance_eval()
+
+    def _advance_eval(self) -> None:
+        # eval kernels do not touch the counters (no K5); advance the in-epoch index here
+        self.ctrl[1:2].add_(1)
+
+    def step_from_tensors(self, x: torch.Tensor, y: torch.Tensor, train: bool = True) -> None:
+        """One step from a host/device batch (generic datasets): x [B,3,32,32], y [B]."""
+        C = self.C
+        B = x.shape[0]
+        if B > self.max_batch:
+            raise ValueError("batch larger than engine max_batch")
+        self.bufs["x"][:B * 3072].copy_(x.reshape(-1), non_blocking=True)
+        self.bufs["targets"][:B].copy_(y.reshape(-1), non_blocking=True)
+        if self.data is not None:
+            self.eng.clear_aug()
+            self.data = None
+        if train:
+            mode = self._train_mode()
+            if self.fused:
+                self.eng.run(mode, B)
+            else:
+                self._dist_step(mode, B, use_graph=False)
+        else:
+            self.eng.run(C.LENET_FWD | C.LENET_CE, B)

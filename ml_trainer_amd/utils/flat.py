@@ -1,0 +1,100 @@
+"""Contiguous flat parameter / gradient storage.
+
+Every trainable parameter of a model becomes a *view* into one fp32 buffer and
+its ``.grad`` a view into a matching gradient buffer. Consequences:
+
+* an optimizer step is one fused HIP launch over the whole buffer
+  (``ops/optim.py``) instead of ~3 launches per tensor (reference SGD step:
+  ``mul_`` x10 + ``add_`` x20, SURVEY.md App. A census);
+* DDP buckets are contiguous slices of the gradient buffer, so the all-reduce
+  needs no copy-in/copy-out (``parallel/ddp.py``);
+* checkpointing the state is a single D2H copy.
+
+Segments start at multiples of ``align`` elements (16 B for fp32) so kernels
+can use float4 accesses on any parameter.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import torch
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+class FlatParams:
+    def __init__(self, params: Iterable[torch.nn.Parameter], device: Optional[torch.device] = None,
+                 align: int = 4, reverse: bool = False, dtype: torch.dtype = torch.float32):
+        ps = [p for p in params if p.requires_grad]
+        if reverse:
+            ps = ps[::-1]
+        self.params: List[torch.nn.Parameter] = ps
+        dev = device or (ps[0].device if ps else torch.device("cpu"))
+        self.device = torch.device(dev)
+        self.offsets: List[int] = []
+        off = 0
+        for p in ps:
+            self.offsets.append(off)
+            off += _round_up(p.numel(), align)
+        self.numel = max(_round_up(off, align), align)
+        self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self._index: Dict[int, int] = {}
+        with torch.no_grad():
+            for i, (p, o) in enumerate(zip(ps, self.offsets)):
+                n = p.numel()
+                self.data[o:o + n].copy_(p.detach().reshape(-1).to(self.device, dtype))
+                p.data = self.data[o:o + n].view_as(p)
+                p.grad = self.grad[o:o + n].view_as(p)
+                self._index[id(p)] = i
+
+    # ------------------------------------------------------------------
+    def segment(self, p: torch.nn.Parameter) -> Tuple[int, int]:
+        i = self._index[id(p)]
+        return self.offsets[i], self.params[i].numel()
+
+    def grad_view(self, i: int) -> torch.Tensor:
+        p, o = self.params[i], self.offsets[i]
+        return self.grad[o:o + p.numel()].view_as(p)
+
+    def rebind_grads(self) -> None:
+        """Re-attach ``p.grad`` to the flat buffer if user code replaced it
+        (e.g. ``module.zero_grad(set_to_none=True)``)."""
+        gp = self.grad.data_ptr()
+        for i, p in enumerate(self.params):
+            g = p.grad
+            o = self.offsets[i]
+            if g is not None and g.data_ptr() == gp + o * self.grad.element_size():
+                continue
+            view = self.grad_view(i)
+            with torch.no_grad():
+                if g is None:
+                    view.zero_()
+                else:
+                    view.copy_(g)
+            p.grad = view
+
+    def rebind_params(self) -> bool:
+        """Re-attach ``p.data`` views if something (e.g. ``module.to()``) replaced
+        them; copies the current values back in. Returns True when anything moved."""
+        moved = False
+        dp = self.data.data_ptr()
+        for i, p in enumerate(self.params):
+            o = self.offsets[i]
+            if p.data.data_ptr() == dp + o * self.data.element_size() and p.device == self.device:
+                continue
+            with torch.no_grad():
+                self.data[o:o + p.numel()].copy_(p.detach().reshape(-1).to(self.device, self.data.dtype))
+            p.data = self.data[o:o + p.numel()].view_as(p)
+            moved = True
+        if moved:
+            self.rebind_grads()
+        return moved
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def state_dict_views(self) -> List[torch.Tensor]:
+        return [self.data[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
