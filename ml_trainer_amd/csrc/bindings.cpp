@@ -170,14 +170,67 @@ static LeNetAug make_aug(const Tensor& data, const Tensor& perm, c10::optional<T
 
 void cifar_augment(Tensor data, Tensor perm, c10::optional<Tensor> ctrl, Tensor dtargets, Tensor out,
                    Tensor targets_out, int64_t seed, int pad, int flip, int batch_stride, std::vector<double> mean,
-                   std::vector<double> stdv, int B) {
+                   std::vector<double> stdv, int B, int64_t step_host, int64_t sie_host) {
   LeNetAug A = make_aug(data, perm, ctrl, seed, pad, flip, batch_stride, mean, stdv);
+  A.step_host = step_host;
+  A.sie_host = sie_host;
   TORCH_CHECK(B > 0, "B must be positive");
   check_dev(out, "out", at::kFloat, (int64_t)B * 3072);
   check_dev(targets_out, "targets_out", at::kLong, B);
   check_dev(dtargets, "dtargets", at::kLong, A.n);
   launch_cifar_augment(A, B, out.data_ptr<float>(), targets_out.data_ptr<int64_t>(), dtargets.data_ptr<int64_t>(),
                        cur_stream());
+}
+
+// ----------------------------------------------------------------------------
+// Losses / metrics
+// ----------------------------------------------------------------------------
+static bool logits_bf16(const Tensor& z) {
+  TORCH_CHECK(z.scalar_type() == at::kFloat || z.scalar_type() == at::kBFloat16, "logits must be fp32 or bf16");
+  return z.scalar_type() == at::kBFloat16;
+}
+
+void ce_fwd(Tensor logits, Tensor tgt, Tensor dl, Tensor acc, c10::optional<Tensor> correct, Tensor loss,
+            int64_t ignore_index, double label_smoothing) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [B, C]");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  const bool bf = logits_bf16(logits);
+  check_dev(logits, "logits", logits.scalar_type(), B * C, 2);
+  check_dev(tgt, "targets", at::kLong, B, 8);
+  TORCH_CHECK(tgt.numel() == B, "targets must have B entries");
+  check_dev(dl, "dl", at::kFloat, B * C, 4);
+  check_dev(acc, "acc", at::kFloat, 2, 4);
+  check_dev(loss, "loss", at::kFloat, 1, 4);
+  float* cp = nullptr;
+  if (correct.has_value()) {
+    check_dev(*correct, "correct", at::kFloat, 1, 4);
+    cp = correct->data_ptr<float>();
+  }
+  launch_ce_fwd(logits.data_ptr(), bf, tgt.data_ptr<int64_t>(), B, (int)C, dl.data_ptr<float>(),
+                acc.data_ptr<float>(), cp, loss.data_ptr<float>(), ignore_index, (float)label_smoothing,
+                cur_stream());
+}
+
+void ce_bwd(Tensor dl, Tensor gout, Tensor acc, Tensor out) {
+  check_dev(dl, "dl", at::kFloat, dl.numel(), 4);
+  check_dev(gout, "grad_out", at::kFloat, 1, 4);
+  check_dev(acc, "acc", at::kFloat, 2, 4);
+  TORCH_CHECK(out.numel() == dl.numel(), "out size");
+  const bool bf = logits_bf16(out);
+  check_dev(out, "out", out.scalar_type(), dl.numel(), 2);
+  launch_ce_bwd(dl.data_ptr<float>(), gout.data_ptr<float>(), acc.data_ptr<float>(), dl.numel(), out.data_ptr(),
+                bf, cur_stream());
+}
+
+void accuracy(Tensor logits, Tensor tgt, Tensor out) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [B, C]");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  const bool bf = logits_bf16(logits);
+  check_dev(logits, "logits", logits.scalar_type(), B * C, 2);
+  check_dev(tgt, "targets", at::kLong, B, 8);
+  TORCH_CHECK(tgt.numel() == B, "targets must have B entries");
+  check_dev(out, "out", at::kFloat, 1, 4);
+  launch_accuracy(logits.data_ptr(), bf, tgt.data_ptr<int64_t>(), B, (int)C, out.data_ptr<float>(), cur_stream());
 }
 
 // ----------------------------------------------------------------------------
@@ -382,6 +435,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_coef", &clip_coef);
   m.def("cast_bf16", &cast_bf16);
   m.def("cifar_augment", &cifar_augment);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("accuracy", &accuracy);
   py::class_<LeNetEngine>(m, "LeNetEngine")
       .def(py::init<int, int, py::dict>())
       .def("set_aug", &LeNetEngine::set_aug)

@@ -45,6 +45,7 @@ struct LeNetPtrs {
 
 struct LeNetAug {
   const uint8_t* data;  // [N,32,32,3] HWC uint8; nullptr -> ptrs.x is the (normalised) input
+  int64_t step_host, sie_host;  // used instead of ctrl[0], ctrl[1] when ctrl == nullptr
   const int32_t* perm;  // epoch sample order
   int64_t* ctrl;        // ctrl[0]: global step (1-based after the step), ctrl[1]: step in epoch
   int64_t n;            // dataset rows
@@ -73,5 +74,16 @@ void launch_lenet(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& 
 // generic (non-LeNet) device data path: out [B,3,32,32] fp32.
 void launch_cifar_augment(const LeNetAug& A, int B, float* out, int64_t* targets_out, const int64_t* dtargets,
                           hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// Losses / metrics (losses.hip)
+// ----------------------------------------------------------------------------
+// acc[2] (zeroed by caller): {sum of row losses, number of valid rows}; loss[0] = mean.
+void launch_ce_fwd(const void* logits, bool bf16, const int64_t* tgt, int64_t B, int C, float* dl, float* acc,
+                   float* correct, float* loss, int64_t ignore_index, float label_smoothing, hipStream_t st);
+void launch_ce_bwd(const float* dl, const float* gout, const float* acc, int64_t n, void* out, bool bf16,
+                   hipStream_t st);
+void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t B, int C, float* out,
+                     hipStream_t st);
 
 }  // namespace mlt

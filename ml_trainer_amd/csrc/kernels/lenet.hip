@@ -796,7 +796,7 @@ __global__ __launch_bounds__(256) void cifar_augment_kernel(LeNetAug aug, float*
                                                             int64_t* __restrict__ targets_out,
                                                             const int64_t* __restrict__ dtargets) {
   const int b = blockIdx.x, t = threadIdx.x;
-  const int64_t step = aug.ctrl ? aug.ctrl[0] : 0, sie = aug.ctrl ? aug.ctrl[1] : 0;
+  const int64_t step = aug.ctrl ? aug.ctrl[0] : aug.step_host, sie = aug.ctrl ? aug.ctrl[1] : aug.sie_host;
   int64_t pos = sie * aug.batch_stride + b;
   if (pos >= aug.perm_len) pos %= aug.perm_len;
   int64_t idx = aug.perm[pos];

@@ -34,7 +34,10 @@ class FusedOptimizer(torch.optim.Optimizer):
         self._flats: List[FlatParams] = []
         for gi, group in enumerate(self.param_groups):
             ps = group["params"]
-            if flat is not None and len(self.param_groups) == 1 and [id(p) for p in flat.params] == [id(p) for p in ps]:
+            # reuse the caller's flat buffer (e.g. DDP's, laid out in reverse order) when it holds
+            # exactly this group's parameters: the update runs over the whole buffer, order is irrelevant
+            if flat is not None and len(self.param_groups) == 1 and \
+                    sorted(id(p) for p in flat.params) == sorted(id(p) for p in ps if p.requires_grad):
                 fp = flat
             else:
                 fp = FlatParams(ps)
@@ -246,3 +249,21 @@ def build_optimizer(name: str, params, lr: float, momentum: float = 0.9, weight_
     if name in OPTIMIZERS:
         return OPTIMIZERS[name](params, lr=lr, weight_decay=weight_decay, flat=flat)
     return None
+
+
+def clip_grad_norm_flat(flat: FlatParams, max_norm: float) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ over a flat gradient buffer: one fused
+    sum-of-squares kernel + one scale, no host sync (returns the device norm)."""
+    g = flat.grad
+    if g.is_cuda:
+        C = require_native()
+        sq = torch.zeros(1, dtype=torch.float32, device=g.device)
+        coef = torch.empty(1, dtype=torch.float32, device=g.device)
+        total = torch.empty(1, dtype=torch.float32, device=g.device)
+        C.sq_norm(g, sq)
+        C.clip_coef(sq, float(max_norm), coef, total)
+        g.mul_(coef)
+        return total.view(())
+    total = g.norm()
+    g.mul_(torch.clamp(max_norm / (total + 1e-6), max=1.0))
+    return total

@@ -1,0 +1,117 @@
+"""Native DDP over gloo with world_size 2 on CPU (fake cluster: spawned processes)."""
+import copy
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import TensorCifar, dist_env, free_port
+
+
+def _ddp_worker(rank, world, port, mode, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(1234 + rank)  # different init per rank: broadcast must fix it
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.0005, first_bucket_mb=0.0002, mode=mode)
+    assert len(ddp.bucket_sizes_bytes) >= 2
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(world * 6, 8, generator=g)
+    y = torch.randn(world * 6, 4, generator=g)
+    xs, ys = x[rank * 6:(rank + 1) * 6], y[rank * 6:(rank + 1) * 6]
+    loss = ((ddp(xs) - ys) ** 2).mean()
+    loss.backward()
+    ddp.after_backward()
+    grads = ddp.flat.grad.clone()
+    torch.save({"grads": grads, "params": ddp.flat.data.clone()}, os.path.join(out_dir, f"r{rank}.pt"))
+    # no_sync: local grads only
+    ddp.flat.zero_grad()
+    with ddp.no_sync():
+        ((ddp(xs) - ys) ** 2).mean().backward()
+    torch.save({"nosync": ddp.flat.grad.clone()}, os.path.join(out_dir, f"ns{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["overlap", "manual"])
+def test_ddp_grads_equal_full_batch(mode):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ddp_worker, args=(world, free_port(), mode, d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(world)]
+        assert torch.equal(r[0]["params"], r[1]["params"])  # broadcast from rank 0
+        assert torch.allclose(r[0]["grads"], r[1]["grads"])
+        # reference: full-batch gradient on one process with rank 0's params
+        from ml_trainer_amd.utils.flat import FlatParams
+        torch.manual_seed(1234)
+        model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+        fp = FlatParams(model.parameters(), reverse=True)
+        assert torch.equal(fp.data, r[0]["params"])
+        g = torch.Generator().manual_seed(7)
+        x = torch.randn(world * 6, 8, generator=g)
+        y = torch.randn(world * 6, 4, generator=g)
+        # mean of per-rank means == full mean (equal shard sizes)
+        ((model(x) - y) ** 2).mean().backward()
+        torch.testing.assert_close(r[0]["grads"], fp.grad, rtol=1e-5, atol=1e-6)
+        ns = [torch.load(os.path.join(d, f"ns{i}.pt"), weights_only=True)["nosync"] for i in range(world)]
+        assert not torch.allclose(ns[0], ns[1])
+
+
+def _trainer_worker(rank, world, port, out_dir, per_device):
+    dist_env(rank, world, port)
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.trainer import Trainer
+    torch.manual_seed(0)
+    tr, va = TensorCifar(96, 0), TensorCifar(32, 1)
+    t = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=2, batch_size=32, is_parallel=True, save_history=True,
+                backend="gloo", model_dir=out_dir, lr=0.02,
+                options={"progress": False, "per_device_batch": per_device, "determinism_check": True})
+    assert t.world_size == world and t.batch_size == (32 if per_device else 16)
+    t.fit()
+    torch.save({"params": t.flat.data.clone(), "losses": t.train_losses},
+               os.path.join(out_dir, f"t{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("per_device", [False, True])
+def test_trainer_gloo_world2(per_device):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_trainer_worker, args=(world, free_port(), d, per_device), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"t{i}.pt"), weights_only=True) for i in range(world)]
+        assert torch.equal(r[0]["params"], r[1]["params"])  # replicas stay identical
+        sd = torch.load(os.path.join(d, "model.pth"), weights_only=True)
+        assert all(k.startswith("module.") for k in sd)  # DDP checkpoint keys (reference B4)
+        assert os.path.exists(os.path.join(d, "history.pkl"))
+
+
+def _fault_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.trainer import Trainer
+    tr, va = TensorCifar(256, 0), TensorCifar(32, 1)
+    t = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=1, batch_size=16, is_parallel=True, backend="gloo",
+                model_dir=out_dir, options={"progress": False, "fault_inject_step": 3, "fault_inject_rank": 1,
+                                            "dist_timeout_s": 20})
+    try:
+        t.fit()
+        status = "completed"
+    except Exception as e:  # noqa: BLE001
+        status = f"error: {type(e).__name__}"
+    with open(os.path.join(out_dir, f"s{rank}.txt"), "w") as f:
+        f.write(status)
+
+
+def test_fault_injection_surfaces_on_all_ranks():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_fault_worker, args=(world, free_port(), d), nprocs=world, join=False,
+                                 start_method="spawn")
+        ctx.join(timeout=120) or None
+        while not ctx.join(timeout=120):
+            pass
+        s = [open(os.path.join(d, f"s{i}.txt")).read() for i in range(world)]
+        assert s[1].startswith("error") and "completed" not in s[0], s
