@@ -1,0 +1,52 @@
+"""bf16 GEMM throughput: native MFMA kernel vs torch.matmul (hipBLASLt) on BERT shapes.
+Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24), random operands."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ml_trainer_amd.ops._ext import require_native  # noqa: E402
+
+C = require_native()
+dev = torch.device("cuda", 0)
+T = 32 * 512  # tokens of BERT-base at batch 32, seq 512
+shapes = [  # (name, M, N, K, a_mn, b_mn)
+    ("qkv_fwd", T, 2304, 768, 0, 0), ("out_fwd", T, 768, 768, 0, 0), ("ffn1_fwd", T, 3072, 768, 0, 0),
+    ("ffn2_fwd", T, 768, 3072, 0, 0), ("ffn1_dgrad", T, 768, 3072, 0, 1), ("ffn1_wgrad", 3072, 768, T, 1, 1),
+    ("sq4096", 4096, 4096, 4096, 0, 0),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+res = []
+for name, M, N, K, a_mn, b_mn in shapes:
+    A = torch.randn((K, M) if a_mn else (M, K), device=dev).to(torch.bfloat16)
+    B = torch.randn((K, N) if b_mn else (N, K), device=dev).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    At = A.t() if a_mn else A
+    Bt = B if b_mn else B.t()
+    best = {"native": 1e9, "torch": 1e9}
+    for _ in range(3):
+        best["native"] = min(best["native"], timeit(lambda: C.gemm(A, B, out, bool(a_mn), bool(b_mn))))
+        best["torch"] = min(best["torch"], timeit(lambda: torch.matmul(At, Bt, out=out)))
+    fl = 2.0 * M * N * K
+    r = {"shape": name, "M": M, "N": N, "K": K, "native_ms": round(best["native"], 4),
+         "torch_ms": round(best["torch"], 4), "native_tflops": round(fl / best["native"] / 1e9, 1),
+         "torch_tflops": round(fl / best["torch"] / 1e9, 1)}
+    res.append(r)
+    print(json.dumps(r), flush=True)

@@ -234,6 +234,66 @@ void accuracy(Tensor logits, Tensor tgt, Tensor out) {
 }
 
 // ----------------------------------------------------------------------------
+// bf16 GEMM
+// ----------------------------------------------------------------------------
+static const uint16_t* bf16_ptr(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+
+// A, B, C are 2-D (row-major, unit column stride). a_mn / b_mn describe the storage:
+//   A: [M,K] (a_mn=0) or [K,M] (a_mn=1);  B: [N,K] (b_mn=0) or [K,N] (b_mn=1);  C: [M,N].
+void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tensor> bias, c10::optional<Tensor> aux,
+          c10::optional<Tensor> res, double alpha, int mode, bool accumulate) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm A/B must be bf16");
+  TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm C must be bf16 or fp32");
+  for (const Tensor* t : {&A, &B, &C}) {
+    TORCH_CHECK(t->is_cuda(), "gemm operands must be device tensors");
+    TORCH_CHECK(t->stride(1) == 1, "gemm operands need unit column stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm operands must be 16-byte aligned");
+  }
+  const int64_t M = a_mn ? A.size(1) : A.size(0), K = a_mn ? A.size(0) : A.size(1);
+  const int64_t N = b_mn ? B.size(1) : B.size(0), K2 = b_mn ? B.size(0) : B.size(1);
+  TORCH_CHECK(K == K2, "gemm inner dimensions differ: ", K, " vs ", K2);
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm C shape mismatch");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm leading dimensions must be multiples of 8");
+  // 16-byte chunks along the contiguous dimension of each operand
+  TORCH_CHECK((a_mn ? M : K) % 8 == 0 && (b_mn ? N : K) % 8 == 0, "contiguous gemm dims must be multiples of 8");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm dims too large");
+  const float* bp = nullptr;
+  const uint16_t* ap = nullptr;
+  const uint16_t* rp = nullptr;
+  int64_t ldaux = 0, ldres = 0;
+  if (bias.has_value()) {
+    check_dev(*bias, "bias", at::kFloat, N, 4);
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm mode");
+  if (mode != 0) {
+    TORCH_CHECK(aux.has_value(), "gemm GELU modes need aux");
+    TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
+                    aux->stride(1) == 1 && aux->is_cuda(), "aux must be bf16 [M,N]");
+    ap = bf16_ptr(*aux);
+    ldaux = aux->stride(0);
+  }
+  if (res.has_value()) {
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->dim() == 2 && res->size(0) == M && res->size(1) == N &&
+                    res->stride(1) == 1 && res->is_cuda(), "res must be bf16 [M,N]");
+    rp = bf16_ptr(*res);
+    ldres = res->stride(0);
+  }
+  TORCH_CHECK(!accumulate || C.scalar_type() == at::kFloat, "accumulate needs an fp32 output");
+  launch_gemm_bf16(a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M, (int)N,
+                   (int)K, A.stride(0), B.stride(0), C.stride(0), bp, ap, ldaux, rp, ldres, (float)alpha, mode,
+                   accumulate ? 1 : 0, cur_stream());
+}
+
+void colsum(Tensor X, Tensor out, bool accumulate) {
+  TORCH_CHECK(X.dim() == 2 && X.scalar_type() == at::kBFloat16 && X.stride(1) == 1 && X.is_cuda(), "colsum X");
+  check_dev(out, "out", at::kFloat, X.size(1), 4);
+  launch_colsum_bf16(bf16_ptr(X), (int)X.size(0), (int)X.size(1), X.stride(0), out.data_ptr<float>(),
+                     accumulate ? 1 : 0, cur_stream());
+}
+
+// ----------------------------------------------------------------------------
 // LeNet engine: holds every buffer pointer once, launches the fused step, and
 // captures multi-step hipGraphs.
 // ----------------------------------------------------------------------------
@@ -438,6 +498,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("accuracy", &accuracy);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("a_mn"), py::arg("b_mn"),
+        py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
+        py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false);
+  m.def("colsum", &colsum);
   py::class_<LeNetEngine>(m, "LeNetEngine")
       .def(py::init<int, int, py::dict>())
       .def("set_aug", &LeNetEngine::set_aug)

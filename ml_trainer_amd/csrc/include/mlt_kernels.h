@@ -86,4 +86,15 @@ void launch_ce_bwd(const float* dl, const float* gout, const float* acc, int64_t
 void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t B, int C, float* out,
                      hipStream_t st);
 
+// ----------------------------------------------------------------------------
+// bf16 MFMA GEMM (gemm.hip): C[M,N] = alpha * op(A) . op(B) (+bias) (+epilogue)
+//   a_mn: A stored [K][M] (else [M][K]);  b_mn: B stored [K][N] (else [N][K])
+//   mode: 0 none, 1 GELU (pre-activation written to aux), 2 dGELU (multiply by gelu'(aux))
+// ----------------------------------------------------------------------------
+void launch_gemm_bf16(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M, int N,
+                      int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias, const uint16_t* aux,
+                      int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate,
+                      hipStream_t st);
+void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, hipStream_t st);
+
 }  // namespace mlt

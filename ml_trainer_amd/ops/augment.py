@@ -14,13 +14,15 @@ from ml_trainer_amd.ops._ext import require_native
 
 
 class DeviceAugmentIterator:
-    def __init__(self, dd, indices: torch.Tensor, batch_size: int, seed: int = 0, step0: int = 0):
+    def __init__(self, dd, indices: torch.Tensor, batch_size: int, seed: int = 0, step0: int = 0,
+                 advance_step: bool = True):
         self.C = require_native()
         self.dd = dd
         self.idx = indices.to(torch.int32).to(dd.device)
         self.B = int(batch_size)
         self.seed = int(seed)
         self.step0 = int(step0)
+        self.advance = advance_step  # eval passes keep one RNG step per epoch (same as the engine's eval)
         self.n = self.idx.numel()
 
     def __len__(self):
@@ -34,5 +36,5 @@ class DeviceAugmentIterator:
             y = torch.empty(b, dtype=torch.int64, device=self.dd.device)
             self.C.cifar_augment(self.dd.data, self.idx, None, self.dd.targets, x, y, self.seed, s["pad"],
                                  1 if s["flip"] else 0, self.B, list(s["mean"]), list(s["std"]), b,
-                                 self.step0 + i, i)
+                                 self.step0 + (i if self.advance else 0), i)
             yield x, y

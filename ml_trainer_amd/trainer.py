@@ -447,8 +447,9 @@ class Trainer:
                 idx = torch.as_tensor(self.train_sampler.indices(), dtype=torch.int32)
             else:
                 idx = torch.randperm(len(loader.dataset)).to(torch.int32)
+            step0 = self.global_step if train else len(self.val_losses) * 1_000_003
             return DeviceAugmentIterator(dd, idx, self.batch_size, seed=self.seed + (0 if train else 1),
-                                         step0=self.global_step)
+                                         step0=step0, advance_step=train)
         if self.device.type == "cuda":
             return DevicePrefetcher(loader, self.device, depth=self.opts.prefetch_depth)
         return loader

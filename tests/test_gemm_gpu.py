@@ -1,0 +1,80 @@
+"""bf16 MFMA GEMM (csrc/kernels/gemm.hip) vs a plain torch fp32 reference of the same op."""
+import pytest
+import torch
+
+from ml_trainer_amd.ops._ext import require_native
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(shape, dev, g):
+    return (torch.randn(*shape, generator=g, device="cpu") * 0.5).to(torch.bfloat16).to(dev)
+
+
+def _ref(A, B, a_mn, b_mn):
+    a = A.float().t() if a_mn else A.float()
+    b = B.float() if b_mn else B.float().t()
+    return a @ b
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (136, 72, 40), (8, 8, 8), (520, 264, 1000)])
+@pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
+def test_gemm_layouts(dev, a_mn, b_mn, M, N, K, out):
+    C = require_native()
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = _mk((K, M) if a_mn else (M, K), dev, g)
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    Cm = torch.empty(M, N, dtype=out, device=dev)
+    C.gemm(A, B, Cm, bool(a_mn), bool(b_mn))
+    ref = _ref(A, B, a_mn, b_mn)
+    tol = 2e-2 if out == torch.bfloat16 else 2e-3
+    torch.testing.assert_close(Cm.float(), ref, rtol=tol, atol=tol * max(1.0, (K ** 0.5) * 0.25))
+
+
+def test_identity_asymmetric(dev):
+    """A = I with an asymmetric B catches any transposed C write (guide §3)."""
+    C = require_native()
+    M = 128
+    A = torch.eye(M, dtype=torch.bfloat16, device=dev)
+    B = (torch.arange(M * 64, device=dev).view(64, M) % 251).to(torch.bfloat16)  # B stored [N=64][K=128]
+    out = torch.empty(M, 64, dtype=torch.float32, device=dev)
+    C.gemm(A, B, out, False, False)
+    torch.testing.assert_close(out, B.float().t())
+
+
+def test_epilogues(dev):
+    C = require_native()
+    g = torch.Generator().manual_seed(0)
+    M, N, K = 256, 192, 128
+    A, B = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, device=dev)
+    res = _mk((M, N), dev, g)
+    ref = A.float() @ B.float().t()
+    # bias + residual + alpha
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, out, False, False, bias=bias, res=res, alpha=0.5)
+    torch.testing.assert_close(out.float(), 0.5 * ref + bias + res.float(), rtol=2e-2, atol=3e-2)
+    # GELU: pre-activation saved to aux
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, out, False, False, bias=bias, aux=aux, mode=1)
+    pre = ref + bias
+    torch.testing.assert_close(aux.float(), pre, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(out.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=3e-2)
+    # dGELU: result * gelu'(aux)
+    x = aux.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(torch.ones_like(x))
+    C.gemm(A, B, out, False, False, aux=aux, mode=2)
+    torch.testing.assert_close(out.float(), ref * x.grad, rtol=3e-2, atol=5e-2)
+    # fp32 accumulate
+    acc = torch.ones(M, N, device=dev)
+    C.gemm(A, B, acc, False, False, accumulate=True)
+    torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-3)
+
+
+def test_colsum(dev):
+    C = require_native()
+    X = torch.randn(1000, 300, device=dev).to(torch.bfloat16)
+    out = torch.zeros(300, device=dev)
+    C.colsum(X, out, False)
+    torch.testing.assert_close(out, X.float().sum(0), rtol=1e-4, atol=1e-3)

@@ -169,7 +169,7 @@ def test_augment_matches_cpu(dev):
     B = 16
     out = torch.empty(B * 3072, device=dev)
     tout = torch.empty(B, dtype=torch.int64, device=dev)
-    C.cifar_augment(data.to(dev), perm.to(dev), ctrl.to(dev), targets.to(dev), out, tout, 123, 4, 1, B, mean, std, B)
+    C.cifar_augment(data.to(dev), perm.to(dev), ctrl.to(dev), targets.to(dev), out, tout, 123, 4, 1, B, mean, std, B, 0, 0)
     ref = _cpu_augment(data, perm, 5, 1, B, 123, 4, True, mean, std)
     torch.testing.assert_close(out.view(B, 3, 32, 32).cpu(), ref, rtol=1e-5, atol=1e-5)
     assert tout.cpu().tolist() == [int(targets[int(perm[B + b])]) for b in range(B)]
