@@ -288,9 +288,142 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
 
 void colsum(Tensor X, Tensor out, bool accumulate) {
   TORCH_CHECK(X.dim() == 2 && X.scalar_type() == at::kBFloat16 && X.stride(1) == 1 && X.is_cuda(), "colsum X");
-  check_dev(out, "out", at::kFloat, X.size(1), 4);
-  launch_colsum_bf16(bf16_ptr(X), (int)X.size(0), (int)X.size(1), X.stride(0), out.data_ptr<float>(),
-                     accumulate ? 1 : 0, cur_stream());
+  TORCH_CHECK(X.size(1) % 8 == 0 && X.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0,
+              "colsum needs 16-byte aligned rows (columns and row stride multiples of 8)");
+  TORCH_CHECK(X.size(0) < (1LL << 31) && X.size(1) < (1LL << 31), "colsum dims too large");
+  check_dev(out, "out", at::kFloat, X.size(1), 16);
+  const int M = (int)X.size(0), N = (int)X.size(1);
+  Tensor ws = at::empty({std::max<int64_t>(colsum_ws_floats(M, N), 4)}, X.options().dtype(at::kFloat));
+  launch_colsum_bf16(bf16_ptr(X), M, N, X.stride(0), out.data_ptr<float>(), accumulate ? 1 : 0,
+                     ws.data_ptr<float>(), cur_stream());
+}
+
+// ----------------------------------------------------------------------------
+// LayerNorm / embeddings / attention
+// ----------------------------------------------------------------------------
+static void check_bf16_2d(const Tensor& t, const char* name, int64_t rows, int64_t cols) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16, name,
+              " must be a contiguous bf16 device tensor");
+  TORCH_CHECK(t.numel() == rows * cols, name, " has ", t.numel(), " elements, expected ", rows, "x", cols);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+void ln_fwd(Tensor X, Tensor gamma, Tensor beta, Tensor Y, Tensor mean, Tensor rstd, double eps) {
+  const int64_t D = gamma.numel(), rows = X.numel() / std::max<int64_t>(D, 1);
+  TORCH_CHECK(D % 256 == 0 && D >= 256 && D <= 1024, "LayerNorm width must be 256/512/768/1024");
+  check_bf16_2d(X, "X", rows, D);
+  check_bf16_2d(Y, "Y", rows, D);
+  check_dev(gamma, "gamma", at::kFloat, D);
+  check_dev(beta, "beta", at::kFloat, D);
+  check_dev(mean, "mean", at::kFloat, rows, 4);
+  check_dev(rstd, "rstd", at::kFloat, rows, 4);
+  launch_ln_fwd(bf16_ptr(X), gamma.data_ptr<float>(), beta.data_ptr<float>(), (uint16_t*)Y.data_ptr(),
+                mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)D, (float)eps, cur_stream());
+}
+
+int64_t ln_partial_blocks(int64_t rows) { return ln_bwd_partial_blocks(rows); }
+
+// dxsum (optional): column sums of DX (bias gradient of the producing linear layer), accumulated
+// into when dxsum_acc.
+void ln_bwd(Tensor DY, Tensor X, Tensor gamma, Tensor mean, Tensor rstd, Tensor DX, Tensor part, Tensor dgamma,
+            Tensor dbeta, bool accumulate, c10::optional<Tensor> dres, c10::optional<Tensor> dxsum,
+            bool dxsum_acc) {
+  const int64_t D = gamma.numel(), rows = X.numel() / std::max<int64_t>(D, 1);
+  TORCH_CHECK(D % 256 == 0 && D >= 256 && D <= 1024, "LayerNorm width must be 256/512/768/1024");
+  check_bf16_2d(X, "X", rows, D);
+  check_bf16_2d(DY, "DY", rows, D);
+  check_bf16_2d(DX, "DX", rows, D);
+  check_dev(gamma, "gamma", at::kFloat, D);
+  check_dev(mean, "mean", at::kFloat, rows, 4);
+  check_dev(rstd, "rstd", at::kFloat, rows, 4);
+  check_dev(part, "part", at::kFloat, (int64_t)ln_bwd_partial_blocks(rows) * (dxsum.has_value() ? 3 : 2) * D);
+  check_dev(dgamma, "dgamma", at::kFloat, D);
+  check_dev(dbeta, "dbeta", at::kFloat, D);
+  float* dxs = nullptr;
+  if (dxsum.has_value()) {
+    check_dev(*dxsum, "dxsum", at::kFloat, D);
+    dxs = dxsum->data_ptr<float>();
+  }
+  const uint16_t* dr = nullptr;
+  if (dres.has_value()) {
+    check_bf16_2d(*dres, "dres", rows, D);
+    dr = bf16_ptr(*dres);
+  }
+  launch_ln_bwd(bf16_ptr(DY), bf16_ptr(X), gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                (uint16_t*)DX.data_ptr(), part.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                rows, (int)D, accumulate ? 1 : 0, dr, dxs, dxsum_acc ? 1 : 0, cur_stream());
+}
+
+void embed_fwd(Tensor ids, c10::optional<Tensor> tt, Tensor Ww, Tensor Wp, Tensor Wt, Tensor out, int64_t S) {
+  const int64_t rows = ids.numel(), D = Ww.size(1);
+  TORCH_CHECK(D % 256 == 0 && D <= 1024, "embedding width must be a multiple of 256 (<= 1024)");
+  TORCH_CHECK(S > 0 && rows % S == 0 && S <= Wp.size(0), "sequence length vs position table");
+  check_dev(ids, "ids", at::kLong, rows, 8);
+  const int64_t* tp = nullptr;
+  if (tt.has_value()) {
+    check_dev(*tt, "token_type", at::kLong, rows, 8);
+    tp = tt->data_ptr<int64_t>();
+  }
+  check_bf16_2d(Ww, "word_emb", Ww.size(0), D);
+  check_bf16_2d(Wp, "pos_emb", Wp.size(0), D);
+  check_bf16_2d(Wt, "type_emb", Wt.size(0), D);
+  TORCH_CHECK(Wt.size(0) <= 2, "at most 2 token types");
+  check_bf16_2d(out, "out", rows, D);
+  launch_embed_fwd(ids.data_ptr<int64_t>(), tp, bf16_ptr(Ww), bf16_ptr(Wp), bf16_ptr(Wt), (uint16_t*)out.data_ptr(),
+                   rows, (int)S, (int)D, Ww.size(0), (int)Wt.size(0), cur_stream());
+}
+
+void embed_bwd(Tensor ids, c10::optional<Tensor> tt, Tensor DX, Tensor gw, Tensor gp, Tensor gt, Tensor part,
+               int64_t S) {
+  const int64_t rows = ids.numel(), D = gw.size(1);
+  TORCH_CHECK(D % 256 == 0 && D <= 1024, "embedding width");
+  TORCH_CHECK(S > 0 && rows % S == 0 && S <= gp.size(0), "sequence length vs position table");
+  check_dev(ids, "ids", at::kLong, rows, 8);
+  const int64_t* tp = nullptr;
+  if (tt.has_value()) {
+    check_dev(*tt, "token_type", at::kLong, rows, 8);
+    tp = tt->data_ptr<int64_t>();
+  }
+  check_bf16_2d(DX, "DX", rows, D);
+  check_dev(gw, "gw", at::kFloat, gw.size(0) * D);
+  check_dev(gp, "gp", at::kFloat, gp.size(0) * D);
+  check_dev(gt, "gt", at::kFloat, gt.size(0) * D);
+  TORCH_CHECK(gt.size(0) <= 2, "at most 2 token types");
+  check_dev(part, "part", at::kFloat, (int64_t)ln_bwd_partial_blocks(rows) * 2 * D);
+  launch_embed_bwd(ids.data_ptr<int64_t>(), tp, bf16_ptr(DX), gw.data_ptr<float>(), gp.data_ptr<float>(),
+                   gt.data_ptr<float>(), part.data_ptr<float>(), rows, (int)S, (int)D, gw.size(0), (int)gt.size(0),
+                   cur_stream());
+}
+
+static const int* lens_ptr(const c10::optional<Tensor>& lens, int64_t B) {
+  if (!lens.has_value()) return nullptr;
+  check_dev(*lens, "lens", at::kInt, B, 4);
+  return lens->data_ptr<int>();
+}
+
+void attn_fwd(Tensor qkv, Tensor out, Tensor lse, c10::optional<Tensor> lens, int64_t B, int64_t S, int64_t H,
+              double scale) {
+  const int64_t D = H * 64;
+  check_bf16_2d(qkv, "qkv", B * S, 3 * D);
+  check_bf16_2d(out, "out", B * S, D);
+  check_dev(lse, "lse", at::kFloat, B * H * S, 4);
+  TORCH_CHECK(B > 0 && S > 0 && H > 0 && B <= 65535 && H <= 65535, "attention dims");
+  launch_attn_fwd(bf16_ptr(qkv), (uint16_t*)out.data_ptr(), lse.data_ptr<float>(), lens_ptr(lens, B), (int)B, (int)S,
+                  (int)H, (float)scale, cur_stream());
+}
+
+void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10::optional<Tensor> lens, Tensor dqkv,
+              int64_t B, int64_t S, int64_t H, double scale) {
+  const int64_t D = H * 64;
+  check_bf16_2d(qkv, "qkv", B * S, 3 * D);
+  check_bf16_2d(out, "out", B * S, D);
+  check_bf16_2d(dout, "dout", B * S, D);
+  check_bf16_2d(dqkv, "dqkv", B * S, 3 * D);
+  check_dev(lse, "lse", at::kFloat, B * H * S, 4);
+  check_dev(delta, "delta", at::kFloat, B * H * S, 4);
+  TORCH_CHECK(B > 0 && S > 0 && H > 0 && B <= 65535 && H <= 65535, "attention dims");
+  launch_attn_bwd(bf16_ptr(qkv), bf16_ptr(out), bf16_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                  lens_ptr(lens, B), (uint16_t*)dqkv.data_ptr(), (int)B, (int)S, (int)H, (float)scale, cur_stream());
 }
 
 // ----------------------------------------------------------------------------
@@ -501,7 +634,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("a_mn"), py::arg("b_mn"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
         py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd, py::arg("DY"), py::arg("X"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("DX"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accumulate") = false,
+        py::arg("dres") = py::none(), py::arg("dxsum") = py::none(), py::arg("dxsum_acc") = false);
+  m.def("ln_partial_blocks", &ln_partial_blocks);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   py::class_<LeNetEngine>(m, "LeNetEngine")
       .def(py::init<int, int, py::dict>())
       .def("set_aug", &LeNetEngine::set_aug)

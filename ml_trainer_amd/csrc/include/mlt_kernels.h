@@ -95,6 +95,33 @@ void launch_gemm_bf16(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const
                       int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias, const uint16_t* aux,
                       int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate,
                       hipStream_t st);
-void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, hipStream_t st);
+int64_t colsum_ws_floats(int M, int N);
+void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,
+                        hipStream_t st);
+// out_k[c] (+)= sum_r part[r * ld + k * seg + c], c < W, k = 0..W/seg-1 (<= 3 segments; bit k of accmask =
+// accumulate into out_k); fixed-order (deterministic)
+struct SegOut {
+  float* p[3];
+};
+void launch_reduce_rows(const float* part, int R, int64_t ld, int W, int seg, SegOut outs, int accmask, hipStream_t st);
+
+// ----------------------------------------------------------------------------
+// LayerNorm / embeddings (layernorm.hip), attention (attention.hip)
+// ----------------------------------------------------------------------------
+void launch_ln_fwd(const uint16_t* X, const float* gamma, const float* beta, uint16_t* Y, float* mean, float* rstd,
+                   int64_t rows, int D, float eps, hipStream_t st);
+int ln_bwd_partial_blocks(int64_t rows);
+void launch_ln_bwd(const uint16_t* DY, const uint16_t* X, const float* gamma, const float* mean, const float* rstd,
+                   uint16_t* DX, float* part, float* dgamma, float* dbeta, int64_t rows, int D, int accumulate,
+                   const uint16_t* DRES, float* dxsum, int dxsum_acc, hipStream_t st);
+void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww, const uint16_t* Wp,
+                      const uint16_t* Wt, uint16_t* out, int64_t rows, int S, int D, int64_t vocab, int ntype,
+                      hipStream_t st);
+void launch_embed_bwd(const int64_t* ids, const int64_t* tt, const uint16_t* DX, float* gw, float* gp, float* gt,
+                      float* part, int64_t rows, int S, int D, int64_t vocab, int ntype, hipStream_t st);
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* lens, int B, int S, int H,
+                     float scale, hipStream_t st);
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st);
 
 }  // namespace mlt

@@ -1,0 +1,467 @@
+// Fused multi-head attention (flash-style) forward / backward for gfx950, bf16 MFMA.
+//
+// Layout: the QKV projection's output qkv [B*S, 3*H*64] is read in place (q | k | v
+// blocks of H heads x 64 dims per row); O [B*S, H*64]; the backward writes dQKV in the
+// same packed layout. Head dim 64, key-padding mask by per-sequence valid length.
+//
+// Forward, one 256-thread block per (64-query block, head, batch), wave = 16 queries:
+//   S^T (keys x queries) = K . Q^T   -- "swapped" product: each lane owns ONE query
+//   column, so the online-softmax max / sum is lane-local plus two xor-shuffles;
+//   O^T (dims x queries) += V^T . P^T -- P^T is the accumulator of S^T re-used as the
+//   MFMA B operand straight from registers (k order permuted identically on both
+//   operands, cdna_hip_programming.md §3), V^T comes from the V tile in LDS through the
+//   transpose read ds_read_b64_tr_b16. The S x S score matrix never touches HBM; the
+//   log-sum-exp per query is saved for the backward pass.
+// Backward = two kernels over the same (64-block, head, batch) grid, no atomics, bitwise
+// reproducible (>= B*H*S/64 workgroups, e.g. 1536 for BERT-base b16 s512):
+//   dK/dV: block = 64 keys, wave = 16 keys (keys on lanes): S = Q K^T, dP = dO V^T,
+//     P = exp2(S*scale*log2e - LSE2), dS = P (dP - delta); dV^T += dO^T P, dK^T += Q^T dS with
+//     accumulators in registers across the whole query loop;
+//   dQ: block = 64 queries, swapped like the forward (queries on lanes): S^T = K Q^T,
+//     dP^T = V dO^T, dS^T lane-local, dQ^T += K^T dS^T with dS^T fed from registers.
+// Global->LDS staging of the next tile is register-staged (loads issued before the MFMA work
+// of the current tile, LDS writes after it), so HBM latency overlaps the math.
+#include "mlt_common.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int AH = 64;  // head dim
+constexpr int AB = 64;  // query / key block
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// [64 rows][64 bf16] LDS tile, 128-byte rows, 16-byte chunks XOR-swizzled by (row & 7)
+__device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+// cooperative global -> LDS copy of a 64x64 bf16 tile (rows `row0..row0+63` of a row-major
+// matrix with row stride ld elements, starting at column col0); rows >= nrows are zero
+__device__ __forceinline__ void stage_tile(uint8_t* lds, const uint16_t* __restrict__ g, int64_t ld, int64_t row0,
+                                           int nrows_valid, int col0) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nrows_valid) v = *reinterpret_cast<const uint4*>(g + (row0 + r) * ld + col0 + c * 8);
+    *reinterpret_cast<uint4*>(lds + tile_off(r, c)) = v;
+  }
+}
+
+// register-staged variant: load_tile issues the global loads, store_tile writes them to LDS
+struct TileRegs {
+  uint4 v[2];
+};
+__device__ __forceinline__ void load_tile(TileRegs& t, const uint16_t* __restrict__ g, int64_t ld, int64_t row0,
+                                          int nrows_valid, int col0) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    t.v[i] = r < nrows_valid ? *reinterpret_cast<const uint4*>(g + (row0 + r) * ld + col0 + c * 8)
+                             : make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void store_tile(uint8_t* lds, const TileRegs& t) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    *reinterpret_cast<uint4*>(lds + tile_off(r, c)) = t.v[i];
+  }
+}
+
+// row fragment: 16 rows starting at `row`, k = 32*kh + 8*(lane>>4) + j (ds_read_b128)
+__device__ __forceinline__ bf16x8 frag_row(const uint8_t* lds, int row, int kh) {
+  const int lane = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(lds + tile_off(row + (lane & 15), kh * 4 + (lane >> 4)));
+}
+// transposed fragment: column (col + lane&15) of rows {r0+q} and {r1+q}, q = 0..3 (ds_read_b64_tr_b16)
+__device__ __forceinline__ bf16x8 frag_tr(const uint8_t* lds, int r0, int r1, int col) {
+  const int lane = threadIdx.x & 63, i = lane & 15, q = i >> 2, p = i & 3;
+  const int cc = col + 4 * p, chunk = cc >> 3, half = (cc & 7) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off(r0 + q, chunk) + half));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off(r1 + q, chunk) + half));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(f); }
+
+// pack an accumulator pair (tiles t0, t1 of 16 rows each) into a k-permuted B/A operand:
+// element j <-> row 16*(j>>2) + 4*(lane>>4) + (j&3) of the 32-row k-step
+__device__ __forceinline__ bf16x8 pack_acc(const f32x4& t0, const f32x4& t1) {
+  const s16x8 r = {bf16_bits(t0[0]), bf16_bits(t0[1]), bf16_bits(t0[2]), bf16_bits(t0[3]),
+                   bf16_bits(t1[0]), bf16_bits(t1[1]), bf16_bits(t1[2]), bf16_bits(t1[3])};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                       float* __restrict__ lse, const int* __restrict__ lens, int S,
+                                                       int H, float scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t Ks[2][AB * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[2][AB * 128];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  const int q = qb * AB + wid * 16 + i;  // this lane's query
+  // Q fragments (B operand of K.Q^T): Q[q][32kh + 8g + j]
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    qf[kh] = q < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q) * ld + h * AH + kh * 32 + 8 * g)
+                   : bf16x8{};
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const int nkb = (len + AB - 1) / AB;
+  const float sl2 = scale * 1.4426950408889634f;  // work in base 2
+  TileRegs kr, vr;
+  if (nkb > 0) {
+    stage_tile(Ks[0], qkv, ld, base, min(AB, S), D + h * AH);
+    stage_tile(Vs[0], qkv, ld, base, min(AB, S), 2 * D + h * AH);
+  }
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    const bool more = kb + 1 < nkb;
+    if (more) {  // issue the next K/V block's loads now, land them in LDS after this block's math
+      const int k1 = (kb + 1) * AB;
+      load_tile(kr, qkv, ld, base + k1, min(AB, S - k1), D + h * AH);
+      load_tile(vr, qkv, ld, base + k1, min(AB, S - k1), 2 * D + h * AH);
+    }
+    // S^T tiles: rows = keys kt*16 + 4g + r, column = this lane's query
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) s[kt] = mfma(frag_row(Ks[cur], kt * 16, kh), qf[kh], s[kt]);
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb * AB + kt * 16 + 4 * g + r;
+        const float v = key < len ? s[kt][r] * sl2 : -INFINITY;
+        s[kt][r] = v;
+        bm = fmaxf(bm, v);
+      }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = exp2f(m - mn);  // m = -inf on the first block -> 0
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[kt][r] - mn);
+        s[kt][r] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    // O^T += V^T . P^T over two 32-key k-steps
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pb = pack_acc(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8 va = frag_tr(Vs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+        o[d] = mfma(va, pb, o[d]);
+      }
+    }
+    if (more) {  // buffer cur^1 was last read before the previous barrier
+      store_tile(Ks[cur ^ 1], kr);
+      store_tile(Vs[cur ^ 1], vr);
+    }
+    __syncthreads();
+  }
+  if (q < S) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* op = out + (base + q) * (int64_t)D + h * AH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      ushort4 u;  // dims d*16 + 4g + r, r = 0..3
+      u.x = f32_to_bf16(o[d][0] * inv);
+      u.y = f32_to_bf16(o[d][1] * inv);
+      u.z = f32_to_bf16(o[d][2] * inv);
+      u.w = f32_to_bf16(o[d][3] * inv);
+      *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
+    }
+    if (g == 0) lse[((int64_t)b * H + h) * S + q] = m + __log2f(l);  // base-2 LSE of the scaled scores
+  }
+}
+
+// delta[b,h,q] = sum_d dO[q, h, d] * O[q, h, d]
+__global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restrict__ dout,
+                                                         const uint16_t* __restrict__ out, float* __restrict__ delta,
+                                                         int64_t rows, int H) {
+  const int64_t idx = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (row, h) pair, 16 lanes each
+  const int sub = threadIdx.x & 15;
+  const int64_t row = idx / H;
+  const int h = (int)(idx - row * H);
+  float s = 0.f;
+  if (row < rows) {
+    const int64_t off = row * (int64_t)H * AH + h * AH + sub * 4;
+    const ushort4 a = *reinterpret_cast<const ushort4*>(dout + off);
+    const ushort4 c = *reinterpret_cast<const ushort4*>(out + off);
+    s = bf16_to_f32(a.x) * bf16_to_f32(c.x) + bf16_to_f32(a.y) * bf16_to_f32(c.y) +
+        bf16_to_f32(a.z) * bf16_to_f32(c.z) + bf16_to_f32(a.w) * bf16_to_f32(c.w);
+  }
+  s = group_sum<16>(s);
+  if (sub == 0 && row < rows) {
+    // layout [B, H, S] like lse: row = b*S + q -> needs S; the host passes rows = B*S and
+    // we store by (row, h) then the backward indexes delta[row * H + h]
+    delta[row * H + h] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward, dK / dV: one block per (64-key block, head, batch)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
+                                                            const uint16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta,
+                                                            const int* __restrict__ lens, uint16_t* __restrict__ dqkv,
+                                                            int S, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t Qs[2][AB * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t Os[2][AB * 128];  // dO tiles
+  __shared__ float lse_s[2][AB], del_s[2][AB];
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  const int key = kb * AB + wid * 16 + i;  // this lane's key
+  if (kb * AB >= len) {  // fully masked key block: zero gradients
+    for (int e = threadIdx.x; e < AB * AH; e += 256) {
+      const int kk = kb * AB + e / AH, d = e % AH;
+      if (kk < S) {
+        dqkv[(base + kk) * ld + D + h * AH + d] = 0;
+        dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
+      }
+    }
+    return;
+  }
+  const float sl2 = scale * 1.4426950408889634f;
+  bf16x8 kf[2], vf[2];  // B operands: K[key][32kh + 8g + j], V[key][...]
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    kf[kh] = key < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key) * ld + D + h * AH + kh * 32 + 8 * g)
+                     : bf16x8{};
+    vf[kh] = key < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key) * ld + 2 * D + h * AH + kh * 32 + 8 * g)
+                     : bf16x8{};
+  }
+  f32x4 dk[4], dv[4];  // dK^T / dV^T [d = dt*16 + 4g + r][key = lane]
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nqb = (S + AB - 1) / AB;
+  auto stage_stats = [&](int buf, int q0) {
+    if (threadIdx.x < AB) {
+      const int qq = q0 + threadIdx.x;
+      lse_s[buf][threadIdx.x] = qq < S ? lse[((int64_t)b * H + h) * S + qq] : 0.f;
+      del_s[buf][threadIdx.x] = qq < S ? delta[(base + qq) * H + h] : 0.f;
+    }
+  };
+  stage_tile(Qs[0], qkv, ld, base, min(AB, S), h * AH);
+  stage_tile(Os[0], dout, (int64_t)D, base, min(AB, S), h * AH);
+  stage_stats(0, 0);
+  __syncthreads();
+  TileRegs qr, orr;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int cur = qb & 1, q0 = qb * AB;
+    const bool more = qb + 1 < nqb;
+    if (more) {
+      const int q1 = q0 + AB;
+      load_tile(qr, qkv, ld, base + q1, min(AB, S - q1), h * AH);
+      load_tile(orr, dout, (int64_t)D, base + q1, min(AB, S - q1), h * AH);
+    }
+    f32x4 p[4], ds[4];  // rows q = qt*16 + 4g + r, column = key (lane)
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        s = mfma(frag_row(Qs[cur], qt * 16, kh), kf[kh], s);
+        dp = mfma(frag_row(Os[cur], qt * 16, kh), vf[kh], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qt * 16 + 4 * g + r;
+        const bool ok = key < len && q0 + ql < S;
+        const float pv = ok ? exp2f(s[r] * sl2 - lse_s[cur][ql]) : 0.f;
+        p[qt][r] = pv;
+        ds[qt][r] = pv * (dp[r] - del_s[cur][ql]);
+      }
+    }
+    // dV^T += dO^T . P ; dK^T += Q^T . dS  (k = queries, two 32-query steps)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pb = pack_acc(p[2 * ks], p[2 * ks + 1]);
+      const bf16x8 sb = pack_acc(ds[2 * ks], ds[2 * ks + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        dv[d] = mfma(frag_tr(Os[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), pb, dv[d]);
+        dk[d] = mfma(frag_tr(Qs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), sb, dk[d]);
+      }
+    }
+    if (more) {
+      store_tile(Qs[cur ^ 1], qr);
+      store_tile(Os[cur ^ 1], orr);
+      stage_stats(cur ^ 1, q0 + AB);
+    }
+    __syncthreads();
+  }
+  if (key < S) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint16_t* kp = dqkv + (base + key) * ld + D + h * AH + d * 16 + 4 * g;
+      uint16_t* vp = dqkv + (base + key) * ld + 2 * D + h * AH + d * 16 + 4 * g;
+      ushort4 uk, uv;
+      uk.x = f32_to_bf16(dk[d][0] * scale);
+      uk.y = f32_to_bf16(dk[d][1] * scale);
+      uk.z = f32_to_bf16(dk[d][2] * scale);
+      uk.w = f32_to_bf16(dk[d][3] * scale);
+      uv.x = f32_to_bf16(dv[d][0]);
+      uv.y = f32_to_bf16(dv[d][1]);
+      uv.z = f32_to_bf16(dv[d][2]);
+      uv.w = f32_to_bf16(dv[d][3]);
+      *reinterpret_cast<ushort4*>(kp) = uk;
+      *reinterpret_cast<ushort4*>(vp) = uv;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward, dQ: one block per (64-query block, head, batch); queries on lanes
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
+                                                          const uint16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta,
+                                                          const int* __restrict__ lens, uint16_t* __restrict__ dqkv,
+                                                          int S, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t Ks[2][AB * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[2][AB * 128];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  const int q = qb * AB + wid * 16 + i;
+  const float sl2 = scale * 1.4426950408889634f;
+  bf16x8 qf[2], of[2];  // B operands: Q[q][32kh + 8g + j], dO[q][...]
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    qf[kh] = q < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q) * ld + h * AH + kh * 32 + 8 * g) : bf16x8{};
+    of[kh] = q < S ? *reinterpret_cast<const bf16x8*>(dout + (base + q) * (int64_t)D + h * AH + kh * 32 + 8 * g)
+                   : bf16x8{};
+  }
+  const float lq = q < S ? lse[((int64_t)b * H + h) * S + q] : 0.f;
+  const float dq_delta = q < S ? delta[(base + q) * H + h] : 0.f;
+  f32x4 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkb = (len + AB - 1) / AB;
+  TileRegs kr, vr;
+  if (nkb > 0) {
+    stage_tile(Ks[0], qkv, ld, base, min(AB, S), D + h * AH);
+    stage_tile(Vs[0], qkv, ld, base, min(AB, S), 2 * D + h * AH);
+  }
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    const bool more = kb + 1 < nkb;
+    if (more) {
+      const int k1 = (kb + 1) * AB;
+      load_tile(kr, qkv, ld, base + k1, min(AB, S - k1), D + h * AH);
+      load_tile(vr, qkv, ld, base + k1, min(AB, S - k1), 2 * D + h * AH);
+    }
+    f32x4 ds[4];  // dS^T rows = keys kt*16 + 4g + r, column = this lane's query
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        s = mfma(frag_row(Ks[cur], kt * 16, kh), qf[kh], s);
+        dp = mfma(frag_row(Vs[cur], kt * 16, kh), of[kh], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb * AB + kt * 16 + 4 * g + r;
+        const float pv = key < len ? exp2f(s[r] * sl2 - lq) : 0.f;
+        ds[kt][r] = pv * (dp[r] - dq_delta);
+      }
+    }
+    // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 sb = pack_acc(ds[2 * ks], ds[2 * ks + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        acc[d] = mfma(frag_tr(Ks[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), sb, acc[d]);
+    }
+    if (more) {
+      store_tile(Ks[cur ^ 1], kr);
+      store_tile(Vs[cur ^ 1], vr);
+    }
+    __syncthreads();
+  }
+  if (q < S) {
+    uint16_t* qp = dqkv + (base + q) * ld + h * AH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      ushort4 u;
+      u.x = f32_to_bf16(acc[d][0] * scale);
+      u.y = f32_to_bf16(acc[d][1] * scale);
+      u.z = f32_to_bf16(acc[d][2] * scale);
+      u.w = f32_to_bf16(acc[d][3] * scale);
+      *reinterpret_cast<ushort4*>(qp + d * 16 + 4 * g) = u;
+    }
+  }
+}
+
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* lens, int B, int S, int H,
+                     float scale, hipStream_t st) {
+  if (B <= 0 || S <= 0) return;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((S + AB - 1) / AB, H, B), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+}
+
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st) {
+  if (B <= 0 || S <= 0) return;
+  const int64_t pairs = (int64_t)B * S * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
+                     (int64_t)B * S, H);
+  const dim3 grid((S + AB - 1) / AB, H, B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+}
+
+}  // namespace mlt

@@ -290,32 +290,76 @@ void launch_gemm_bf16(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const
 }
 
 // ---- column sums (bias gradients): out[n] (+)= sum_m X[m, n], X bf16 [M, N] ----------
-__global__ __launch_bounds__(256) void colsum_bf16_kernel(const uint16_t* __restrict__ X, int M, int N, int64_t ldx,
-                                                          float* __restrict__ out, int accumulate) {
-  // block: 64 columns x 4 row-groups; fixed-order reduction through LDS (deterministic)
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < N) {
-    int m = rg;
-    for (; m + 12 < M; m += 16) {
-      const float a = bf16_to_f32(X[(int64_t)m * ldx + c]), b = bf16_to_f32(X[(int64_t)(m + 4) * ldx + c]);
-      const float d = bf16_to_f32(X[(int64_t)(m + 8) * ldx + c]), f = bf16_to_f32(X[(int64_t)(m + 12) * ldx + c]);
-      s += (a + b) + (d + f);
+// Column sums of a bf16 [M, N] matrix (bias gradients), two deterministic stages:
+// (1) grid (N/512 column strips, R row slabs): lane = 8 columns (one 16-byte load per row),
+//     4 waves interleave rows, reduced through LDS -> part[R][N];
+// (2) reduce_rows (layernorm.hip): wave = 4 columns, lanes stride the R partials, xor-tree.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ X, int M, int N,
+                                                             int64_t ldx, int rpb, float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + lane * 8;
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  auto acc = [&](const uint4& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[2 * j] += __uint_as_float(w[j] << 16);
+      a[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
     }
-    for (; m < M; m += 4) s += bf16_to_f32(X[(int64_t)m * ldx + c]);
+  };
+  if (c < N) {
+    const uint16_t* p = X + c;
+    int r = r0 + wid;
+    for (; r + 12 < r1; r += 16) {
+      const uint4 v0 = *reinterpret_cast<const uint4*>(p + (int64_t)r * ldx);
+      const uint4 v1 = *reinterpret_cast<const uint4*>(p + (int64_t)(r + 4) * ldx);
+      const uint4 v2 = *reinterpret_cast<const uint4*>(p + (int64_t)(r + 8) * ldx);
+      const uint4 v3 = *reinterpret_cast<const uint4*>(p + (int64_t)(r + 12) * ldx);
+      acc(v0);
+      acc(v1);
+      acc(v2);
+      acc(v3);
+    }
+    for (; r < r1; r += 4) acc(*reinterpret_cast<const uint4*>(p + (int64_t)r * ldx));
   }
-  red[rg][threadIdx.x & 63] = s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wid][lane * 8 + j] = a[j];
   __syncthreads();
-  if (rg == 0 && c < N) {
-    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    out[c] = accumulate ? out[c] + t : t;
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int cc = blockIdx.x * 512 + i;
+    if (cc < N) part[(int64_t)blockIdx.y * N + cc] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
-void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, hipStream_t st) {
+static void colsum_geometry(int M, int& R, int& rpb) {
+  R = M < 32 ? 1 : (M + 31) / 32;
+  if (R > 256) R = 256;
+  rpb = (M + R - 1) / R;
+  R = (M + rpb - 1) / rpb;
+}
+
+int64_t colsum_ws_floats(int M, int N) {
+  int R, rpb;
+  colsum_geometry(M, R, rpb);
+  return (int64_t)R * N;
+}
+
+void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,
+                        hipStream_t st) {
   if (N <= 0) return;
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, st, X, M, N, ldx, out, accumulate);
+  if (M <= 0) {
+    if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
+    return;
+  }
+  int R, rpb;
+  colsum_geometry(M, R, rpb);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 511) / 512, R), dim3(256), 0, st, X, M, N, ldx, rpb, ws);
+  SegOut o{{out, nullptr, nullptr}};
+  launch_reduce_rows(ws, R, N, N, N, o, accumulate ? 1 : 0, st);
 }
 
 }  // namespace mlt

@@ -1,0 +1,346 @@
+// LayerNorm forward/backward and BERT embedding gather/scatter for gfx950.
+//
+// LayerNorm over rows of length D (768 / 1024): one wave per row, 4 rows per
+// 256-thread block, bf16 in/out with 8-byte (4 x bf16) vector accesses, fp32
+// statistics (two-pass mean / variance in registers), fp32 gamma/beta read
+// directly from the master parameters. Backward: dx per row in one pass; dgamma /
+// dbeta accumulated per lane across a grid-stride set of rows, reduced across the
+// block's waves in LDS, written as per-block partials and summed over blocks by a
+// second kernel in a fixed order (deterministic, no atomics).
+#include "mlt_common.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+template <int VPL>  // 4-element vectors per lane: D = VPL * 256
+__device__ __forceinline__ void load_row(const uint16_t* __restrict__ p, float (&x)[VPL * 4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const ushort4 u = reinterpret_cast<const ushort4*>(p)[lane + 64 * v];
+    x[4 * v + 0] = bf16_to_f32(u.x);
+    x[4 * v + 1] = bf16_to_f32(u.y);
+    x[4 * v + 2] = bf16_to_f32(u.z);
+    x[4 * v + 3] = bf16_to_f32(u.w);
+  }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ X, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, uint16_t* __restrict__ Y,
+                                                     float* __restrict__ mean, float* __restrict__ rstd, int64_t rows,
+                                                     float eps) {
+  constexpr int D = VPL * 256, E = VPL * 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float x[E];
+  load_row<VPL>(X + row * D, x);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < E; ++i) s += x[i];
+  const float mu = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const float d = x[i] - mu;
+    q += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = 4 * (lane + 64 * v);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    ushort4 o;
+    o.x = f32_to_bf16((x[4 * v + 0] - mu) * rs * g.x + b.x);
+    o.y = f32_to_bf16((x[4 * v + 1] - mu) * rs * g.y + b.y);
+    o.z = f32_to_bf16((x[4 * v + 2] - mu) * rs * g.z + b.z);
+    o.w = f32_to_bf16((x[4 * v + 3] - mu) * rs * g.w + b.w);
+    reinterpret_cast<ushort4*>(Y + row * D)[lane + 64 * v] = o;
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)); partial dgamma/dbeta per block.
+// DXS: also emit per-block column sums of the (bf16-rounded) dx -- the bias gradient of the
+// linear layer whose output (plus residual) fed this LayerNorm, fused here for free.
+template <int VPL, bool DXS>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ DY, const uint16_t* __restrict__ X,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, uint16_t* __restrict__ DX,
+                                                     float* __restrict__ part, int64_t rows,
+                                                     const uint16_t* __restrict__ DRES) {
+  constexpr int D = VPL * 256, E = VPL * 4;
+  constexpr int NS = DXS ? 3 : 2;
+  __shared__ float red[4][NS * D];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float dg[E], db[E], g[E], dxs[DXS ? E : 1];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    dg[i] = 0.f;
+    db[i] = 0.f;
+    if constexpr (DXS) dxs[i] = 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const float4 gv = *reinterpret_cast<const float4*>(gamma + 4 * (lane + 64 * v));
+    g[4 * v] = gv.x;
+    g[4 * v + 1] = gv.y;
+    g[4 * v + 2] = gv.z;
+    g[4 * v + 3] = gv.w;
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    float x[E], dy[E];
+    load_row<VPL>(X + row * D, x);
+    load_row<VPL>(DY + row * D, dy);
+    const float mu = mean[row], rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float xh = (x[i] - mu) * rs;
+      x[i] = xh;
+      const float t = dy[i] * g[i];
+      s1 += t;
+      s2 += t * xh;
+      dg[i] += dy[i] * xh;
+      db[i] += dy[i];
+    }
+    s1 = wave_sum(s1) * (1.f / D);
+    s2 = wave_sum(s2) * (1.f / D);
+    float dres[E];
+    if (DRES) load_row<VPL>(DRES + row * D, dres);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * v + q;
+        o[q] = rs * (dy[i] * g[i] - s1 - x[i] * s2) + (DRES ? dres[i] : 0.f);
+      }
+      ushort4 u;
+      u.x = f32_to_bf16(o[0]);
+      u.y = f32_to_bf16(o[1]);
+      u.z = f32_to_bf16(o[2]);
+      u.w = f32_to_bf16(o[3]);
+      reinterpret_cast<ushort4*>(DX + row * D)[lane + 64 * v] = u;
+      if constexpr (DXS) {
+        dxs[4 * v + 0] += bf16_to_f32(u.x);
+        dxs[4 * v + 1] += bf16_to_f32(u.y);
+        dxs[4 * v + 2] += bf16_to_f32(u.z);
+        dxs[4 * v + 3] += bf16_to_f32(u.w);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * (lane + 64 * v) + q;
+      red[wid][c] = dg[4 * v + q];
+      red[wid][D + c] = db[4 * v + q];
+      if constexpr (DXS) red[wid][2 * D + c] = dxs[4 * v + q];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < NS * D; c += 256)
+    part[(int64_t)blockIdx.x * NS * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+// out_k[c] (+)= sum_r part[r][k*seg + c]: wave = 4 columns, lanes stride the rows, xor tree (fixed order)
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int64_t ld, int W,
+                                                          int seg, SegOut o, int accmask) {
+  const int lane = threadIdx.x & 63;
+  const int c = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+  if (c >= W) return;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+  for (int r = lane; r < R; r += 64) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)r * ld + c);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s.x += __shfl_xor(s.x, off, 64);
+    s.y += __shfl_xor(s.y, off, 64);
+    s.z += __shfl_xor(s.z, off, 64);
+    s.w += __shfl_xor(s.w, off, 64);
+  }
+  if (lane == 0) {
+    const int k = c / seg;
+    float* out = o.p[k] + (c - k * seg);
+    if ((accmask >> k) & 1) {
+      const float4 prev = *reinterpret_cast<const float4*>(out);
+      s.x += prev.x;
+      s.y += prev.y;
+      s.z += prev.z;
+      s.w += prev.w;
+    }
+    *reinterpret_cast<float4*>(out) = s;
+  }
+}
+
+void launch_reduce_rows(const float* part, int R, int64_t ld, int W, int seg, SegOut outs, int accmask, hipStream_t st) {
+  if (W <= 0 || R <= 0) return;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((W / 4 + 3) / 4), dim3(256), 0, st, part, R, ld, W, seg, outs, accmask);
+}
+
+static int ln_vpl(int D) { return D / 256; }
+
+void launch_ln_fwd(const uint16_t* X, const float* gamma, const float* beta, uint16_t* Y, float* mean, float* rstd,
+                   int64_t rows, int D, float eps, hipStream_t st) {
+  if (rows <= 0) return;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (ln_vpl(D)) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, X, gamma, beta, Y, mean, rstd, rows, eps); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, st, X, gamma, beta, Y, mean, rstd, rows, eps); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, block, 0, st, X, gamma, beta, Y, mean, rstd, rows, eps); break;
+    case 4: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, st, X, gamma, beta, Y, mean, rstd, rows, eps); break;
+    default: break;
+  }
+}
+
+int ln_bwd_partial_blocks(int64_t rows) {
+  int64_t nb = (rows + 3) / 4;
+  return (int)(nb < 512 ? nb : 512);
+}
+
+void launch_ln_bwd(const uint16_t* DY, const uint16_t* X, const float* gamma, const float* mean, const float* rstd,
+                   uint16_t* DX, float* part, float* dgamma, float* dbeta, int64_t rows, int D, int accumulate,
+                   const uint16_t* DRES, float* dxsum, int dxsum_acc, hipStream_t st) {
+  if (rows <= 0) return;
+  const int nb = ln_bwd_partial_blocks(rows);
+  const dim3 grid(nb), block(256);
+#define MLT_LN_BWD(V)                                                                                              \
+  if (dxsum)                                                                                                       \
+    hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, st, DY, X, gamma, mean, rstd, DX, part, rows, DRES); \
+  else                                                                                                             \
+    hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, st, DY, X, gamma, mean, rstd, DX, part, rows, DRES);
+  switch (ln_vpl(D)) {
+    case 1: MLT_LN_BWD(1) break;
+    case 2: MLT_LN_BWD(2) break;
+    case 3: MLT_LN_BWD(3) break;
+    case 4: MLT_LN_BWD(4) break;
+    default: return;
+  }
+#undef MLT_LN_BWD
+  SegOut o{{dgamma, dbeta, dxsum}};
+  launch_reduce_rows(part, nb, (dxsum ? 3 : 2) * D, (dxsum ? 3 : 2) * D, D, o, (accumulate ? 3 : 0) | (dxsum_acc ? 4 : 0), st);
+}
+
+// ---------------------------------------------------------------------------
+// BERT embeddings: out[t] = Wword[ids[t]] + Wpos[pos[t]] + Wtype[tt[t]]  (bf16 tables, bf16 out)
+// ---------------------------------------------------------------------------
+template <int VPL>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                        const uint16_t* __restrict__ Ww, const uint16_t* __restrict__ Wp,
+                                                        const uint16_t* __restrict__ Wt, uint16_t* __restrict__ out,
+                                                        int64_t rows, int S, int64_t vocab, int ntype) {
+  constexpr int D = VPL * 256, E = VPL * 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  int64_t ty = tt ? tt[row] : 0;
+  ty = ty < 0 ? 0 : (ty >= ntype ? ntype - 1 : ty);
+  const int pos = (int)(row % S);
+  float a[E], b[E], c[E];
+  load_row<VPL>(Ww + id * D, a);
+  load_row<VPL>(Wp + (int64_t)pos * D, b);
+  load_row<VPL>(Wt + ty * D, c);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    ushort4 o;
+    o.x = f32_to_bf16(a[4 * v] + b[4 * v] + c[4 * v]);
+    o.y = f32_to_bf16(a[4 * v + 1] + b[4 * v + 1] + c[4 * v + 1]);
+    o.z = f32_to_bf16(a[4 * v + 2] + b[4 * v + 2] + c[4 * v + 2]);
+    o.w = f32_to_bf16(a[4 * v + 3] + b[4 * v + 3] + c[4 * v + 3]);
+    reinterpret_cast<ushort4*>(out + row * D)[lane + 64 * v] = o;
+  }
+}
+
+// word / position grads: fp32 atomics (the vocabulary rows hit are sparse and spread);
+// token-type grads: per-block partials over the (few) type rows, reduced in fixed order.
+template <int VPL>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                        const uint16_t* __restrict__ DX, float* __restrict__ gw,
+                                                        float* __restrict__ gp, float* __restrict__ part_t,
+                                                        int64_t rows, int S, int64_t vocab, int ntype) {
+  constexpr int D = VPL * 256, E = VPL * 4;
+  __shared__ float red[4][2 * D];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float t0[E], t1[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    t0[i] = 0.f;
+    t1[i] = 0.f;
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    float d[E];
+    load_row<VPL>(DX + row * D, d);
+    int64_t id = ids[row];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    const int pos = (int)(row % S);
+    const int64_t ty = tt ? tt[row] : 0;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * (lane + 64 * v) + q;
+        atomicAdd(gw + id * D + c, d[4 * v + q]);
+        atomicAdd(gp + (int64_t)pos * D + c, d[4 * v + q]);
+        if (ty == 0) t0[4 * v + q] += d[4 * v + q];
+        else t1[4 * v + q] += d[4 * v + q];
+      }
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * (lane + 64 * v) + q;
+      red[wid][c] = t0[4 * v + q];
+      red[wid][D + c] = t1[4 * v + q];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    part_t[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww, const uint16_t* Wp,
+                      const uint16_t* Wt, uint16_t* out, int64_t rows, int S, int D, int64_t vocab, int ntype,
+                      hipStream_t st) {
+  if (rows <= 0) return;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (D / 256) {
+    case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, block, 0, st, ids, tt, Ww, Wp, Wt, out, rows, S, vocab, ntype); break;
+    case 4: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, block, 0, st, ids, tt, Ww, Wp, Wt, out, rows, S, vocab, ntype); break;
+    case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, block, 0, st, ids, tt, Ww, Wp, Wt, out, rows, S, vocab, ntype); break;
+    case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, block, 0, st, ids, tt, Ww, Wp, Wt, out, rows, S, vocab, ntype); break;
+    default: break;
+  }
+}
+
+void launch_embed_bwd(const int64_t* ids, const int64_t* tt, const uint16_t* DX, float* gw, float* gp, float* gt,
+                      float* part, int64_t rows, int S, int D, int64_t vocab, int ntype, hipStream_t st) {
+  if (rows <= 0) return;
+  const int nb = ln_bwd_partial_blocks(rows);
+  const dim3 grid(nb), block(256);
+  switch (D / 256) {
+    case 3: hipLaunchKernelGGL(embed_bwd_kernel<3>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
+    case 4: hipLaunchKernelGGL(embed_bwd_kernel<4>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
+    case 1: hipLaunchKernelGGL(embed_bwd_kernel<1>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
+    case 2: hipLaunchKernelGGL(embed_bwd_kernel<2>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
+    default: return;
+  }
+  // type rows 0 and 1 (ntype <= 2): accumulate the partials into gt[0:D] and gt[D:2D]
+  SegOut o{{gt, gt + D, nullptr}};
+  launch_reduce_rows(part, nb, 2 * D, ntype >= 2 ? 2 * D : D, D, o, ntype >= 2 ? 3 : 1, st);
+}
+
+}  // namespace mlt

@@ -113,10 +113,13 @@ class FusedOptimizer(torch.optim.Optimizer):
             h = self.hyper(gi)
             if fp.device.type == "cuda":
                 C = require_native()
+                shadow = fp.shadow if fp.shadow is not None and fp._shadow_ver == fp.data._version else None
                 C.flat_optim(fp.data, fp.grad, self._s1[gi], self._s2[gi], h["kind"], h["lr"], h["momentum"],
                              h["dampening"], h["weight_decay"], h["beta1"], h["beta2"], h["eps"], h["lr_decay"],
                              h["grad_scale"], h["nesterov"], h["maximize"], None, None, None,
-                             float(self._steps[gi]), None, None)
+                             float(self._steps[gi]), shadow, None)
+                if shadow is not None:
+                    fp.mark_shadow_fresh()  # the kernel rewrote the bf16 copy of every updated weight
             else:
                 _cpu_update(h, float(self._steps[gi]), fp.data, fp.grad, self._s1[gi], self._s2[gi])
         return loss

@@ -1,0 +1,285 @@
+"""Autograd blocks of the transformer path over the native gfx950 kernels.
+
+Mixed precision: parameters are fp32 masters (in a FlatParams buffer when an
+optimizer/DDP owns them); compute reads their bf16 *shadow* (refreshed by the
+fused optimizer kernel in the same pass that updates the master, so there is
+no separate cast per step). Weight / bias gradients come back in fp32.
+
+Blocks (one autograd node each, so the backward can fuse across ops):
+
+* ``attention_block``: x -> QKV GEMM(+bias) -> fused flash attention -> out-proj
+  GEMM (+bias +residual x). Backward: wgrad/colsum/dgrad of out-proj, attention
+  backward into the packed dQKV, wgrad/colsum of QKV and dgrad with the residual
+  gradient folded into the GEMM epilogue.
+* ``ffn_block``: x -> FFN1 GEMM (+bias, GELU epilogue that also stores the
+  pre-activation) -> FFN2 GEMM (+bias +residual). Backward: FFN2's dgrad GEMM
+  applies gelu'(pre) in its epilogue (no separate elementwise pass).
+* ``attention_ln_block`` / ``ffn_ln_block``: the block followed by its post-LayerNorm as one
+  node; the LayerNorm backward kernel also produces the column sums of its dx, which are the
+  bias gradient of the block's last linear layer (no separate pass over dy).
+* ``layer_norm``, ``embeddings``.
+
+Linear layout conventions (nn.Linear weight [out, in]):
+  fwd   y  = x . W^T         gemm(x, W, a_mn=0, b_mn=0)
+  dgrad dx = dy . W          gemm(dy, W, a_mn=0, b_mn=1)
+  wgrad dW = dy^T . x        gemm(dy, x, a_mn=1, b_mn=1) -> fp32
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ml_trainer_amd.ops._ext import require_native
+from ml_trainer_amd.utils.flat import FlatParams
+
+
+def bf16_weight(p: torch.Tensor) -> torch.Tensor:
+    """bf16 compute copy of an fp32 master parameter."""
+    fp = FlatParams.owner(p)
+    if fp is not None and fp.device.type == "cuda":
+        return fp.shadow_view(p)
+    cache = getattr(p, "_mlt_bf16", None)
+    if cache is not None and cache[0] == p._version and cache[1] == p.data_ptr():
+        return cache[2]
+    w = p.detach().to(torch.bfloat16).contiguous()
+    p._mlt_bf16 = (p._version, p.data_ptr(), w)
+    return w
+
+
+def _gemm(C, A, B, out, a_mn, b_mn, **kw):
+    C.gemm(A, B, out, a_mn, b_mn, **kw)
+    return out
+
+
+def linear_fwd(x, w16, bias=None, gelu_aux=None, res=None):
+    C = require_native()
+    y = torch.empty(x.shape[0], w16.shape[0], dtype=torch.bfloat16, device=x.device)
+    C.gemm(x, w16, y, False, False, bias=bias, aux=gelu_aux, res=res, mode=1 if gelu_aux is not None else 0)
+    return y
+
+
+def linear_wgrad(dy, x):
+    C = require_native()
+    dw = torch.empty(dy.shape[1], x.shape[1], dtype=torch.float32, device=dy.device)
+    C.gemm(dy, x, dw, True, True)
+    return dw
+
+
+def colsum(dy):
+    C = require_native()
+    db = torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device)
+    C.colsum(dy, db, False)
+    return db
+
+
+def _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H):
+    C = require_native()
+    wqkv16, wo16 = bf16_weight(wqkv), bf16_weight(wo)
+    qkv = linear_fwd(x, wqkv16, bqkv)
+    attn = torch.empty(B * S, H * 64, dtype=torch.bfloat16, device=x.device)
+    lse = torch.empty(B * H * S, dtype=torch.float32, device=x.device)
+    C.attn_fwd(qkv, attn, lse, lens, B, S, H, _ATTN_SCALE)
+    y = linear_fwd(attn, wo16, bo, res=x)  # out-proj + bias + residual
+    return y, (x, qkv, attn, lse, wqkv16, wo16)
+
+
+def _attn_bwd(saved, lens, B, S, H, dy, dbo=None):
+    """Backward of the attention block; `dbo` = precomputed bias grad of the out-proj (fused
+    into the LayerNorm backward that produced dy) or None to compute it here."""
+    C = require_native()
+    x, qkv, attn, lse, wqkv16, wo16 = saved
+    dwo = linear_wgrad(dy, attn)
+    if dbo is None:
+        dbo = colsum(dy)
+    dattn = torch.empty_like(attn)
+    C.gemm(dy, wo16, dattn, False, True)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
+    C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
+    dwqkv = linear_wgrad(dqkv, x)
+    dbqkv = colsum(dqkv)
+    dx = torch.empty_like(x)
+    C.gemm(dqkv, wqkv16, dx, False, True, res=dy)  # dx = dqkv . Wqkv + dy (residual)
+    return dx, dwqkv, dbqkv, dwo, dbo
+
+
+def _ffn_fwd(x, w1, b1, w2, b2):
+    w116, w216 = bf16_weight(w1), bf16_weight(w2)
+    pre = torch.empty(x.shape[0], w116.shape[0], dtype=torch.bfloat16, device=x.device)
+    a = linear_fwd(x, w116, b1, gelu_aux=pre)  # a = gelu(pre), pre saved
+    y = linear_fwd(a, w216, b2, res=x)
+    return y, (x, pre, a, w116, w216)
+
+
+def _ffn_bwd(saved, dy, db2=None):
+    C = require_native()
+    x, pre, a, w116, w216 = saved
+    dw2 = linear_wgrad(dy, a)
+    if db2 is None:
+        db2 = colsum(dy)
+    dpre = torch.empty_like(pre)
+    C.gemm(dy, w216, dpre, False, True, aux=pre, mode=2)  # (dy . W2) * gelu'(pre)
+    dw1 = linear_wgrad(dpre, x)
+    db1 = colsum(dpre)
+    dx = torch.empty_like(x)
+    C.gemm(dpre, w116, dx, False, True, res=dy)
+    return dx, dw1, db1, dw2, db2
+
+
+def _ln_fwd(x, gamma, beta, eps):
+    C = require_native()
+    rows = x.shape[0]
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    C.ln_fwd(x, gamma, beta, y, mean, rstd, eps)
+    return y, (x, gamma, mean, rstd)
+
+
+def _ln_bwd(saved, dy, want_dxsum=False):
+    C = require_native()
+    x, gamma, mean, rstd = saved
+    D = gamma.numel()
+    dx = torch.empty_like(x)
+    part = torch.empty(C.ln_partial_blocks(x.shape[0]) * (3 if want_dxsum else 2) * D, dtype=torch.float32,
+                       device=x.device)
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    dxs = torch.empty(D, dtype=torch.float32, device=x.device) if want_dxsum else None
+    C.ln_bwd(dy, x, gamma, mean, rstd, dx, part, dg, db, dxsum=dxs)
+    return dx, dg, db, dxs
+
+
+_ATTN_SCALE = 1.0 / 8.0  # 1/sqrt(head_dim = 64)
+
+
+class _AttentionBlock(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, wo, bo, lens, B, S, H):
+        y, saved = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+        ctx.save_for_backward(*saved)
+        ctx.lens, ctx.dims = lens, (B, S, H)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous().to(torch.bfloat16)
+        grads = _attn_bwd(ctx.saved_tensors, ctx.lens, *ctx.dims, dy)
+        return grads + (None, None, None, None)
+
+
+class _FFNBlock(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        y, saved = _ffn_fwd(x, w1, b1, w2, b2)
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _ffn_bwd(ctx.saved_tensors, dy.contiguous().to(torch.bfloat16))
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        y, saved = _ln_fwd(x, gamma, beta, eps)
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx, dg, db, _ = _ln_bwd(ctx.saved_tensors, dy.contiguous().to(torch.bfloat16))
+        return dx, dg, db, None
+
+
+class _AttentionLNBlock(torch.autograd.Function):
+    """LN(attention_block(x)) as one node: the LayerNorm backward also emits the out-proj bias
+    gradient (column sums of its dx), so no separate pass over dy."""
+
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps):
+        a, s1 = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+        y, s2 = _ln_fwd(a, gamma, beta, eps)
+        ctx.save_for_backward(*s1, *s2)
+        ctx.lens, ctx.dims = lens, (B, S, H)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        da, dg, db, dbo = _ln_bwd(t[6:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
+        dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:6], ctx.lens, *ctx.dims, da, dbo=dbo)
+        return dx, dwqkv, dbqkv, dwo, dbo, dg, db, None, None, None, None, None
+
+
+class _FFNLNBlock(torch.autograd.Function):
+    """LN(ffn_block(x)) as one node (FFN2 bias gradient fused into the LayerNorm backward)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, eps):
+        f, s1 = _ffn_fwd(x, w1, b1, w2, b2)
+        y, s2 = _ln_fwd(f, gamma, beta, eps)
+        ctx.save_for_backward(*s1, *s2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        df, dg, db, db2 = _ln_bwd(t[5:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
+        dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:5], df, db2=db2)
+        return dx, dw1, db1, dw2, db2, dg, db, None
+
+
+class _Embeddings(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, tt, ww, wp, wt, S):
+        C = require_native()
+        ids = ids.contiguous().view(-1).to(torch.int64)
+        ttf = tt.contiguous().view(-1).to(torch.int64) if tt is not None else None
+        D = ww.shape[1]
+        out = torch.empty(ids.numel(), D, dtype=torch.bfloat16, device=ids.device)
+        C.embed_fwd(ids, ttf, bf16_weight(ww), bf16_weight(wp), bf16_weight(wt), out, S)
+        ctx.save_for_backward(ids, ttf if ttf is not None else torch.empty(0, dtype=torch.int64))
+        ctx.meta = (tt is not None, S, ww.shape, wp.shape, wt.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = require_native()
+        ids, ttf = ctx.saved_tensors
+        has_tt, S, sw, sp, st = ctx.meta
+        dout = dout.contiguous().to(torch.bfloat16)
+        gw = torch.zeros(sw, dtype=torch.float32, device=dout.device)
+        gp = torch.zeros(sp, dtype=torch.float32, device=dout.device)
+        gt = torch.zeros(st, dtype=torch.float32, device=dout.device)
+        D = sw[1]
+        part = torch.empty(C.ln_partial_blocks(ids.numel()) * 2 * D, dtype=torch.float32, device=dout.device)
+        C.embed_bwd(ids, ttf if has_tt else None, dout, gw, gp, gt, part, S)
+        return None, None, gw, gp, gt, None
+
+
+def attention_block(x, wqkv, bqkv, wo, bo, lens: Optional[torch.Tensor], B: int, S: int, H: int):
+    return _AttentionBlock.apply(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+
+
+def ffn_block(x, w1, b1, w2, b2):
+    return _FFNBlock.apply(x, w1, b1, w2, b2)
+
+
+def attention_ln_block(x, wqkv, bqkv, wo, bo, gamma, beta, lens: Optional[torch.Tensor], B: int, S: int, H: int,
+                       eps: float):
+    return _AttentionLNBlock.apply(x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps)
+
+
+def ffn_ln_block(x, w1, b1, w2, b2, gamma, beta, eps: float):
+    return _FFNLNBlock.apply(x, w1, b1, w2, b2, gamma, beta, eps)
+
+
+def layer_norm(x, gamma, beta, eps: float):
+    return _LayerNorm.apply(x, gamma, beta, eps)
+
+
+def embeddings(ids, tt, ww, wp, wt, S: int):
+    return _Embeddings.apply(ids, tt, ww, wp, wt, S)

@@ -15,9 +15,13 @@ can use float4 accesses on any parameter.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
+
+# parameter id -> FlatParams that owns it (lets ops find a param's bf16 shadow view)
+_OWNER: "weakref.WeakValueDictionary[int, FlatParams]" = weakref.WeakValueDictionary()
 
 
 def _round_up(x: int, a: int) -> int:
@@ -49,6 +53,9 @@ class FlatParams:
                 p.data = self.data[o:o + n].view_as(p)
                 p.grad = self.grad[o:o + n].view_as(p)
                 self._index[id(p)] = i
+                _OWNER[id(p)] = self
+        self.shadow: Optional[torch.Tensor] = None  # bf16 copy of `data` for mixed-precision compute
+        self._shadow_ver = -1
 
     # ------------------------------------------------------------------
     def segment(self, p: torch.nn.Parameter) -> Tuple[int, int]:
@@ -95,6 +102,38 @@ class FlatParams:
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+
+    # ------------------------------------------------------------------ bf16 shadow
+    @staticmethod
+    def owner(p: torch.Tensor) -> Optional["FlatParams"]:
+        fp = _OWNER.get(id(p))
+        if fp is not None and id(p) in fp._index:
+            return fp
+        return None
+
+    def refresh_shadow(self) -> torch.Tensor:
+        """(Re)build the bf16 shadow when the fp32 master changed outside the fused optimizer
+        (load_state_dict, manual edits bump the tensor version counter; the optimizer kernel
+        writes the shadow itself and leaves the counter alone)."""
+        if self.shadow is None:
+            self.shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            self._shadow_ver = -1
+        if self._shadow_ver != self.data._version:
+            if self.device.type == "cuda":
+                from ml_trainer_amd.ops._ext import require_native
+                require_native().cast_bf16(self.data, self.shadow)
+            else:
+                self.shadow.copy_(self.data)
+            self._shadow_ver = self.data._version
+        return self.shadow
+
+    def shadow_view(self, p: torch.Tensor) -> torch.Tensor:
+        sh = self.refresh_shadow()
+        o, n = self.segment(p)
+        return sh[o:o + n].view(p.shape)
+
+    def mark_shadow_fresh(self) -> None:
+        self._shadow_ver = self.data._version
 
     def state_dict_views(self) -> List[torch.Tensor]:
         return [self.data[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]

@@ -1,0 +1,286 @@
+"""Transformer kernels (layernorm.hip, attention.hip) and autograd blocks
+(ops/transformer.py) vs plain torch fp32 references of the same ops."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ml_trainer_amd.ops._ext import require_native
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(shape, g, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(dev)
+
+
+def _close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= tol * ref, f"max abs err {err:.4g} vs ref max {ref:.4g} (tol {tol})"
+
+
+# ---------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [256, 768, 1024])
+@pytest.mark.parametrize("rows", [1, 37, 1024])
+def test_layernorm_fwd_bwd(dev, D, rows):
+    C = require_native()
+    g = torch.Generator().manual_seed(D + rows)
+    x = _bf((rows, D), g, 2.0) + 0.5
+    gamma = (torch.randn(D, generator=g) * 0.2 + 1).to(dev)
+    beta = (torch.randn(D, generator=g) * 0.1).to(dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    C.ln_fwd(x, gamma, beta, y, mean, rstd, 1e-5)
+    xr = x.float().requires_grad_()
+    gr, br = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    yr = F.layer_norm(xr, (D,), gr, br, 1e-5)
+    _close(y, yr, 1e-2)
+    torch.testing.assert_close(mean, xr.detach().mean(1), rtol=1e-4, atol=1e-4)
+    dy = _bf((rows, D), g)
+    yr.backward(dy.float())
+    dx = torch.empty_like(x)
+    part = torch.empty(C.ln_partial_blocks(rows) * 2 * D, device=dev)
+    dg = torch.empty(D, device=dev)
+    db = torch.empty(D, device=dev)
+    C.ln_bwd(dy, x, gamma, mean, rstd, dx, part, dg, db, False, None)
+    _close(dx, xr.grad, 1.5e-2)
+    _close(dg, gr.grad, 2e-3)
+    _close(db, br.grad, 2e-3)
+    # residual-gradient fusion + accumulate + fused column sums of dx
+    dres = _bf((rows, D), g)
+    dg2, db2 = dg.clone(), db.clone()
+    part3 = torch.empty(C.ln_partial_blocks(rows) * 3 * D, device=dev)
+    dxs = torch.ones(D, device=dev)
+    C.ln_bwd(dy, x, gamma, mean, rstd, dx, part3, dg2, db2, True, dres, dxsum=dxs, dxsum_acc=True)
+    _close(dx, xr.grad + dres.float(), 1.5e-2)
+    _close(dg2, 2 * gr.grad, 2e-3)
+    _close(db2, 2 * br.grad, 2e-3)
+    torch.testing.assert_close(dxs, 1 + dx.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N", [(1, 8), (37, 768), (8192, 2304), (1000, 3072), (300, 520)])
+def test_colsum(dev, M, N):
+    C = require_native()
+    g = torch.Generator().manual_seed(M + N)
+    X = _bf((M, N), g)
+    out = torch.empty(N, device=dev)
+    C.colsum(X, out)
+    torch.testing.assert_close(out, X.float().sum(0), rtol=1e-4, atol=1e-3)
+    C.colsum(X, out, accumulate=True)
+    torch.testing.assert_close(out, 2 * X.float().sum(0), rtol=1e-4, atol=2e-3)
+    # strided view (row stride != N)
+    W = _bf((M, N + 16), g)[:, 8:N + 8]
+    C.colsum(W, out)
+    torch.testing.assert_close(out, W.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+# ---------------------------------------------------------------- embeddings
+@pytest.mark.parametrize("with_tt", [False, True])
+def test_embeddings(dev, with_tt):
+    C = require_native()
+    g = torch.Generator().manual_seed(3)
+    V, P, D, B, S = 500, 128, 256, 3, 96
+    ww, wp, wt = _bf((V, D), g), _bf((P, D), g), _bf((2, D), g)
+    ids = torch.randint(0, V, (B, S), generator=g).to(dev)
+    ids[0, :10] = 7  # repeated ids exercise the scatter-add
+    tt = torch.randint(0, 2, (B, S), generator=g).to(dev) if with_tt else None
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=dev)
+    C.embed_fwd(ids.view(-1), tt.view(-1) if tt is not None else None, ww, wp, wt, out, S)
+    t = tt if tt is not None else torch.zeros_like(ids)
+    ref = ww.float()[ids] + wp.float()[torch.arange(S, device=dev)][None] + wt.float()[t]
+    _close(out.view(B, S, D), ref, 1e-2)
+    dout = _bf((B * S, D), g)
+    gw, gp, gt = (torch.zeros(V, D, device=dev), torch.zeros(P, D, device=dev), torch.zeros(2, D, device=dev))
+    part = torch.empty(C.ln_partial_blocks(B * S) * 2 * D, device=dev)
+    C.embed_bwd(ids.view(-1), tt.view(-1) if tt is not None else None, dout, gw, gp, gt, part, S)
+    d = dout.float().view(B, S, D)
+    rgw = torch.zeros(V, D, device=dev).index_add_(0, ids.view(-1), d.view(-1, D))
+    rgp = torch.zeros(P, D, device=dev)
+    rgp[:S] = d.sum(0)
+    rgt = torch.zeros(2, D, device=dev).index_add_(0, t.view(-1), d.view(-1, D))
+    _close(gw, rgw, 1e-4)
+    _close(gp, rgp, 1e-4)
+    _close(gt, rgt, 1e-4)
+
+
+# ---------------------------------------------------------------- attention
+def _attn_ref(qkv, B, S, H, lens, scale):
+    q, k, v = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    if lens is not None:
+        mask = torch.arange(S, device=qkv.device)[None, :] < lens[:, None]
+        s = s.masked_fill(~mask[:, None, None, :], float("-inf"))
+    return (s.softmax(-1) @ v).permute(0, 2, 1, 3).reshape(B * S, H * 64)
+
+
+@pytest.mark.parametrize("B,S,H,use_lens", [(2, 64, 1, False), (2, 128, 2, False), (3, 200, 2, True),
+                                            (1, 512, 4, False), (2, 256, 3, True)])
+def test_attention(dev, B, S, H, use_lens):
+    C = require_native()
+    g = torch.Generator().manual_seed(B * 1000 + S + H)
+    D = H * 64
+    qkv = _bf((B * S, 3 * D), g, 1.0)
+    lens = None
+    if use_lens:
+        lens = torch.randint(1, S + 1, (B,), generator=g).to(torch.int32)
+        lens[0] = S
+        lens = lens.to(dev)
+    scale = 1.0 / math.sqrt(64)
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * H * S, device=dev)
+    C.attn_fwd(qkv, out, lse, lens, B, S, H, scale)
+    qr = qkv.float().requires_grad_()
+    ref = _attn_ref(qr, B, S, H, lens, scale)
+    _close(out, ref, 2e-2)
+    # base-2 log-sum-exp of the scaled scores
+    q, k, _ = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    if lens is not None:
+        mask = torch.arange(S, device=dev)[None, :] < lens[:, None]
+        s = s.masked_fill(~mask[:, None, None, :], float("-inf"))
+    torch.testing.assert_close(lse.view(B, H, S), torch.logsumexp(s, -1) / math.log(2), rtol=1e-3, atol=1e-3)
+    dout = _bf((B * S, D), g)
+    ref.backward(dout.float())
+    dqkv = torch.full_like(qkv, float("nan"))
+    delta = torch.empty(B * S * H, device=dev)
+    C.attn_bwd(qkv, out, dout, lse, delta, lens, dqkv, B, S, H, scale)
+    assert torch.isfinite(dqkv.float()).all()
+    gr = qr.grad.view(B * S, 3, D)
+    dg = dqkv.view(B * S, 3, D)
+    for j, name in enumerate("qkv"):
+        err = (dg[:, j].float() - gr[:, j]).abs().max().item()
+        ref_max = gr[:, j].abs().max().item() + 1e-6
+        assert err <= 3e-2 * ref_max, f"d{name}: {err:.4g} vs {ref_max:.4g}"
+
+
+# ---------------------------------------------------------------- blocks
+def test_attention_block_and_ffn_block(dev):
+    from ml_trainer_amd.ops import transformer as T
+    torch.manual_seed(0)
+    B, S, H = 2, 128, 4
+    D, Fh = H * 64, 1024
+    x = (torch.randn(B * S, D, device=dev) * 0.5).to(torch.bfloat16)
+    wqkv = (torch.randn(3 * D, D, device=dev) * 0.05).requires_grad_()
+    bqkv = (torch.randn(3 * D, device=dev) * 0.05).requires_grad_()
+    wo = (torch.randn(D, D, device=dev) * 0.05).requires_grad_()
+    bo = (torch.randn(D, device=dev) * 0.05).requires_grad_()
+    xa = x.clone().requires_grad_()
+    y = T.attention_block(xa, wqkv, bqkv, wo, bo, None, B, S, H)
+    # fp32 reference on the bf16-rounded weights the kernels consume
+    wq_r, wo_r = wqkv.detach().bfloat16().float().requires_grad_(), wo.detach().bfloat16().float().requires_grad_()
+    bq_r, bo_r = bqkv.detach().clone().requires_grad_(), bo.detach().clone().requires_grad_()
+    xr = x.float().requires_grad_()
+    qkv = xr @ wq_r.t() + bq_r
+    ctx = _attn_ref(qkv, B, S, H, None, 0.125)
+    yr = ctx @ wo_r.t() + bo_r + xr
+    _close(y, yr, 2e-2)
+    dy = (torch.randn(B * S, D, device=dev)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(xa.grad, xr.grad, 3e-2)
+    _close(wqkv.grad, wq_r.grad, 3e-2)
+    _close(bqkv.grad, bq_r.grad, 3e-2)
+    _close(wo.grad, wo_r.grad, 2e-2)
+    _close(bo.grad, bo_r.grad, 1e-2)
+
+    w1 = (torch.randn(Fh, D, device=dev) * 0.05).requires_grad_()
+    b1 = (torch.randn(Fh, device=dev) * 0.05).requires_grad_()
+    w2 = (torch.randn(D, Fh, device=dev) * 0.05).requires_grad_()
+    b2 = (torch.randn(D, device=dev) * 0.05).requires_grad_()
+    xf = x.clone().requires_grad_()
+    yf = T.ffn_block(xf, w1, b1, w2, b2)
+    w1r, w2r = w1.detach().bfloat16().float().requires_grad_(), w2.detach().bfloat16().float().requires_grad_()
+    b1r, b2r = b1.detach().clone().requires_grad_(), b2.detach().clone().requires_grad_()
+    xfr = x.float().requires_grad_()
+    yfr = F.gelu(xfr @ w1r.t() + b1r) @ w2r.t() + b2r + xfr
+    _close(yf, yfr, 2e-2)
+    yf.backward(dy)
+    yfr.backward(dy.float())
+    _close(xf.grad, xfr.grad, 3e-2)
+    _close(w1.grad, w1r.grad, 3e-2)
+    _close(b1.grad, b1r.grad, 3e-2)
+    _close(w2.grad, w2r.grad, 2e-2)
+    _close(b2.grad, b2r.grad, 1e-2)
+
+
+def _grads(m, fn, ids, mask, y):
+    m.zero_grad(set_to_none=True)
+    F.cross_entropy(fn(ids, mask).float(), y).backward()
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("use_mask", [False, True])
+def test_bert_tiny_matches_reference(dev, use_mask):
+    """Native bf16 gradients vs the fp32 reference, error-budgeted against PyTorch's own bf16
+    autocast path (same weights): the native error may not exceed 2x autocast's (+ floor)."""
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    torch.manual_seed(0)
+    m = BertClassifier(bert_config("bert-tiny")).to(dev)
+    ids = torch.randint(5, 1000, (2, 128), device=dev)
+    mask = torch.ones(2, 128, dtype=torch.long, device=dev)
+    if use_mask:
+        mask[1, 100:] = 0
+    y = torch.tensor([0, 1], device=dev)
+    out = m(ids, mask)
+    ref = m.forward_reference(ids, mask)
+    _close(out, ref, 5e-2)
+    gn = _grads(m, m, ids, mask, y)
+    gr = _grads(m, m.forward_reference, ids, mask, y)
+    ga = _grads(m, m.forward_torch_bf16, ids, mask, y)
+    for n in gr:
+        nr = gr[n].norm().item()
+        if nr < 1e-8:
+            continue
+        e_nat = (gn[n] - gr[n]).norm().item() / nr
+        e_ac = (ga[n] - gr[n]).norm().item() / nr
+        assert e_nat <= max(2.0 * e_ac, 0.02), f"{n}: native rel err {e_nat:.4f} vs autocast {e_ac:.4f}"
+
+
+def test_fused_ln_blocks_match_unfused(dev):
+    from ml_trainer_amd.ops import transformer as T
+    torch.manual_seed(1)
+    B, S, H = 2, 128, 4
+    D = H * 64
+    x = (torch.randn(B * S, D, device=dev)).to(torch.bfloat16)
+    ps = [(torch.randn(3 * D, D, device=dev) * 0.05), torch.randn(3 * D, device=dev) * 0.05,
+          torch.randn(D, D, device=dev) * 0.05, torch.randn(D, device=dev) * 0.05,
+          1 + 0.1 * torch.randn(D, device=dev), 0.1 * torch.randn(D, device=dev)]
+    dy = torch.randn(B * S, D, device=dev).to(torch.bfloat16)
+
+    def run(fused):
+        xs = x.clone().requires_grad_()
+        qs = [p.clone().requires_grad_() for p in ps]
+        if fused:
+            y = T.attention_ln_block(xs, *qs[:4], qs[4], qs[5], None, B, S, H, 1e-12)
+        else:
+            y = T.layer_norm(T.attention_block(xs, *qs[:4], None, B, S, H), qs[4], qs[5], 1e-12)
+        y.backward(dy)
+        return [y, xs.grad] + [q.grad for q in qs]
+
+    for a, b in zip(run(True), run(False)):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_bert_tiny_trains(dev):
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = BertClassifier(bert_config("bert-tiny")).to(dev)
+    opt = FusedAdamW(m.parameters(), lr=3e-4, weight_decay=0.01)
+    assert FlatParams.owner(m.layers[0].qkv.weight) is not None
+    ids = torch.randint(5, 1000, (8, 128), device=dev)
+    y = torch.randint(0, 2, (8,), device=dev)
+    ids[y == 1, 5] = 3  # learnable marker
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = F.cross_entropy(m(ids), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0], losses
