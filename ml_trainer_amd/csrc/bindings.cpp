@@ -14,6 +14,7 @@
 #include <memory>
 
 #include "mlt_kernels.h"
+#include "mlt_comm.h"
 #include "mlt_runtime.h"
 
 namespace py = pybind11;
@@ -427,6 +428,107 @@ void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10
 }
 
 // ----------------------------------------------------------------------------
+// Native RCCL communicator over torch tensors (enqueued on the current stream, so
+// collectives order with compute and can be captured into hipGraphs).
+// ----------------------------------------------------------------------------
+static CommDtype comm_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return CommDtype::F32;
+    case at::kBFloat16: return CommDtype::BF16;
+    case at::kHalf: return CommDtype::F16;
+    case at::kInt: return CommDtype::I32;
+    case at::kLong: return CommDtype::I64;
+    case at::kByte: return CommDtype::U8;
+    default: TORCH_CHECK(false, "unsupported dtype for a collective: ", t.scalar_type());
+  }
+}
+
+static CommOp comm_op(const std::string& op) {
+  if (op == "sum") return CommOp::SUM;
+  if (op == "avg") return CommOp::AVG;
+  if (op == "max") return CommOp::MAX;
+  if (op == "min") return CommOp::MIN;
+  TORCH_CHECK(false, "unknown reduce op ", op);
+}
+
+class PyComm {
+ public:
+  PyComm(py::bytes uid, int nranks, int rank, int device) : c_(std::string(uid), nranks, rank, device) {}
+  static py::bytes unique_id() { return py::bytes(Communicator::unique_id()); }
+  int rank() const { return c_.rank(); }
+  int size() const { return c_.size(); }
+  void all_reduce(Tensor t, const std::string& op) {
+    chk(t);
+    c_.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t), comm_op(op), cur_stream());
+  }
+  void reduce_scatter(Tensor in, Tensor out, const std::string& op) {
+    chk(in);
+    chk(out);
+    TORCH_CHECK(in.numel() == out.numel() * c_.size() && in.scalar_type() == out.scalar_type(), "reduce_scatter sizes");
+    c_.reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), comm_dtype(in), comm_op(op), cur_stream());
+  }
+  void all_gather(Tensor in, Tensor out) {
+    chk(in);
+    chk(out);
+    TORCH_CHECK(out.numel() == in.numel() * c_.size() && in.scalar_type() == out.scalar_type(), "all_gather sizes");
+    c_.all_gather(in.data_ptr(), out.data_ptr(), in.numel(), comm_dtype(in), cur_stream());
+  }
+  void broadcast(Tensor t, int root) {
+    chk(t);
+    TORCH_CHECK(root >= 0 && root < c_.size(), "broadcast root");
+    c_.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t), root, cur_stream());
+  }
+  void all_to_all(Tensor in, Tensor out) {
+    chk(in);
+    chk(out);
+    TORCH_CHECK(in.numel() == out.numel() && in.numel() % c_.size() == 0 && in.scalar_type() == out.scalar_type(),
+                "all_to_all sizes");
+    c_.all_to_all(in.data_ptr(), out.data_ptr(), in.numel() / c_.size(), comm_dtype(in), cur_stream());
+  }
+  std::string async_error() const { return c_.async_error(); }
+  void abort() { c_.abort(); }
+  Communicator& raw() { return c_; }
+
+ private:
+  void chk(const Tensor& t) const {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "collective tensors must be contiguous device tensors");
+    TORCH_CHECK(t.get_device() == c_.device(), "tensor on device ", t.get_device(), ", communicator on ",
+                c_.device());
+  }
+  Communicator c_;
+};
+
+// Pinned-host staging slots exposed as CPU uint8 tensors (collate straight into them).
+class PyPrefetcher {
+ public:
+  PyPrefetcher(int64_t slot_bytes, int depth, int device) : p_((size_t)slot_bytes, depth, device), bytes_(slot_bytes) {}
+  Tensor slot(int i) {
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    return torch::from_blob(p_.slot_ptr(i), {bytes_}, torch::TensorOptions().dtype(at::kByte));
+  }
+  void copy_to_device(int i, Tensor dst, int64_t nbytes) {
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "dst must be a contiguous device tensor");
+    TORCH_CHECK(nbytes >= 0 && nbytes <= bytes_ && nbytes <= (int64_t)(dst.numel() * dst.element_size()),
+                "copy size");
+    p_.copy_to_device(i, dst.data_ptr(), (size_t)nbytes, cur_stream());
+  }
+  bool ready(int i) {
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    return p_.slot_ready(i);
+  }
+  void wait(int i) {
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    p_.wait_slot(i);
+  }
+  int depth() const { return p_.depth(); }
+  int64_t slot_bytes() const { return bytes_; }
+
+ private:
+  PinnedPrefetcher p_;
+  int64_t bytes_;
+};
+
+// ----------------------------------------------------------------------------
 // LeNet engine: holds every buffer pointer once, launches the fused step, and
 // captures multi-step hipGraphs.
 // ----------------------------------------------------------------------------
@@ -554,8 +656,25 @@ class LeNetEngine {
     graphs_.clear();
   }
 
+  // Data-parallel step (mode & LENET_REDUCE): after the backward kernels, all-reduce the
+  // flat gradient (AVG) over the native communicator and apply the flat optimizer with lr /
+  // step read from device memory -- all inside the same stream (and graph).
+  void set_comm(py::object comm) {
+    if (comm.is_none()) {
+      comm_ = nullptr;
+      comm_keep_ = py::none();
+    } else {
+      comm_ = &comm.cast<PyComm&>().raw();
+      comm_keep_ = comm;
+    }
+    graphs_.clear();
+  }
+
   void check_mode(int mode, int B) const {
     TORCH_CHECK(B > 0 && B <= max_b_, "batch ", B, " outside [1, ", max_b_, "]");
+    TORCH_CHECK(!((mode & LENET_OPT) && (mode & LENET_REDUCE)),
+                "LENET_OPT (fused local update) and LENET_REDUCE (all-reduce + update) are exclusive");
+    if (mode & LENET_REDUCE) TORCH_CHECK(A_.ctrl != nullptr, "ctrl required for the data-parallel update");
     if (mode & (LENET_OPT | LENET_REDUCE)) TORCH_CHECK(O_.g != nullptr, "set_opt() first");
     if (mode & LENET_OPT) TORCH_CHECK(A_.ctrl != nullptr, "ctrl required for the fused optimizer");
     if ((mode & LENET_OPT) && O_.lr_table) TORCH_CHECK(A_.ctrl != nullptr, "lr table needs ctrl");
@@ -563,7 +682,18 @@ class LeNetEngine {
 
   void run(int mode, int B) {
     check_mode(mode, B);
-    launch_lenet(cfg_, mode, B, P_, A_, O_, cur_stream());
+    launch_step(cfg_, mode, B, P_, A_, O_, comm_, cur_stream());
+  }
+
+  static void launch_step(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                          Communicator* comm, hipStream_t s) {
+    launch_lenet(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
+    if (mode & LENET_REDUCE) {
+      if (comm && comm->size() > 1) comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
+      // ctrl[0] = steps taken (already advanced by the backward kernel) -> Adam t; ctrl[1] -> lr table index
+      launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
+                        nullptr, nullptr, s);
+    }
   }
 
   // Capture `nsteps` consecutive steps (the device step counter advances inside)
@@ -577,8 +707,9 @@ class LeNetEngine {
     const LeNetAug A = A_;
     const LeNetOpt O = O_;
     const int cfg = cfg_;
+    Communicator* comm = comm_;
     g->capture([&](hipStream_t s) {
-      for (int i = 0; i < nsteps; ++i) launch_lenet(cfg, mode, B, P, A, O, s);
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, s);
     });
     graphs_[key(mode, B, nsteps)] = std::move(g);
   }
@@ -609,6 +740,8 @@ class LeNetEngine {
   LeNetOpt O_{};
   std::vector<Tensor> keep_, aug_keep_, opt_keep_;
   Tensor ctrl_keep_;
+  Communicator* comm_ = nullptr;
+  py::object comm_keep_ = py::none();
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
 };
 
@@ -644,9 +777,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  py::class_<PyComm>(m, "Communicator")
+      .def(py::init<py::bytes, int, int, int>(), py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
+           py::arg("device"))
+      .def_static("unique_id", &PyComm::unique_id)
+      .def_property_readonly("rank", &PyComm::rank)
+      .def_property_readonly("size", &PyComm::size)
+      .def("all_reduce", &PyComm::all_reduce, py::arg("tensor"), py::arg("op") = "sum")
+      .def("reduce_scatter", &PyComm::reduce_scatter, py::arg("input"), py::arg("output"), py::arg("op") = "sum")
+      .def("all_gather", &PyComm::all_gather, py::arg("input"), py::arg("output"))
+      .def("broadcast", &PyComm::broadcast, py::arg("tensor"), py::arg("root") = 0)
+      .def("all_to_all", &PyComm::all_to_all, py::arg("input"), py::arg("output"))
+      .def("async_error", &PyComm::async_error)
+      .def("abort", &PyComm::abort);
+  py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
+      .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
+      .def("slot", &PyPrefetcher::slot)
+      .def("copy_to_device", &PyPrefetcher::copy_to_device)
+      .def("ready", &PyPrefetcher::ready)
+      .def("wait", &PyPrefetcher::wait)
+      .def_property_readonly("depth", &PyPrefetcher::depth)
+      .def_property_readonly("slot_bytes", &PyPrefetcher::slot_bytes);
   py::class_<LeNetEngine>(m, "LeNetEngine")
       .def(py::init<int, int, py::dict>())
       .def("set_aug", &LeNetEngine::set_aug)
+      .def("set_comm", &LeNetEngine::set_comm)
       .def("clear_aug", &LeNetEngine::clear_aug)
       .def("set_ctrl", &LeNetEngine::set_ctrl)
       .def("set_opt", &LeNetEngine::set_opt)

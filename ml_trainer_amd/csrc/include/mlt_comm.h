@@ -1,0 +1,46 @@
+// Native RCCL communicator (one process per GPU, xGMI inside the node).
+//
+// Replaces the reference's SMDDP backend (src/trainer.py:43-44,59): the
+// unique id is generated on rank 0 and distributed by the caller (Python passes it
+// through the torch.distributed store); collectives are enqueued on any HIP stream, so
+// they can be captured into a hipGraph together with the compute of a training step
+// (the LeNet engine's multi-step graphs contain the gradient all-reduce).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+
+namespace mlt {
+
+enum class CommDtype { F32 = 0, BF16 = 1, F16 = 2, I32 = 3, I64 = 4, U8 = 5 };
+enum class CommOp { SUM = 0, AVG = 1, MAX = 2, MIN = 3 };
+
+class Communicator {
+ public:
+  static std::string unique_id();  // NCCL_UNIQUE_ID_BYTES opaque bytes
+  Communicator(const std::string& uid, int nranks, int rank, int device);
+  ~Communicator();
+  Communicator(const Communicator&) = delete;
+  Communicator& operator=(const Communicator&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  int device() const { return device_; }
+
+  void all_reduce(const void* send, void* recv, size_t count, CommDtype dt, CommOp op, hipStream_t st);
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, CommDtype dt, CommOp op, hipStream_t st);
+  void all_gather(const void* send, void* recv, size_t send_count, CommDtype dt, hipStream_t st);
+  void broadcast(const void* send, void* recv, size_t count, CommDtype dt, int root, hipStream_t st);
+  void all_to_all(const void* send, void* recv, size_t count_per_peer, CommDtype dt, hipStream_t st);
+  // ncclCommGetAsyncError; returns "" when healthy
+  std::string async_error() const;
+  void abort();
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int nranks_ = 0, rank_ = 0, device_ = 0;
+};
+
+}  // namespace mlt

@@ -10,10 +10,13 @@ zero_grad -> H2D -> forward -> CE -> loss.item() -> backward (DDP all-reduce)
   multi-step hipGraph, so the host submits one graph per ``steps_per_graph``
   steps and never synchronises inside an epoch (B12: no ``loss.item()``, no
   sklearn host round trip per batch);
-* W > 1: graph(K1..K5 + conv1 partial reduce) -> RCCL all-reduce (AVG) of the
-  flat gradient buffer (one 248 KB bucket; latency-bound, so a single
-  collective) -> fused flat optimizer launch that reads lr/step from device
-  memory.
+* W > 1: K1..K5 -> RCCL all-reduce (AVG) of the flat gradient buffer (one
+  248 KB bucket; latency-bound, so a single collective) -> fused flat optimizer
+  launch that reads lr/step from device memory. With the native communicator
+  (parallel/comm.py) the all-reduce is enqueued by C++ on the capture stream, so
+  multi-step hipGraphs contain compute, collective and update of every step and
+  the host is out of the loop exactly as at W = 1; without it (MLT_NATIVE_COMM=0)
+  each step is graph(K1..K5) + torch.distributed all-reduce + optimizer launch.
 
 The device step counter ``ctrl`` (``[global_step, step_in_epoch]``) drives
 batch selection from the epoch permutation, the augmentation RNG, the lr table
@@ -61,6 +64,17 @@ class LeNetStepEngine:
         self.eng = C.LeNetEngine(model.cfg_id, self.max_batch, bufs)
         self.eng.set_ctrl(self.ctrl)
         self.offsets = [flat.segment(p)[0] for p in params]
+        self.comm = None
+        if self.world_size > 1:
+            from ml_trainer_amd.parallel.comm import create_native_comm
+            try:
+                self.comm = create_native_comm(process_group, self.device)
+            except RuntimeError as e:  # RCCL bring-up failed: keep the torch.distributed path
+                import warnings
+                warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
+                self.comm = None
+            if self.comm is not None:
+                self.eng.set_comm(self.comm)
         self.optimizer = None
         self.lr_table: Optional[torch.Tensor] = None
         self._use_table = False
@@ -127,15 +141,21 @@ class LeNetStepEngine:
     def fused(self) -> bool:
         return self.world_size == 1
 
+    @property
+    def in_graph_collective(self) -> bool:
+        return self.comm is not None
+
     def _train_mode(self) -> int:
         C = self.C
         base = C.LENET_FWD | C.LENET_CE | C.LENET_BWD
-        return base | (C.LENET_OPT if self.fused else 0)
+        if self.fused:
+            return base | C.LENET_OPT
+        return base | (C.LENET_REDUCE if self.in_graph_collective else 0)
 
     def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8) -> None:
         """Run ``n`` full training steps of batch ``B`` from the device dataset."""
         mode = self._train_mode()
-        if self.fused:
+        if self.fused or self.in_graph_collective:
             if not use_graph:
                 for _ in range(n):
                     self.eng.run(mode, B)
@@ -203,6 +223,9 @@ class LeNetStepEngine:
             if self.fused:
                 self.eng.run(mode, B)
             else:
-                self._dist_step(mode, B, use_graph=False)
+                if self.in_graph_collective:
+                    self.eng.run(self._train_mode(), B)
+                else:
+                    self._dist_step(mode, B, use_graph=False)
         else:
             self.eng.run(C.LENET_FWD | C.LENET_CE, B)

@@ -259,3 +259,66 @@ def test_engine_graph_training_converges(dev):
             first = loss
     assert loss < first * 0.7, (first, loss)
     assert int(eng.ctrl[0]) == 4 * steps
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adamw"])
+def test_engine_reduce_mode_matches_fused(dev, opt):
+    """The data-parallel step layout (backward kernels -> [all-reduce] -> flat optimizer launch,
+    LENET_REDUCE) at world size 1 must reproduce the fused in-kernel update, graphs included."""
+    from ml_trainer_amd.utils.flat import FlatParams
+    N = 512
+    data, targets = _toy_data(N, 3)
+    ms = [_mk("default", 5).to(dev) for _ in range(2)]
+    engs = [_engine(m, opt)[0] for m in ms]
+    for e in engs:
+        e.set_dataset(data, targets, batch_size=32)
+        e.start_epoch(torch.arange(N))
+    C = engs[0].C
+    base = C.LENET_FWD | C.LENET_CE | C.LENET_BWD
+    engs[0].train_steps(32, 8, use_graph=True, steps_per_graph=4)  # fused update (LENET_OPT)
+    e1 = engs[1]
+    e1.eng.capture(base | C.LENET_REDUCE, 32, 4)
+    e1.eng.replay(base | C.LENET_REDUCE, 32, 4)
+    e1.eng.replay(base | C.LENET_REDUCE, 32, 4)
+    torch.cuda.synchronize()
+    assert int(engs[0].ctrl[0]) == int(e1.ctrl[0]) == 8
+    torch.testing.assert_close(e1.flat.data, engs[0].flat.data, rtol=1e-5, atol=1e-6)
+    assert isinstance(e1.flat, FlatParams)
+
+
+def test_native_communicator_single_rank(dev):
+    """RCCL communicator bring-up on one GPU (world size 1): collectives are identities and
+    the ops enqueue on the current stream."""
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    comm = C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index or 0)
+    assert comm.size == 1 and comm.rank == 0
+    t = torch.arange(1000, dtype=torch.float32, device=dev)
+    comm.all_reduce(t, "sum")
+    comm.all_reduce(t, "avg")
+    comm.broadcast(t, 0)
+    out = torch.empty_like(t)
+    comm.all_gather(t, out)
+    comm.reduce_scatter(t, out, "sum")
+    comm.all_to_all(t, out)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(t, torch.arange(1000, dtype=torch.float32, device=dev))
+    torch.testing.assert_close(out, t)
+    tb = torch.ones(64, dtype=torch.bfloat16, device=dev)
+    comm.all_reduce(tb, "sum")
+    torch.cuda.synchronize()
+    assert comm.async_error() == ""
+
+
+def test_pinned_prefetcher(dev):
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    pf = C.PinnedPrefetcher(4096, 3, dev.index or 0)
+    dst = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    for i in range(6):
+        s = pf.slot(i % 3)
+        pf.wait(i % 3)
+        s.fill_(i + 1)
+        pf.copy_to_device(i % 3, dst, 4096)
+        torch.cuda.current_stream().synchronize()
+        assert int(dst[0]) == i + 1 and int(dst[-1]) == i + 1
