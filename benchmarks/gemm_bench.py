@@ -13,10 +13,13 @@ from ml_trainer_amd.ops._ext import require_native  # noqa: E402
 C = require_native()
 dev = torch.device("cuda", 0)
 T = 32 * 512  # tokens of BERT-base at batch 32, seq 512
+T = int(os.environ.get("GEMM_BENCH_TOKENS", T))
 shapes = [  # (name, M, N, K, a_mn, b_mn)
     ("qkv_fwd", T, 2304, 768, 0, 0), ("out_fwd", T, 768, 768, 0, 0), ("ffn1_fwd", T, 3072, 768, 0, 0),
-    ("ffn2_fwd", T, 768, 3072, 0, 0), ("ffn1_dgrad", T, 768, 3072, 0, 1), ("ffn1_wgrad", 3072, 768, T, 1, 1),
-    ("sq4096", 4096, 4096, 4096, 0, 0),
+    ("ffn2_fwd", T, 768, 3072, 0, 0), ("qkv_dgrad", T, 768, 2304, 0, 1), ("ffn1_dgrad", T, 768, 3072, 0, 1),
+    ("ffn2_dgrad", T, 3072, 768, 0, 1), ("qkv_wgrad", 2304, 768, T, 1, 1), ("out_wgrad", 768, 768, T, 1, 1),
+    ("ffn1_wgrad", 3072, 768, T, 1, 1), ("ffn2_wgrad", 768, 3072, T, 1, 1),
+    ("sq4096", 4096, 4096, 4096, 0, 0), ("sq8192", 8192, 8192, 8192, 0, 0),
 ]
 
 
@@ -40,13 +43,18 @@ for name, M, N, K, a_mn, b_mn in shapes:
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     At = A.t() if a_mn else A
     Bt = B if b_mn else B.t()
-    best = {"native": 1e9, "torch": 1e9}
+    plan = C.gemm_plan(bool(a_mn), bool(b_mn), M, N, K)
+    variants = {"native": {}, "legacy128": {"cfg": 0}, "t256x256": {"cfg": 1}, "t256x128": {"cfg": 2},
+                "t128x256": {"cfg": 3}}
+    best = {k: 1e9 for k in list(variants) + ["torch"]}
     for _ in range(3):
-        best["native"] = min(best["native"], timeit(lambda: C.gemm(A, B, out, bool(a_mn), bool(b_mn))))
+        for k, kw in variants.items():
+            best[k] = min(best[k], timeit(lambda: C.gemm(A, B, out, bool(a_mn), bool(b_mn), **kw)))
         best["torch"] = min(best["torch"], timeit(lambda: torch.matmul(At, Bt, out=out)))
     fl = 2.0 * M * N * K
-    r = {"shape": name, "M": M, "N": N, "K": K, "native_ms": round(best["native"], 4),
+    r = {"shape": name, "M": M, "N": N, "K": K, "plan": list(plan), "native_ms": round(best["native"], 4),
          "torch_ms": round(best["torch"], 4), "native_tflops": round(fl / best["native"] / 1e9, 1),
          "torch_tflops": round(fl / best["torch"] / 1e9, 1)}
+    r.update({k + "_tflops": round(fl / best[k] / 1e9, 1) for k in variants if k != "native"})
     res.append(r)
     print(json.dumps(r), flush=True)

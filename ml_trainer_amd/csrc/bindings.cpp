@@ -242,7 +242,7 @@ static const uint16_t* bf16_ptr(const Tensor& t) { return reinterpret_cast<const
 // A, B, C are 2-D (row-major, unit column stride). a_mn / b_mn describe the storage:
 //   A: [M,K] (a_mn=0) or [K,M] (a_mn=1);  B: [N,K] (b_mn=0) or [K,N] (b_mn=1);  C: [M,N].
 void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tensor> bias, c10::optional<Tensor> aux,
-          c10::optional<Tensor> res, double alpha, int mode, bool accumulate) {
+          c10::optional<Tensor> res, double alpha, int mode, bool accumulate, int cfg, int splits) {
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm A/B must be bf16");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm C must be bf16 or fp32");
@@ -282,9 +282,21 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
     ldres = res->stride(0);
   }
   TORCH_CHECK(!accumulate || C.scalar_type() == at::kFloat, "accumulate needs an fp32 output");
-  launch_gemm_bf16(a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M, (int)N,
-                   (int)K, A.stride(0), B.stride(0), C.stride(0), bp, ap, ldaux, rp, ldres, (float)alpha, mode,
-                   accumulate ? 1 : 0, cur_stream());
+  const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
+  Tensor ws, cnt;
+  if (plan.ws_floats > 0) {
+    ws = at::empty({plan.ws_floats}, A.options().dtype(at::kFloat));
+    cnt = at::empty({plan.cnt_ints}, A.options().dtype(at::kInt));
+  }
+  launch_gemm_bf16(plan, a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M,
+                   (int)N, (int)K, A.stride(0), B.stride(0), C.stride(0), bp, ap, ldaux, rp, ldres, (float)alpha, mode,
+                   accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr,
+                   cnt.defined() ? reinterpret_cast<unsigned*>(cnt.data_ptr<int>()) : nullptr, cur_stream());
+}
+
+py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {
+  const GemmPlan p = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
+  return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats);
 }
 
 void colsum(Tensor X, Tensor out, bool accumulate) {
@@ -766,7 +778,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("accuracy", &accuracy);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("a_mn"), py::arg("b_mn"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
-        py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false);
+        py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false, py::arg("cfg") = -1,
+        py::arg("splits") = 0);
+  m.def("gemm_plan", &gemm_plan, py::arg("a_mn"), py::arg("b_mn"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd, py::arg("DY"), py::arg("X"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),

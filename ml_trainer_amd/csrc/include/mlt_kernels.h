@@ -91,10 +91,22 @@ void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t 
 //   a_mn: A stored [K][M] (else [M][K]);  b_mn: B stored [K][N] (else [N][K])
 //   mode: 0 none, 1 GELU (pre-activation written to aux), 2 dGELU (multiply by gelu'(aux))
 // ----------------------------------------------------------------------------
-void launch_gemm_bf16(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M, int N,
-                      int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias, const uint16_t* aux,
-                      int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate,
-                      hipStream_t st);
+// Kernel choice per shape: cfg 0 = 128x128 register-staged kernel (any K % 8 == 0), cfg 1..3 =
+// 256x256 / 256x128 / 128x256 global_load_lds kernels (K % 64 == 0) with optional split-K
+// (deterministic in-launch slab reduction; needs ws_floats of fp32 workspace and cnt_ints
+// zero-initialised tile counters, both provided by the caller).
+struct GemmPlan {
+  int cfg;
+  int splits;
+  int ksteps;  // K-steps (of 64) per split
+  int64_t ws_floats;
+  int64_t cnt_ints;
+};
+GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits);
+void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
+                      void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
+                      const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
+                      int accumulate, float* ws, unsigned* cnt, hipStream_t st);
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,
                         hipStream_t st);

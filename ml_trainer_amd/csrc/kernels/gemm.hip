@@ -26,6 +26,7 @@
 // vectors, fusing bias, GELU (saving the pre-activation), dGELU, residual add and
 // accumulate-into-output.
 #include "mlt_common.h"
+#include "mlt_gemm.h"
 #include "mlt_kernels.h"
 
 namespace mlt {
@@ -36,13 +37,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64, G_THREADS = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KB per operand tile
-
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
 
 // ---- global -> register staging ------------------------------------------------
 // k-contiguous tile: rows r in [0,128), 8 chunks of 8 bf16 per row; 1024 chunks, 4 per thread.
@@ -103,16 +97,6 @@ __device__ __forceinline__ bf16x8 frag_mn(const uint8_t* lds, int mn, int kh) {
   const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
-
-struct GemmEpi {
-  const float* bias;     // [N] or nullptr
-  const uint16_t* aux;   // GELU: pre-activation output (written); DGELU: pre-activation input (read)
-  const uint16_t* res;   // residual [M,N] bf16 (added) or nullptr
-  int64_t ldaux, ldres;
-  float alpha;
-  int mode;              // 0 none, 1 gelu (writes aux), 2 dgelu (reads aux)
-  int accumulate;        // C += result (fp32 output only)
-};
 
 template <bool AM, bool BN, typename OutT>
 __global__ __launch_bounds__(G_THREADS, 2) void gemm_bf16_kernel(const uint16_t* __restrict__ A,
@@ -178,7 +162,6 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_bf16_kernel(const uint16_t*
 #undef AS
 #undef BS
   // ---- epilogue: registers (alpha, bias) -> LDS tile -> 16-byte vector stores (+aux ops) ----
-  constexpr bool F32 = sizeof(OutT) == 4;
   float* cs = reinterpret_cast<float*>(smem);  // [128][128] fp32 staging (64 KB)
   const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -200,56 +183,9 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_bf16_kernel(const uint16_t*
     const int row = e >> 5, c4 = (e & 31) * 4;
     const int gm = m0 + row, gn = n0 + c4;
     if (gm >= M || gn >= N) continue;
-    float4 v = *reinterpret_cast<const float4*>(cs + row * 128 + c4);
+    const float4 v = *reinterpret_cast<const float4*>(cs + row * 128 + c4);
     float vv[4] = {v.x, v.y, v.z, v.w};
-    const bool full = gn + 4 <= N;
-    if (epi.mode == 1) {  // GELU: keep the pre-activation for the backward pass
-      uint16_t* aux = const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (full || gn + q < N) aux[q] = f32_to_bf16(vv[q]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) vv[q] = gelu_f(bf16_to_f32(f32_to_bf16(vv[q])));
-    } else if (epi.mode == 2) {
-      const uint16_t* aux = epi.aux + (int64_t)gm * epi.ldaux + gn;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (full || gn + q < N) vv[q] *= gelu_grad(bf16_to_f32(aux[q]));
-    }
-    if (epi.res) {
-      const uint16_t* rp = epi.res + (int64_t)gm * epi.ldres + gn;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (full || gn + q < N) vv[q] += bf16_to_f32(rp[q]);
-    }
-    OutT* cp = C + (int64_t)gm * ldc + gn;
-    if (F32) {
-      float* fp = reinterpret_cast<float*>(cp);
-      if (full && (((uintptr_t)fp) & 15) == 0) {
-        float4 o = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        if (epi.accumulate) {
-          const float4 old = *reinterpret_cast<float4*>(fp);
-          o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
-        }
-        *reinterpret_cast<float4*>(fp) = o;
-      } else {
-        for (int q = 0; q < 4; ++q)
-          if (gn + q < N) fp[q] = epi.accumulate ? fp[q] + vv[q] : vv[q];
-      }
-    } else {
-      uint16_t* hp = reinterpret_cast<uint16_t*>(cp);
-      if (full && (((uintptr_t)hp) & 7) == 0) {
-        ushort4 o;
-        o.x = f32_to_bf16(vv[0]);
-        o.y = f32_to_bf16(vv[1]);
-        o.z = f32_to_bf16(vv[2]);
-        o.w = f32_to_bf16(vv[3]);
-        *reinterpret_cast<ushort4*>(hp) = o;
-      } else {
-        for (int q = 0; q < 4; ++q)
-          if (gn + q < N) hp[q] = f32_to_bf16(vv[q]);
-      }
-    }
+    epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
   }
 }
 
@@ -268,12 +204,9 @@ static void launch_one(const uint16_t* A, const uint16_t* B, OutT* C, int M, int
                      ldb, ldc, e);
 }
 
-void launch_gemm_bf16(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M, int N,
-                      int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias, const uint16_t* aux,
-                      int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate,
-                      hipStream_t st) {
+void launch_gemm_bf16_128(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M,
+                          int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate};
 #define MLT_GEMM_CASE(AMV, BNV)                                                                          \
   if (a_mn == AMV && b_mn == BNV) {                                                                      \
     if (out_f32)                                                                                         \

@@ -1,0 +1,362 @@
+// Large-tile bf16 GEMM for gfx950: 512 threads (8 waves), 256x256 / 256x128 / 128x256 block
+// tiles, BK = 64, operands staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR round
+// trip, 16 B per lane per instruction) into two LDS buffers: tile k+1's DMA is issued before
+// the MFMAs of tile k and retired by the one barrier per K-step
+// (cdna_hip_programming.md §5 "glds vs register staging": the 256^2, ~1 block/CU regime).
+//
+// LDS images are lane-linear (a glds writes base + lane*16), so the bank-conflict swizzle is
+// applied to the per-lane SOURCE address and undone on the read (rule 21):
+//   k-contiguous operand  [rows][64 k]  : position p of row r holds 16-B chunk p ^ (r & 7)
+//   mn-contiguous operand [64 k][BM|BN] : position p of k-row kk holds chunk p ^ (kk & 15)
+// and fragments are read with ds_read_b128 (k-contiguous) or the gfx950 transpose read
+// ds_read_b64_tr_b16 (mn-contiguous: dgrad / wgrad operands need no transpose pass).
+//
+// M / N tails: source rows / columns are clamped into the matrix (garbage lands only in
+// output rows / columns >= M / N, which are never stored); K must be a multiple of 64.
+//
+// Split-K (gridDim.y = splits): each split writes its fp32 accumulators to a workspace slab
+// in fragment order (coalesced 16-B stores), publishes with an agent-scope release and a
+// relaxed ticket; the last arriver (acquire) sums the slabs in split order -- deterministic
+// for any arrival order and any XCD placement -- and runs the fused epilogue
+// (§5 "Projection GEMM" item 2; §6 Guideline 16).
+//
+// Epilogue: each wave stages 64-row halves of its sub-tile through a padded LDS image and
+// writes 4 consecutive columns per lane (bias, GELU / dGELU, residual, accumulate fused).
+#include "mlt_common.h"
+#include "mlt_gemm.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int T_BK = 64, T_NT = 512;
+constexpr int T_EPI_STRIDE = 68;                          // padded fp32 row of the epilogue image
+constexpr int T_EPI_BYTES = 8 * 64 * T_EPI_STRIDE * 4;    // 8 waves x 64 rows
+
+template <int BM, int BN>
+struct TileGeom {
+  static constexpr int A_BYTES = BM * T_BK * 2, B_BYTES = BN * T_BK * 2, BUF = A_BYTES + B_BYTES;
+  static constexpr int SMEM = 2 * BUF > T_EPI_BYTES ? 2 * BUF : T_EPI_BYTES;
+};
+
+// ---- fragments --------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 tfrag_k(const uint8_t* lds, int row, int kh) {
+  const int lane = threadIdx.x & 63;
+  const int r = row + (lane & 15), c = kh * 4 + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
+}
+template <int RB>  // row bytes of the mn-contiguous image (2 * BM or 2 * BN)
+__device__ __forceinline__ bf16x8 tfrag_mn(const uint8_t* lds, int mn, int kh) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = mn + 4 * p;
+  const int c = col >> 3, half = (col & 7) * 2;
+  const int k0 = kh * 32 + 8 * g + q, k1 = k0 + 4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ (k0 & 15)) << 4) + half));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ (k1 & 15)) << 4) + half));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// ---- per-thread glds sources -----------------------------------------------------------
+// Chunk e = i * 512 + threadIdx.x of an operand image lands at LDS byte e * 16.
+template <int ROWS, bool MN>  // ROWS = extent of the operand's M (or N) side of the tile
+__device__ __forceinline__ const uint16_t* glds_src(const uint16_t* __restrict__ base, int64_t ld, int i, int mn0,
+                                                    int nmn) {
+  const int e = i * T_NT + threadIdx.x;
+  if (!MN) {  // [ROWS][64 k]: 8 chunks per row
+    const int r = e >> 3, p = e & 7, c = p ^ (r & 7);
+    const int row = min(mn0 + r, nmn - 1);
+    return base + (int64_t)row * ld + c * 8;
+  } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row
+    constexpr int CPR = ROWS / 8;
+    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & 15);
+    const int col = min(mn0 + c * 8, nmn - 8);
+    return base + (int64_t)kk * ld + col;
+  }
+}
+
+template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT>
+__global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __restrict__ A,
+                                                             const uint16_t* __restrict__ B, OutT* __restrict__ C,
+                                                             int M, int N, int K, int64_t lda, int64_t ldb,
+                                                             int64_t ldc, GemmEpi epi, float* __restrict__ ws,
+                                                             unsigned* __restrict__ cnt, int ksteps) {
+  using G = TileGeom<BM, BN>;
+  constexpr int WARPS_N = 8 / WARPS_M, WTM = BM / WARPS_M, WTN = BN / WARPS_N, TI = WTM / 16, TJ = WTN / 16;
+  constexpr int A_CH = G::A_BYTES / 16 / T_NT, B_CH = G::B_BYTES / 16 / T_NT;
+  static_assert(WTN == 64, "epilogue image assumes 64-column wave tiles");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
+  const int id = xcd_remap(blockIdx.x, tiles);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = (wid / WARPS_N) * WTM, wn = (wid % WARPS_N) * WTN;
+  const int nk = K / T_BK;
+  const int kt0 = blockIdx.y * ksteps, kt1 = min(nk, kt0 + ksteps);
+
+  const uint16_t* asrc[A_CH];
+  const uint16_t* bsrc[B_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) asrc[i] = glds_src<BM, AM>(A, lda, i, m0, M);
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) bsrc[i] = glds_src<BN, BNL>(B, ldb, i, n0, N);
+  const int64_t astep = AM ? (int64_t)T_BK * lda : T_BK, bstep = BNL ? (int64_t)T_BK * ldb : T_BK;
+
+  auto stage = [&](int buf, int kt) {
+    uint8_t* base = smem + buf * G::BUF;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kt * astep),
+                                       (lds_void*)(base + (i * T_NT + wid * 64) * 16), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kt * bstep),
+                                       (lds_void*)(base + G::A_BYTES + (i * T_NT + wid * 64) * 16), 16, 0, 0);
+  };
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) stage(0, kt0);
+  __syncthreads();  // waits the DMA (vmcnt(0)) and publishes buffer 0
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
+    const uint8_t* As = smem + cur * G::BUF;
+    const uint8_t* Bs = As + G::A_BYTES;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8 bfr[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = BNL ? tfrag_mn<2 * BN>(Bs, wn + 16 * j, kh) : tfrag_k(Bs, wn + 16 * j, kh);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const bf16x8 af = AM ? tfrag_mn<2 * BM>(As, wm + 16 * i, kh) : tfrag_k(As, wm + 16 * i, kh);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // retires tile kt+1's DMA and frees buffer `cur` for tile kt+2
+  }
+
+  // ---- split-K: slab publish / last-arriver reduction --------------------------------------
+  if (gridDim.y > 1) {
+    constexpr int SLAB = BM * BN;
+    float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        *reinterpret_cast<f32x4*>(slab + ((int64_t)wid * TI * TJ * 64 + lane) * 4 + (i * TJ + j) * 256) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(cnt + id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == gridDim.y - 1;
+      if (last) __hip_atomic_store(cnt + id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // sum the slabs in split order (own slab re-read: same order whoever arrives last)
+    const int64_t fo = ((int64_t)wid * TI * TJ * 64 + lane) * 4;
+    {
+      const float* sl = ws + (int64_t)id * SLAB + fo;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = *reinterpret_cast<const f32x4*>(sl + (i * TJ + j) * 256);
+    }
+    for (int z = 1; z < (int)gridDim.y; ++z) {
+      const float* sl = ws + ((int64_t)z * tiles + id) * SLAB + fo;
+      f32x4 v[TI][TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) v[i][j] = *reinterpret_cast<const f32x4*>(sl + (i * TJ + j) * 256);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += v[i][j];
+    }
+  }
+
+  // ---- epilogue ----------------------------------------------------------------------------
+  const int g = lane >> 4, cl = lane & 15;
+  float* cs = reinterpret_cast<float*>(smem) + wid * (64 * T_EPI_STRIDE);
+  float bv[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int gn = n0 + wn + 16 * j + cl;
+    bv[j] = (epi.bias && gn < N) ? epi.bias[gn] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < TI / 4; ++h) {
+    __syncthreads();  // LDS free (main loop / previous half)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(16 * ii + 4 * g + r) * T_EPI_STRIDE + 16 * j + cl] = acc[4 * h + ii][j][r] * epi.alpha + bv[j];
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int e = it * 64 + lane, row = e >> 4, c4 = (e & 15) * 4;
+      const int gm = m0 + wm + 64 * h + row, gn = n0 + wn + c4;
+      if (gm >= M || gn >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(cs + row * T_EPI_STRIDE + c4);
+      float vv[4] = {v.x, v.y, v.z, v.w};
+      epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host: planning + dispatch
+// ---------------------------------------------------------------------------------------------
+void launch_gemm_bf16_128(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M,
+                          int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, hipStream_t st);
+
+namespace {
+constexpr int kCUs = 256;
+struct CfgDesc {
+  int bm, bn;
+  double rate;  // sustained FLOP/s per CU (relative model, measured ordering)
+  int per_cu;   // resident blocks per CU
+};
+const CfgDesc kCfg[4] = {{128, 128, 0.55e15 / kCUs, 2},
+                         {256, 256, 1.10e15 / kCUs, 1},
+                         {256, 128, 0.95e15 / kCUs, 1},
+                         {128, 256, 0.95e15 / kCUs, 1}};
+
+double est_time(int cfg, int splits, int M, int N, int K) {
+  const CfgDesc& c = kCfg[cfg];
+  const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+  const int64_t blocks = tiles * splits;
+  const int64_t slots = (int64_t)kCUs * c.per_cu;
+  const int64_t rounds = (blocks + slots - 1) / slots;
+  const int nk = (K + 63) / 64, ks = (nk + splits - 1) / splits;
+  const double t_block = 2.0 * c.bm * c.bn * 64.0 * ks / (c.rate / c.per_cu) + 1.0e-6;
+  double t = rounds * t_block;
+  if (splits > 1) t += (double)tiles * splits * c.bm * c.bn * 4.0 * 2.0 / 4.0e12 + 2.0e-6;
+  return t;
+}
+}  // namespace
+
+GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
+  (void)a_mn;
+  (void)b_mn;
+  GemmPlan p{0, 1, 0, 0, 0};
+  const bool big_ok = K % 64 == 0 && K >= 64 && M >= 64 && N >= 64;
+  int best_cfg = 0, best_s = 1;
+  if (force_cfg >= 0) {
+    best_cfg = (force_cfg >= 1 && force_cfg <= 3 && big_ok) ? force_cfg : 0;
+    best_s = best_cfg ? (force_splits > 0 ? force_splits : 1) : 1;
+  } else if (big_ok) {
+    double best = est_time(0, 1, M, N, K);
+    const int nk = K / 64;
+    for (int cfg = 1; cfg <= 3; ++cfg)
+      for (int s : {1, 2, 3, 4, 6, 8, 12, 16}) {
+        if (s > nk) break;
+        const int ks = (nk + s - 1) / s;
+        if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
+        if (s > 1 && ks < 4) continue;
+        const double t = est_time(cfg, s, M, N, K);
+        if (t < best * 0.97) {
+          best = t;
+          best_cfg = cfg;
+          best_s = s;
+        }
+      }
+    if (force_splits > 0 && best_cfg) best_s = force_splits;
+  }
+  p.cfg = best_cfg;
+  p.splits = best_s;
+  if (best_cfg) {
+    const int nk = K / 64;
+    if (p.splits > nk) p.splits = nk;
+    p.ksteps = (nk + p.splits - 1) / p.splits;
+    const CfgDesc& c = kCfg[best_cfg];
+    const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    if (p.splits > 1) {
+      p.ws_floats = tiles * p.splits * c.bm * c.bn;
+      p.cnt_ints = tiles;
+    }
+  }
+  return p;
+}
+
+template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT>
+static void launch_tile(const GemmPlan& p, const uint16_t* A, const uint16_t* B, OutT* C, int M, int N, int K,
+                        int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt,
+                        hipStream_t st) {
+  using G = TileGeom<BM, BN>;
+  auto kern = gemm_tile_kernel<BM, BN, WARPS_M, AM, BNL, OutT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    attr_set = true;
+  }
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (p.splits > 1) (void)hipMemsetAsync(cnt, 0, sizeof(unsigned) * tiles, st);
+  hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), G::SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws,
+                     cnt, p.ksteps);
+}
+
+template <bool AM, bool BNL, typename OutT>
+static void launch_cfg(const GemmPlan& p, const uint16_t* A, const uint16_t* B, OutT* C, int M, int N, int K,
+                       int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt,
+                       hipStream_t st) {
+  switch (p.cfg) {
+    case 1: launch_tile<256, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 2: launch_tile<256, 128, 4, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 3: launch_tile<128, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    default: break;
+  }
+}
+
+void launch_gemm_bf16(const GemmPlan& p, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
+                      void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
+                      const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
+                      int accumulate, float* ws, unsigned* cnt, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate};
+  if (p.cfg == 0) {
+    launch_gemm_bf16_128(a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, e, st);
+    return;
+  }
+#define MLT_TILE_CASE(AMV, BNV)                                                                                  \
+  if (a_mn == AMV && b_mn == BNV) {                                                                              \
+    if (out_f32)                                                                                                 \
+      launch_cfg<AMV, BNV, float>(p, A, B, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);                   \
+    else                                                                                                         \
+      launch_cfg<AMV, BNV, uint16_t>(p, A, B, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);             \
+    return;                                                                                                      \
+  }
+  MLT_TILE_CASE(0, 0)
+  MLT_TILE_CASE(0, 1)
+  MLT_TILE_CASE(1, 0)
+  MLT_TILE_CASE(1, 1)
+#undef MLT_TILE_CASE
+}
+
+}  // namespace mlt

@@ -74,7 +74,65 @@ def test_epilogues(dev):
 
 def test_colsum(dev):
     C = require_native()
-    X = torch.randn(1000, 300, device=dev).to(torch.bfloat16)
-    out = torch.zeros(300, device=dev)
+    X = torch.randn(1000, 304, device=dev).to(torch.bfloat16)
+    out = torch.zeros(304, device=dev)
     C.colsum(X, out, False)
     torch.testing.assert_close(out, X.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (1, 3), (2, 4), (3, 2)])
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_tile_kernels(dev, cfg, splits, a_mn, b_mn):
+    """256-wide global_load_lds kernels (gemm_tile.hip), forced config / split-K, with M/N tails
+    and a strided leading dimension, vs the fp32 reference; epilogues on the split-K path."""
+    C = require_native()
+    M, N, K = 328, 264, 768
+    g = torch.Generator().manual_seed(cfg * 100 + splits * 10 + a_mn * 2 + b_mn)
+    A = _mk((K, M + 8) if a_mn else (M, K + 64), dev, g)
+    A = A[:, :M] if a_mn else A[:, :K]
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    ref = _ref(A, B, a_mn, b_mn)
+    plan = C.gemm_plan(bool(a_mn), bool(b_mn), M, N, K, cfg, splits)
+    assert plan[0] == cfg and plan[1] == splits
+    for out_dtype in (torch.bfloat16, torch.float32):
+        out = torch.empty(M, N, dtype=out_dtype, device=dev)
+        C.gemm(A, B, out, bool(a_mn), bool(b_mn), cfg=cfg, splits=splits)
+        tol = 2e-2 if out_dtype == torch.bfloat16 else 2e-3
+        torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * 8)
+    bias = torch.randn(N, device=dev)
+    res = _mk((M, N), dev, g)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, out, bool(a_mn), bool(b_mn), bias=bias, aux=aux, mode=1, cfg=cfg, splits=splits)
+    torch.testing.assert_close(aux.float(), ref + bias, rtol=2e-2, atol=0.15)
+    torch.testing.assert_close(out.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=0.15)
+    C.gemm(A, B, out, bool(a_mn), bool(b_mn), res=res, alpha=0.5, cfg=cfg, splits=splits)
+    torch.testing.assert_close(out.float(), 0.5 * ref + res.float(), rtol=2e-2, atol=0.15)
+    acc = torch.ones(M, N, device=dev)
+    C.gemm(A, B, acc, bool(a_mn), bool(b_mn), accumulate=True, cfg=cfg, splits=splits)
+    torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-2)
+
+
+def test_tile_split_k_deterministic(dev):
+    C = require_native()
+    g = torch.Generator().manual_seed(7)
+    A = _mk((4096, 768), dev, g)   # [K][M]
+    B = _mk((4096, 1024), dev, g)  # [K][N]
+    outs = []
+    for _ in range(3):
+        o = torch.empty(768, 1024, device=dev)
+        C.gemm(A, B, o, True, True, cfg=1, splits=8)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    torch.testing.assert_close(outs[0], A.float().t() @ B.float(), rtol=2e-3, atol=2e-2)
+
+
+def test_identity_asymmetric_tile(dev):
+    C = require_native()
+    M = 256
+    A = torch.eye(M, dtype=torch.bfloat16, device=dev)
+    B = (torch.arange(M * 128, device=dev).view(128, M) % 251).to(torch.bfloat16)
+    for cfg in (1, 2, 3):
+        out = torch.empty(M, 128, dtype=torch.float32, device=dev)
+        C.gemm(A, B, out, False, False, cfg=cfg)
+        torch.testing.assert_close(out, B.float().t())
