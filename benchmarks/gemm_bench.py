@@ -44,7 +44,7 @@ for name, M, N, K, a_mn, b_mn in shapes:
     At = A.t() if a_mn else A
     Bt = B if b_mn else B.t()
     plan = C.gemm_plan(bool(a_mn), bool(b_mn), M, N, K)
-    variants = {"native": {}, "legacy128": {"cfg": 0}, "t256x256": {"cfg": 1}, "t256x128": {"cfg": 2},
+    variants = {"native": {}, "legacy128": {"cfg": 0}, "t256x256": {"cfg": 1}, "t256x128": {"cfg": 2}, "t256x192": {"cfg": 4},
                 "t128x256": {"cfg": 3}}
     best = {k: 1e9 for k in list(variants) + ["torch"]}
     for _ in range(3):

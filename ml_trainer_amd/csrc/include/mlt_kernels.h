@@ -91,8 +91,8 @@ void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t 
 //   a_mn: A stored [K][M] (else [M][K]);  b_mn: B stored [K][N] (else [N][K])
 //   mode: 0 none, 1 GELU (pre-activation written to aux), 2 dGELU (multiply by gelu'(aux))
 // ----------------------------------------------------------------------------
-// Kernel choice per shape: cfg 0 = 128x128 register-staged kernel (any K % 8 == 0), cfg 1..3 =
-// 256x256 / 256x128 / 128x256 global_load_lds kernels (K % 64 == 0) with optional split-K
+// Kernel choice per shape: cfg 0 = 128x128 register-staged kernel (any K % 8 == 0), cfg 1..4 =
+// 256x256 / 256x128 / 128x256 / 256x192 global_load_lds kernels (K % 64 == 0) with split-K
 // (deterministic in-launch slab reduction; needs ws_floats of fp32 workspace and cnt_ints
 // zero-initialised tile counters, both provided by the caller).
 struct GemmPlan {

@@ -1,4 +1,4 @@
-// Large-tile bf16 GEMM for gfx950: 512 threads (8 waves), 256x256 / 256x128 / 128x256 block
+// Large-tile bf16 GEMM for gfx950: 512 threads (8 waves), 256x256 / 256x192 / 256x128 / 128x256 block
 // tiles, BK = 64, operands staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR round
 // trip, 16 B per lane per instruction) into two LDS buffers: tile k+1's DMA is issued before
 // the MFMAs of tile k and retired by the one barrier per K-step
@@ -36,13 +36,22 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int T_BK = 64, T_NT = 512;
-constexpr int T_EPI_STRIDE = 68;                          // padded fp32 row of the epilogue image
-constexpr int T_EPI_BYTES = 8 * 64 * T_EPI_STRIDE * 4;    // 8 waves x 64 rows
 
-template <int BM, int BN>
+// mn-contiguous images XOR-swizzle the 16-B chunk index within aligned groups of 16 (or 8
+// when a k-row holds 24 chunks) so the permutation never leaves the row
+template <int CPR>
+struct MnSwz {
+  static constexpr int MASK = CPR % 16 == 0 ? 15 : 7;
+};
+
+template <int BM, int BN, int WARPS_M>
 struct TileGeom {
   static constexpr int A_BYTES = BM * T_BK * 2, B_BYTES = BN * T_BK * 2, BUF = A_BYTES + B_BYTES;
-  static constexpr int SMEM = 2 * BUF > T_EPI_BYTES ? 2 * BUF : T_EPI_BYTES;
+  static constexpr int WTN = BN / (8 / WARPS_M);
+  static constexpr int EPR = WTN <= 64 ? 64 : 32;        // epilogue rows per pass per wave
+  static constexpr int EPS = WTN + 4;                     // padded fp32 row stride of the image
+  static constexpr int EPI_BYTES = 8 * EPR * EPS * 4;
+  static constexpr int SMEM = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
 };
 
 // ---- fragments --------------------------------------------------------------------------
@@ -53,12 +62,13 @@ __device__ __forceinline__ bf16x8 tfrag_k(const uint8_t* lds, int row, int kh) {
 }
 template <int RB>  // row bytes of the mn-contiguous image (2 * BM or 2 * BN)
 __device__ __forceinline__ bf16x8 tfrag_mn(const uint8_t* lds, int mn, int kh) {
+  constexpr int SW = MnSwz<RB / 16>::MASK;
   const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int col = mn + 4 * p;
   const int c = col >> 3, half = (col & 7) * 2;
   const int k0 = kh * 32 + 8 * g + q, k1 = k0 + 4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ (k0 & 15)) << 4) + half));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ (k1 & 15)) << 4) + half));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ (k0 & SW)) << 4) + half));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ (k1 & SW)) << 4) + half));
   const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
@@ -75,7 +85,7 @@ __device__ __forceinline__ const uint16_t* glds_src(const uint16_t* __restrict__
     return base + (int64_t)row * ld + c * 8;
   } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row
     constexpr int CPR = ROWS / 8;
-    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & 15);
+    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
     const int col = min(mn0 + c * 8, nmn - 8);
     return base + (int64_t)kk * ld + col;
   }
@@ -87,10 +97,11 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
                                                              int M, int N, int K, int64_t lda, int64_t ldb,
                                                              int64_t ldc, GemmEpi epi, float* __restrict__ ws,
                                                              unsigned* __restrict__ cnt, int ksteps) {
-  using G = TileGeom<BM, BN>;
+  using G = TileGeom<BM, BN, WARPS_M>;
   constexpr int WARPS_N = 8 / WARPS_M, WTM = BM / WARPS_M, WTN = BN / WARPS_N, TI = WTM / 16, TJ = WTN / 16;
   constexpr int A_CH = G::A_BYTES / 16 / T_NT, B_CH = G::B_BYTES / 16 / T_NT;
-  static_assert(WTN == 64, "epilogue image assumes 64-column wave tiles");
+  static_assert(A_CH * 16 * T_NT == G::A_BYTES && B_CH * 16 * T_NT == G::B_BYTES, "glds chunking");
+  static_assert(WTM % G::EPR == 0 && (G::EPR * WTN / 4) % 64 == 0, "epilogue geometry");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
@@ -199,8 +210,9 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
   }
 
   // ---- epilogue ----------------------------------------------------------------------------
+  constexpr int EPR = G::EPR, EPS = G::EPS, RI = EPR / 16;
   const int g = lane >> 4, cl = lane & 15;
-  float* cs = reinterpret_cast<float*>(smem) + wid * (64 * T_EPI_STRIDE);
+  float* cs = reinterpret_cast<float*>(smem) + wid * (EPR * EPS);
   float bv[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
@@ -208,22 +220,22 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
     bv[j] = (epi.bias && gn < N) ? epi.bias[gn] : 0.f;
   }
 #pragma unroll
-  for (int h = 0; h < TI / 4; ++h) {
-    __syncthreads();  // LDS free (main loop / previous half)
+  for (int h = 0; h < TI / RI; ++h) {
+    __syncthreads();  // LDS free (main loop / previous pass)
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
+    for (int ii = 0; ii < RI; ++ii)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          cs[(16 * ii + 4 * g + r) * T_EPI_STRIDE + 16 * j + cl] = acc[4 * h + ii][j][r] * epi.alpha + bv[j];
+          cs[(16 * ii + 4 * g + r) * EPS + 16 * j + cl] = acc[RI * h + ii][j][r] * epi.alpha + bv[j];
     __syncthreads();
 #pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int e = it * 64 + lane, row = e >> 4, c4 = (e & 15) * 4;
-      const int gm = m0 + wm + 64 * h + row, gn = n0 + wn + c4;
+    for (int it = 0; it < EPR * WTN / 4 / 64; ++it) {
+      const int e = it * 64 + lane, row = e / (WTN / 4), c4 = (e % (WTN / 4)) * 4;
+      const int gm = m0 + wm + EPR * h + row, gn = n0 + wn + c4;
       if (gm >= M || gn >= N) continue;
-      const float4 v = *reinterpret_cast<const float4*>(cs + row * T_EPI_STRIDE + c4);
+      const float4 v = *reinterpret_cast<const float4*>(cs + row * EPS + c4);
       float vv[4] = {v.x, v.y, v.z, v.w};
       epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
     }
@@ -243,10 +255,12 @@ struct CfgDesc {
   double rate;  // sustained FLOP/s per CU (relative model, measured ordering)
   int per_cu;   // resident blocks per CU
 };
-const CfgDesc kCfg[4] = {{128, 128, 0.55e15 / kCUs, 2},
-                         {256, 256, 1.10e15 / kCUs, 1},
-                         {256, 128, 0.95e15 / kCUs, 1},
-                         {128, 256, 0.95e15 / kCUs, 1}};
+constexpr int kNumCfg = 5;
+const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2},
+                               {256, 256, 1.15e15 / kCUs, 1},
+                               {256, 128, 0.92e15 / kCUs, 1},
+                               {128, 256, 0.92e15 / kCUs, 1},
+                               {256, 192, 1.05e15 / kCUs, 1}};
 
 double est_time(int cfg, int splits, int M, int N, int K) {
   const CfgDesc& c = kCfg[cfg];
@@ -269,12 +283,12 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
   const bool big_ok = K % 64 == 0 && K >= 64 && M >= 64 && N >= 64;
   int best_cfg = 0, best_s = 1;
   if (force_cfg >= 0) {
-    best_cfg = (force_cfg >= 1 && force_cfg <= 3 && big_ok) ? force_cfg : 0;
+    best_cfg = (force_cfg >= 1 && force_cfg < kNumCfg && big_ok) ? force_cfg : 0;
     best_s = best_cfg ? (force_splits > 0 ? force_splits : 1) : 1;
   } else if (big_ok) {
     double best = est_time(0, 1, M, N, K);
     const int nk = K / 64;
-    for (int cfg = 1; cfg <= 3; ++cfg)
+    for (int cfg = 1; cfg < kNumCfg; ++cfg)
       for (int s : {1, 2, 3, 4, 6, 8, 12, 16}) {
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
@@ -309,7 +323,7 @@ template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT>
 static void launch_tile(const GemmPlan& p, const uint16_t* A, const uint16_t* B, OutT* C, int M, int N, int K,
                         int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt,
                         hipStream_t st) {
-  using G = TileGeom<BM, BN>;
+  using G = TileGeom<BM, BN, WARPS_M>;
   auto kern = gemm_tile_kernel<BM, BN, WARPS_M, AM, BNL, OutT>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -330,6 +344,7 @@ static void launch_cfg(const GemmPlan& p, const uint16_t* A, const uint16_t* B, 
     case 1: launch_tile<256, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 2: launch_tile<256, 128, 4, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 3: launch_tile<128, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 4: launch_tile<256, 192, 4, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     default: break;
   }
 }

@@ -80,7 +80,7 @@ def test_colsum(dev):
     torch.testing.assert_close(out, X.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (1, 3), (2, 4), (3, 2)])
+@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (1, 3), (2, 4), (3, 2), (4, 2)])
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_tile_kernels(dev, cfg, splits, a_mn, b_mn):
     """256-wide global_load_lds kernels (gemm_tile.hip), forced config / split-K, with M/N tails
@@ -132,7 +132,7 @@ def test_identity_asymmetric_tile(dev):
     M = 256
     A = torch.eye(M, dtype=torch.bfloat16, device=dev)
     B = (torch.arange(M * 128, device=dev).view(128, M) % 251).to(torch.bfloat16)
-    for cfg in (1, 2, 3):
+    for cfg in (1, 2, 3, 4):
         out = torch.empty(M, 128, dtype=torch.float32, device=dev)
         C.gemm(A, B, out, False, False, cfg=cfg)
         torch.testing.assert_close(out, B.float().t())
