@@ -283,15 +283,11 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
   }
   TORCH_CHECK(!accumulate || C.scalar_type() == at::kFloat, "accumulate needs an fp32 output");
   const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
-  Tensor ws, cnt;
-  if (plan.ws_floats > 0) {
-    ws = at::empty({plan.ws_floats}, A.options().dtype(at::kFloat));
-    cnt = at::empty({plan.cnt_ints}, A.options().dtype(at::kInt));
-  }
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, A.options().dtype(at::kFloat));
   launch_gemm_bf16(plan, a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M,
                    (int)N, (int)K, A.stride(0), B.stride(0), C.stride(0), bp, ap, ldaux, rp, ldres, (float)alpha, mode,
-                   accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr,
-                   cnt.defined() ? reinterpret_cast<unsigned*>(cnt.data_ptr<int>()) : nullptr, cur_stream());
+                   accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
 }
 
 py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {

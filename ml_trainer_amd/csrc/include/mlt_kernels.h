@@ -93,8 +93,8 @@ void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t 
 // ----------------------------------------------------------------------------
 // Kernel choice per shape: cfg 0 = 128x128 register-staged kernel (any K % 8 == 0), cfg 1..4 =
 // 256x256 / 256x128 / 128x256 / 256x192 global_load_lds kernels (K % 64 == 0) with split-K
-// (deterministic in-launch slab reduction; needs ws_floats of fp32 workspace and cnt_ints
-// zero-initialised tile counters, both provided by the caller).
+// (deterministic in-launch slab reduction; needs ws_floats of fp32 workspace from the caller;
+// tile counters come from an internal self-resetting pool when cnt == nullptr).
 struct GemmPlan {
   int cfg;
   int splits;

@@ -21,6 +21,8 @@
 //     dP^T = V dO^T, dS^T lane-local, dQ^T += K^T dS^T with dS^T fed from registers.
 // Global->LDS staging of the next tile is register-staged (loads issued before the MFMA work
 // of the current tile, LDS writes after it), so HBM latency overlaps the math.
+#include <cstdlib>
+
 #include "mlt_common.h"
 #include "mlt_kernels.h"
 
@@ -101,32 +103,52 @@ __device__ __forceinline__ bf16x8 pack_acc(const f32x4& t0, const f32x4& t1) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// 1-D grid of (row block, head, batch) with the XCD-aware remap: the row blocks of one
+// (batch, head) are consecutive after the remap, so they run on one XCD and its L2 serves the
+// K / V (or Q / dO) tiles they all re-read instead of every XCD fetching them from HBM.
+__device__ __forceinline__ void block_coords(int S, int rows_per_block, int H, int& rb, int& h, int& b) {
+  const int nrb = (S + rows_per_block - 1) / rows_per_block;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  rb = id % nrb;
+  h = (id / nrb) % H;
+  b = id / (nrb * H);
+}
+
 // ---------------------------------------------------------------------------
-// forward
+// forward: NQ 16-query groups per wave (the K / V^T fragments read from LDS feed NQ MFMAs)
 // ---------------------------------------------------------------------------
+template <int NQ>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ lens, int S,
                                                        int H, float scale) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[2][AB * 128];
   __shared__ __attribute__((aligned(16))) uint8_t Vs[2][AB * 128];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  block_coords(S, 64 * NQ, H, qb, h, b);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
   const int D = H * AH;
   const int64_t ld = 3 * (int64_t)D;
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
-  const int q = qb * AB + wid * 16 + i;  // this lane's query
-  // Q fragments (B operand of K.Q^T): Q[q][32kh + 8g + j]
-  bf16x8 qf[2];
+  int q[NQ];
+  bf16x8 qf[NQ][2];  // Q fragments (B operand of K.Q^T): Q[q][32kh + 8g + j]
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    qf[kh] = q < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q) * ld + h * AH + kh * 32 + 8 * g)
-                   : bf16x8{};
+  for (int n = 0; n < NQ; ++n) {
+    q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+      qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
+                           : bf16x8{};
   }
-  f32x4 o[4];
+  f32x4 o[NQ][4];
+  float m[NQ], l[NQ];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int n = 0; n < NQ; ++n) {
+    m[n] = -INFINITY;
+    l[n] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int nkb = (len + AB - 1) / AB;
   const float sl2 = scale * 1.4426950408889634f;  // work in base 2
   TileRegs kr, vr;
@@ -143,51 +165,62 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       load_tile(kr, qkv, ld, base + k1, min(AB, S - k1), D + h * AH);
       load_tile(vr, qkv, ld, base + k1, min(AB, S - k1), 2 * D + h * AH);
     }
-    // S^T tiles: rows = keys kt*16 + 4g + r, column = this lane's query
-    f32x4 s[4];
+    // S^T tiles: rows = keys kt*16 + 4g + r, column = query of group n
+    f32x4 s[NQ][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh) s[kt] = mfma(frag_row(Ks[cur], kt * 16, kh), qf[kh], s[kt]);
+      for (int n = 0; n < NQ; ++n) s[n][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const bf16x8 kfr = frag_row(Ks[cur], kt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) s[n][kt] = mfma(kfr, qf[n][kh], s[n][kt]);
+      }
     }
-    float bm = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int n = 0; n < NQ; ++n) {
+      float bm = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * AB + kt * 16 + 4 * g + r;
-        const float v = key < len ? s[kt][r] * sl2 : -INFINITY;
-        s[kt][r] = v;
-        bm = fmaxf(bm, v);
-      }
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    const float mn = fmaxf(m, bm);
-    const float alpha = exp2f(m - mn);  // m = -inf on the first block -> 0
-    float ps = 0.f;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * AB + kt * 16 + 4 * g + r;
+          const float v = key < len ? s[n][kt][r] * sl2 : -INFINITY;
+          s[n][kt][r] = v;
+          bm = fmaxf(bm, v);
+        }
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m[n], bm);
+      const float alpha = exp2f(m[n] - mn);  // m = -inf on the first block -> 0
+      float ps = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kt][r] - mn);
-        s[kt][r] = p;
-        ps += p;
-      }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    l = l * alpha + ps;
-    m = mn;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[n][kt][r] - mn);
+          s[n][kt][r] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l[n] = l[n] * alpha + ps;
+      m[n] = mn;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[n][d] *= alpha;
+    }
     // O^T += V^T . P^T over two 32-key k-steps
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pb = pack_acc(s[2 * ks], s[2 * ks + 1]);
+      bf16x8 pb[NQ];
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) pb[n] = pack_acc(s[n][2 * ks], s[n][2 * ks + 1]);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const bf16x8 va = frag_tr(Vs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
-        o[d] = mfma(va, pb, o[d]);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) o[n][d] = mfma(va, pb[n], o[n][d]);
       }
     }
     if (more) {  // buffer cur^1 was last read before the previous barrier
@@ -196,19 +229,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
     }
     __syncthreads();
   }
-  if (q < S) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    uint16_t* op = out + (base + q) * (int64_t)D + h * AH;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      ushort4 u;  // dims d*16 + 4g + r, r = 0..3
-      u.x = f32_to_bf16(o[d][0] * inv);
-      u.y = f32_to_bf16(o[d][1] * inv);
-      u.z = f32_to_bf16(o[d][2] * inv);
-      u.w = f32_to_bf16(o[d][3] * inv);
-      *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
+  for (int n = 0; n < NQ; ++n) {
+    if (q[n] < S) {
+      const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
+      uint16_t* op = out + (base + q[n]) * (int64_t)D + h * AH;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        ushort4 u;  // dims d*16 + 4g + r, r = 0..3
+        u.x = f32_to_bf16(o[n][d][0] * inv);
+        u.y = f32_to_bf16(o[n][d][1] * inv);
+        u.z = f32_to_bf16(o[n][d][2] * inv);
+        u.w = f32_to_bf16(o[n][d][3] * inv);
+        *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
+      }
+      if (g == 0) lse[((int64_t)b * H + h) * S + q[n]] = m[n] + __log2f(l[n]);  // base-2 LSE of scaled scores
     }
-    if (g == 0) lse[((int64_t)b * H + h) * S + q] = m + __log2f(l);  // base-2 LSE of the scaled scores
   }
 }
 
@@ -237,8 +273,9 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restr
 }
 
 // ---------------------------------------------------------------------------
-// backward, dK / dV: one block per (64-key block, head, batch)
+// backward, dK / dV: one block per (64*NK-key block, head, batch); NK 16-key groups per wave
 // ---------------------------------------------------------------------------
+template <int NK>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
                                                             const uint16_t* __restrict__ dout,
                                                             const float* __restrict__ lse,
@@ -248,16 +285,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
   __shared__ __attribute__((aligned(16))) uint8_t Qs[2][AB * 128];
   __shared__ __attribute__((aligned(16))) uint8_t Os[2][AB * 128];  // dO tiles
   __shared__ float lse_s[2][AB], del_s[2][AB];
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int kbk, h, b;
+  block_coords(S, 64 * NK, H, kbk, h, b);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
   const int D = H * AH;
   const int64_t ld = 3 * (int64_t)D;
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
-  const int key = kb * AB + wid * 16 + i;  // this lane's key
-  if (kb * AB >= len) {  // fully masked key block: zero gradients
-    for (int e = threadIdx.x; e < AB * AH; e += 256) {
-      const int kk = kb * AB + e / AH, d = e % AH;
+  const int k0b = kbk * (64 * NK);
+  if (k0b >= len) {  // fully masked key block: zero gradients
+    for (int e = threadIdx.x; e < 64 * NK * AH; e += 256) {
+      const int kk = k0b + e / AH, d = e % AH;
       if (kk < S) {
         dqkv[(base + kk) * ld + D + h * AH + d] = 0;
         dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
@@ -266,20 +304,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
     return;
   }
   const float sl2 = scale * 1.4426950408889634f;
-  bf16x8 kf[2], vf[2];  // B operands: K[key][32kh + 8g + j], V[key][...]
+  int key[NK];
+  bf16x8 kf[NK][2], vf[NK][2];  // B operands: K[key][32kh + 8g + j], V[key][...]
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    kf[kh] = key < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key) * ld + D + h * AH + kh * 32 + 8 * g)
-                     : bf16x8{};
-    vf[kh] = key < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key) * ld + 2 * D + h * AH + kh * 32 + 8 * g)
-                     : bf16x8{};
-  }
-  f32x4 dk[4], dv[4];  // dK^T / dV^T [d = dt*16 + 4g + r][key = lane]
+  for (int n = 0; n < NK; ++n) {
+    key[n] = k0b + n * 64 + wid * 16 + i;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kh = 0; kh < 2; ++kh) {
+      kf[n][kh] = key[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key[n]) * ld + D + h * AH + kh * 32 + 8 * g)
+                             : bf16x8{};
+      vf[n][kh] = key[n] < S
+                      ? *reinterpret_cast<const bf16x8*>(qkv + (base + key[n]) * ld + 2 * D + h * AH + kh * 32 + 8 * g)
+                      : bf16x8{};
+    }
   }
+  f32x4 dk[NK][4], dv[NK][4];  // dK^T / dV^T [d = dt*16 + 4g + r][key = lane]
+#pragma unroll
+  for (int n = 0; n < NK; ++n)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dk[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   const int nqb = (S + AB - 1) / AB;
   auto stage_stats = [&](int buf, int q0) {
     if (threadIdx.x < AB) {
@@ -301,33 +347,53 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
       load_tile(qr, qkv, ld, base + q1, min(AB, S - q1), h * AH);
       load_tile(orr, dout, (int64_t)D, base + q1, min(AB, S - q1), h * AH);
     }
-    f32x4 p[4], ds[4];  // rows q = qt*16 + 4g + r, column = key (lane)
+    f32x4 p[NK][4], ds[NK][4];  // rows q = qt*16 + 4g + r, column = key (lane)
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 sv[NK], dp[NK];
+#pragma unroll
+      for (int n = 0; n < NK; ++n) {
+        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
-        s = mfma(frag_row(Qs[cur], qt * 16, kh), kf[kh], s);
-        dp = mfma(frag_row(Os[cur], qt * 16, kh), vf[kh], dp);
+        const bf16x8 qa = frag_row(Qs[cur], qt * 16, kh), oa = frag_row(Os[cur], qt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          sv[n] = mfma(qa, kf[n][kh], sv[n]);
+          dp[n] = mfma(oa, vf[n][kh], dp[n]);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = qt * 16 + 4 * g + r;
-        const bool ok = key < len && q0 + ql < S;
-        const float pv = ok ? exp2f(s[r] * sl2 - lse_s[cur][ql]) : 0.f;
-        p[qt][r] = pv;
-        ds[qt][r] = pv * (dp[r] - del_s[cur][ql]);
-      }
+      for (int n = 0; n < NK; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qt * 16 + 4 * g + r;
+          const bool ok = key[n] < len && q0 + ql < S;
+          const float pv = ok ? exp2f(sv[n][r] * sl2 - lse_s[cur][ql]) : 0.f;
+          p[n][qt][r] = pv;
+          ds[n][qt][r] = pv * (dp[n][r] - del_s[cur][ql]);
+        }
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS  (k = queries, two 32-query steps)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pb = pack_acc(p[2 * ks], p[2 * ks + 1]);
-      const bf16x8 sb = pack_acc(ds[2 * ks], ds[2 * ks + 1]);
+      bf16x8 pb[NK], sb[NK];
+#pragma unroll
+      for (int n = 0; n < NK; ++n) {
+        pb[n] = pack_acc(p[n][2 * ks], p[n][2 * ks + 1]);
+        sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
+      }
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        dv[d] = mfma(frag_tr(Os[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), pb, dv[d]);
-        dk[d] = mfma(frag_tr(Qs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), sb, dk[d]);
+        const bf16x8 ot = frag_tr(Os[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+        const bf16x8 qt = frag_tr(Qs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          dv[n][d] = mfma(ot, pb[n], dv[n][d]);
+          dk[n][d] = mfma(qt, sb[n], dk[n][d]);
+        }
       }
     }
     if (more) {
@@ -337,29 +403,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
     }
     __syncthreads();
   }
-  if (key < S) {
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint16_t* kp = dqkv + (base + key) * ld + D + h * AH + d * 16 + 4 * g;
-      uint16_t* vp = dqkv + (base + key) * ld + 2 * D + h * AH + d * 16 + 4 * g;
-      ushort4 uk, uv;
-      uk.x = f32_to_bf16(dk[d][0] * scale);
-      uk.y = f32_to_bf16(dk[d][1] * scale);
-      uk.z = f32_to_bf16(dk[d][2] * scale);
-      uk.w = f32_to_bf16(dk[d][3] * scale);
-      uv.x = f32_to_bf16(dv[d][0]);
-      uv.y = f32_to_bf16(dv[d][1]);
-      uv.z = f32_to_bf16(dv[d][2]);
-      uv.w = f32_to_bf16(dv[d][3]);
-      *reinterpret_cast<ushort4*>(kp) = uk;
-      *reinterpret_cast<ushort4*>(vp) = uv;
+  for (int n = 0; n < NK; ++n) {
+    if (key[n] < S) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint16_t* kp = dqkv + (base + key[n]) * ld + D + h * AH + d * 16 + 4 * g;
+        uint16_t* vp = dqkv + (base + key[n]) * ld + 2 * D + h * AH + d * 16 + 4 * g;
+        ushort4 uk, uv;
+        uk.x = f32_to_bf16(dk[n][d][0] * scale);
+        uk.y = f32_to_bf16(dk[n][d][1] * scale);
+        uk.z = f32_to_bf16(dk[n][d][2] * scale);
+        uk.w = f32_to_bf16(dk[n][d][3] * scale);
+        uv.x = f32_to_bf16(dv[n][d][0]);
+        uv.y = f32_to_bf16(dv[n][d][1]);
+        uv.z = f32_to_bf16(dv[n][d][2]);
+        uv.w = f32_to_bf16(dv[n][d][3]);
+        *reinterpret_cast<ushort4*>(kp) = uk;
+        *reinterpret_cast<ushort4*>(vp) = uv;
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// backward, dQ: one block per (64-query block, head, batch); queries on lanes
+// backward, dQ: one block per (64*NQ-query block, head, batch); queries on lanes
 // ---------------------------------------------------------------------------
+template <int NQ>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                           const uint16_t* __restrict__ dout,
                                                           const float* __restrict__ lse,
@@ -368,26 +438,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
                                                           int S, int H, float scale) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[2][AB * 128];
   __shared__ __attribute__((aligned(16))) uint8_t Vs[2][AB * 128];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  block_coords(S, 64 * NQ, H, qb, h, b);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
   const int D = H * AH;
   const int64_t ld = 3 * (int64_t)D;
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
-  const int q = qb * AB + wid * 16 + i;
   const float sl2 = scale * 1.4426950408889634f;
-  bf16x8 qf[2], of[2];  // B operands: Q[q][32kh + 8g + j], dO[q][...]
+  int q[NQ];
+  bf16x8 qf[NQ][2], of[NQ][2];  // B operands: Q[q][32kh + 8g + j], dO[q][...]
+  float lq[NQ], dl[NQ];
+  f32x4 acc[NQ][4];
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    qf[kh] = q < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q) * ld + h * AH + kh * 32 + 8 * g) : bf16x8{};
-    of[kh] = q < S ? *reinterpret_cast<const bf16x8*>(dout + (base + q) * (int64_t)D + h * AH + kh * 32 + 8 * g)
-                   : bf16x8{};
+  for (int n = 0; n < NQ; ++n) {
+    q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
+                           : bf16x8{};
+      of[n][kh] = q[n] < S
+                      ? *reinterpret_cast<const bf16x8*>(dout + (base + q[n]) * (int64_t)D + h * AH + kh * 32 + 8 * g)
+                      : bf16x8{};
+    }
+    lq[n] = q[n] < S ? lse[((int64_t)b * H + h) * S + q[n]] : 0.f;
+    dl[n] = q[n] < S ? delta[(base + q[n]) * H + h] : 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const float lq = q < S ? lse[((int64_t)b * H + h) * S + q] : 0.f;
-  const float dq_delta = q < S ? delta[(base + q) * H + h] : 0.f;
-  f32x4 acc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nkb = (len + AB - 1) / AB;
   TileRegs kr, vr;
   if (nkb > 0) {
@@ -403,29 +481,45 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
       load_tile(kr, qkv, ld, base + k1, min(AB, S - k1), D + h * AH);
       load_tile(vr, qkv, ld, base + k1, min(AB, S - k1), 2 * D + h * AH);
     }
-    f32x4 ds[4];  // dS^T rows = keys kt*16 + 4g + r, column = this lane's query
+    f32x4 ds[NQ][4];  // dS^T rows = keys kt*16 + 4g + r, column = query of group n
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 sv[NQ], dp[NQ];
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
-        s = mfma(frag_row(Ks[cur], kt * 16, kh), qf[kh], s);
-        dp = mfma(frag_row(Vs[cur], kt * 16, kh), of[kh], dp);
+        const bf16x8 ka = frag_row(Ks[cur], kt * 16, kh), va = frag_row(Vs[cur], kt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          sv[n] = mfma(ka, qf[n][kh], sv[n]);
+          dp[n] = mfma(va, of[n][kh], dp[n]);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * AB + kt * 16 + 4 * g + r;
-        const float pv = key < len ? exp2f(s[r] * sl2 - lq) : 0.f;
-        ds[kt][r] = pv * (dp[r] - dq_delta);
-      }
+      for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * AB + kt * 16 + 4 * g + r;
+          const float pv = key < len ? exp2f(sv[n][r] * sl2 - lq[n]) : 0.f;
+          ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+        }
     }
     // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 sb = pack_acc(ds[2 * ks], ds[2 * ks + 1]);
+      bf16x8 sb[NQ];
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
-        acc[d] = mfma(frag_tr(Ks[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16), sb, acc[d]);
+      for (int n = 0; n < NQ; ++n) sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8 kt = frag_tr(Ks[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[n][d] = mfma(kt, sb[n], acc[n][d]);
+      }
     }
     if (more) {
       store_tile(Ks[cur ^ 1], kr);
@@ -433,24 +527,41 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
     }
     __syncthreads();
   }
-  if (q < S) {
-    uint16_t* qp = dqkv + (base + q) * ld + h * AH;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      ushort4 u;
-      u.x = f32_to_bf16(acc[d][0] * scale);
-      u.y = f32_to_bf16(acc[d][1] * scale);
-      u.z = f32_to_bf16(acc[d][2] * scale);
-      u.w = f32_to_bf16(acc[d][3] * scale);
-      *reinterpret_cast<ushort4*>(qp + d * 16 + 4 * g) = u;
+  for (int n = 0; n < NQ; ++n) {
+    if (q[n] < S) {
+      uint16_t* qp = dqkv + (base + q[n]) * ld + h * AH;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        ushort4 u;
+        u.x = f32_to_bf16(acc[n][d][0] * scale);
+        u.y = f32_to_bf16(acc[n][d][1] * scale);
+        u.z = f32_to_bf16(acc[n][d][2] * scale);
+        u.w = f32_to_bf16(acc[n][d][3] * scale);
+        *reinterpret_cast<ushort4*>(qp + d * 16 + 4 * g) = u;
+      }
     }
   }
+}
+
+// 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
+// MLT_ATTN_FWD_GROUPS / MLT_ATTN_DKDV_GROUPS / MLT_ATTN_DQ_GROUPS = 1|2 override the choice
+// Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dK/dV 1 group (2 groups need
+// > 256 VGPRs and halve the occupancy), dQ 2 groups.
+static int attn_groups(const char* env, int S, int dflt = 2) {
+  const char* v = getenv(env);
+  if (v && (v[0] == '1' || v[0] == '2')) return S >= 128 ? v[0] - '0' : 1;
+  return S >= 128 ? dflt : 1;
 }
 
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* lens, int B, int S, int H,
                      float scale, hipStream_t st) {
   if (B <= 0 || S <= 0) return;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((S + AB - 1) / AB, H, B), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+  const unsigned g2 = (unsigned)((S + 127) / 128 * H * B), g1 = (unsigned)((S + 63) / 64 * H * B);
+  if (attn_groups("MLT_ATTN_FWD_GROUPS", S, 1) == 2)
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
 }
 
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
@@ -459,9 +570,15 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   const int64_t pairs = (int64_t)B * S * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
                      (int64_t)B * S, H);
-  const dim3 grid((S + AB - 1) / AB, H, B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  const dim3 g2((S + 127) / 128 * H * B), g1((S + 63) / 64 * H * B);
+  if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  if (attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
 }
 
 }  // namespace mlt

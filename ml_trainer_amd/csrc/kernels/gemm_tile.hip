@@ -276,6 +276,25 @@ double est_time(int cfg, int splits, int M, int N, int K) {
 }
 }  // namespace
 
+// Split-K tile counters: one zero-initialised device pool (allocated on first use, i.e. in an
+// eager warm-up call, never inside a graph capture), handed out as a ring of slices. Every
+// launch leaves its slice zeroed (the last arriver of each tile resets its counter), so no
+// per-call memset node is needed; a ring of kCntSlices slices keeps split GEMMs that are in
+// flight on different streams apart.
+constexpr int kCntSlices = 16, kCntSlice = 1 << 14;
+unsigned* split_counters(int64_t need) {
+  static unsigned* pool = nullptr;
+  static int next = 0;
+  if (need > kCntSlice) return nullptr;
+  if (!pool) {
+    if (hipMalloc(&pool, sizeof(unsigned) * kCntSlices * kCntSlice) != hipSuccess) return nullptr;
+    if (hipMemset(pool, 0, sizeof(unsigned) * kCntSlices * kCntSlice) != hipSuccess) return nullptr;
+  }
+  unsigned* s = pool + (int64_t)(next % kCntSlices) * kCntSlice;
+  ++next;
+  return s;
+}
+
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
   (void)a_mn;
   (void)b_mn;
@@ -289,7 +308,7 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
     double best = est_time(0, 1, M, N, K);
     const int nk = K / 64;
     for (int cfg = 1; cfg < kNumCfg; ++cfg)
-      for (int s : {1, 2, 3, 4, 6, 8, 12, 16}) {
+      for (int s = 1; s <= 16; ++s) {
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
         if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
@@ -331,7 +350,6 @@ static void launch_tile(const GemmPlan& p, const uint16_t* A, const uint16_t* B,
     attr_set = true;
   }
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (p.splits > 1) (void)hipMemsetAsync(cnt, 0, sizeof(unsigned) * tiles, st);
   hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), G::SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws,
                      cnt, p.ksteps);
 }
@@ -357,6 +375,15 @@ void launch_gemm_bf16(const GemmPlan& p, int a_mn, int b_mn, bool out_f32, const
   GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate};
   if (p.cfg == 0) {
     launch_gemm_bf16_128(a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, e, st);
+    return;
+  }
+  if (p.splits > 1 && cnt == nullptr) cnt = split_counters(p.cnt_ints);
+  if (p.splits > 1 && (cnt == nullptr || ws == nullptr)) {  // no workspace: run unsplit
+    GemmPlan q = p;
+    q.splits = 1;
+    q.ksteps = K / 64;
+    launch_gemm_bf16(q, a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, alpha,
+                     mode, accumulate, nullptr, nullptr, st);
     return;
   }
 #define MLT_TILE_CASE(AMV, BNV)                                                                                  \
