@@ -56,5 +56,12 @@ for name, M, N, K, a_mn, b_mn in shapes:
          "torch_ms": round(best["torch"], 4), "native_tflops": round(fl / best["native"] / 1e9, 1),
          "torch_tflops": round(fl / best["torch"] / 1e9, 1)}
     r.update({k + "_tflops": round(fl / best[k] / 1e9, 1) for k in variants if k != "native"})
+    if not a_mn and not b_mn and K % 128 == 0:  # fp8 e4m3 x e4m3 (MX-scaled MFMA) on the same shape
+        A8 = A.to(torch.float8_e4m3fn)
+        B8 = B.to(torch.float8_e4m3fn)
+        one = torch.ones(1, device=dev)
+        t8 = min(timeit(lambda: C.gemm_f8(A8, B8, out, 0, 0, one, one)) for _ in range(3))
+        r["fp8_tflops"] = round(fl / t8 / 1e9, 1)
+        r["fp8_plan"] = list(C.gemm_f8_plan(M, N, K))
     res.append(r)
     print(json.dumps(r), flush=True)

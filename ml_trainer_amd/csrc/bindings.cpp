@@ -290,6 +290,115 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
                    accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
 }
 
+// ---------------------------------------------------------------------------- fp8
+static bool is_fp8_storage(const Tensor& t) {
+  return t.scalar_type() == at::kByte || t.scalar_type() == at::kFloat8_e4m3fn ||
+         t.scalar_type() == at::kFloat8_e5m2;
+}
+static const uint8_t* u8(const Tensor& t) { return reinterpret_cast<const uint8_t*>(t.data_ptr()); }
+
+void gemm_f8(Tensor A, Tensor B, Tensor C, int fmt_a, int fmt_b, Tensor inv_scale_a, Tensor inv_scale_b,
+             c10::optional<Tensor> bias, c10::optional<Tensor> aux, c10::optional<Tensor> res, double alpha, int mode,
+             bool accumulate, int cfg, int splits) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f8 operands must be 2-D");
+  TORCH_CHECK(is_fp8_storage(A) && is_fp8_storage(B), "gemm_f8 A/B must be fp8 (or uint8) storage");
+  TORCH_CHECK((fmt_a == 0 || fmt_a == 1) && (fmt_b == 0 || fmt_b == 1) && !(fmt_a == 1 && fmt_b == 1),
+              "fp8 formats: 0 = e4m3, 1 = e5m2 (e5m2 x e5m2 not supported)");
+  TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm_f8 C must be bf16 or fp32");
+  for (const Tensor* t : {&A, &B, &C}) {
+    TORCH_CHECK(t->is_cuda() && t->stride(1) == 1, "gemm_f8 operands: device tensors with unit column stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f8 operands must be 16-byte aligned");
+  }
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm_f8 inner dimensions differ");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm_f8 C shape mismatch");
+  TORCH_CHECK(K % 128 == 0 && M >= 64 && N >= 64, "gemm_f8 needs K % 128 == 0 and M, N >= 64");
+  TORCH_CHECK(A.stride(0) % 16 == 0 && B.stride(0) % 16 == 0, "gemm_f8 row strides must be multiples of 16");
+  check_dev(inv_scale_a, "inv_scale_a", at::kFloat, 1, 4);
+  check_dev(inv_scale_b, "inv_scale_b", at::kFloat, 1, 4);
+  const float* bp = nullptr;
+  const uint16_t* ap = nullptr;
+  const uint16_t* rp = nullptr;
+  int64_t ldaux = 0, ldres = 0;
+  if (bias.has_value()) {
+    check_dev(*bias, "bias", at::kFloat, N, 4);
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm mode");
+  if (mode != 0) {
+    TORCH_CHECK(aux.has_value() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
+                    aux->size(1) == N && aux->stride(1) == 1 && aux->is_cuda(), "aux must be bf16 [M,N]");
+    ap = bf16_ptr(*aux);
+    ldaux = aux->stride(0);
+  }
+  if (res.has_value()) {
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->dim() == 2 && res->size(0) == M && res->size(1) == N &&
+                    res->stride(1) == 1 && res->is_cuda(), "res must be bf16 [M,N]");
+    rp = bf16_ptr(*res);
+    ldres = res->stride(0);
+  }
+  TORCH_CHECK(!accumulate || C.scalar_type() == at::kFloat, "accumulate needs an fp32 output");
+  const GemmPlan plan = plan_gemm_f8((int)M, (int)N, (int)K, cfg, splits);
+  TORCH_CHECK(plan.cfg >= 1, "no fp8 GEMM configuration for this shape");
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options().dtype(at::kFloat));
+  launch_gemm_f8(plan, fmt_a, fmt_b, C.scalar_type() == at::kFloat, u8(A), u8(B), C.data_ptr(), (int)M, (int)N,
+                 (int)K, A.stride(0), B.stride(0), C.stride(0), inv_scale_a.data_ptr<float>(),
+                 inv_scale_b.data_ptr<float>(), bp, ap, ldaux, rp, ldres, (float)alpha, mode, accumulate ? 1 : 0,
+                 ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
+}
+
+void fp8_cast(Tensor x, Tensor y, Tensor scale, c10::optional<Tensor> amax, int fmt) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "fp8_cast x: contiguous bf16/fp32 device tensor");
+  TORCH_CHECK(y.is_cuda() && y.is_contiguous() && is_fp8_storage(y) && y.numel() == x.numel(), "fp8_cast y");
+  TORCH_CHECK(x.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0, "fp8_cast needs numel % 8 == 0 and aligned data");
+  check_dev(scale, "scale", at::kFloat, 1, 4);
+  float* am = nullptr;
+  if (amax.has_value()) {
+    check_dev(*amax, "amax", at::kFloat, 1, 4);
+    am = amax->data_ptr<float>();
+  }
+  launch_cast_fp8(x.data_ptr(), x.scalar_type() == at::kFloat, reinterpret_cast<uint8_t*>(y.data_ptr()), x.numel(),
+                  scale.data_ptr<float>(), am, fmt, cur_stream());
+}
+
+void fp8_amax(Tensor x, Tensor amax) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "fp8_amax x");
+  TORCH_CHECK(x.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "fp8_amax alignment");
+  check_dev(amax, "amax", at::kFloat, 1, 4);
+  launch_amax(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), amax.data_ptr<float>(), cur_stream());
+}
+
+void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::optional<Tensor> amax, int fmt) {
+  TORCH_CHECK(w.dim() == 2 && w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat, "w: fp32 [R,C]");
+  const int64_t R = w.size(0), Cc = w.size(1);
+  TORCH_CHECK(R % 4 == 0 && Cc % 4 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w shape/alignment");
+  TORCH_CHECK(y.is_cuda() && y.is_contiguous() && is_fp8_storage(y) && y.numel() == R * Cc, "y");
+  TORCH_CHECK(yt.is_cuda() && yt.is_contiguous() && is_fp8_storage(yt) && yt.numel() == R * Cc, "yt");
+  check_dev(scale, "scale", at::kFloat, 1, 4);
+  float* am = nullptr;
+  if (amax.has_value()) {
+    check_dev(*amax, "amax", at::kFloat, 1, 4);
+    am = amax->data_ptr<float>();
+  }
+  launch_cast_transpose_fp8(w.data_ptr<float>(), reinterpret_cast<uint8_t*>(y.data_ptr()),
+                            reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(), am,
+                            fmt, cur_stream());
+}
+
+void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, Tensor step, int fmt, int margin) {
+  check_dev(hist, "hist", at::kFloat, 1, 4);
+  check_dev(amax, "amax", at::kFloat, 1, 4);
+  check_dev(scale, "scale", at::kFloat, 1, 4);
+  check_dev(inv_scale, "inv_scale", at::kFloat, 1, 4);
+  check_dev(step, "step", at::kLong, 1, 8);
+  launch_fp8_update_scale(hist.data_ptr<float>(), (int)hist.numel(), amax.data_ptr<float>(), scale.data_ptr<float>(),
+                          inv_scale.data_ptr<float>(), fmt, margin, step.data_ptr<int64_t>(), cur_stream());
+}
+
 py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {
   const GemmPlan p = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
   return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats);
@@ -776,6 +885,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
         py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false, py::arg("cfg") = -1,
         py::arg("splits") = 0);
+  m.def("gemm_f8", &gemm_f8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("fmt_a"), py::arg("fmt_b"),
+        py::arg("inv_scale_a"), py::arg("inv_scale_b"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("res") = py::none(), py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false,
+        py::arg("cfg") = -1, py::arg("splits") = 0);
+  m.def("gemm_f8_plan", [](int64_t M, int64_t N, int64_t K, int cfg, int splits) {
+    const GemmPlan p = plan_gemm_f8((int)M, (int)N, (int)K, cfg, splits);
+    return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats);
+  }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cfg") = -1, py::arg("splits") = 0);
+  m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
+        py::arg("fmt") = 0);
+  m.def("fp8_amax", &fp8_amax);
+  m.def("fp8_cast_transpose", &fp8_cast_transpose, py::arg("w"), py::arg("y"), py::arg("yt"), py::arg("scale"),
+        py::arg("amax") = py::none(), py::arg("fmt") = 0);
+  m.def("fp8_update_scale", &fp8_update_scale, py::arg("hist"), py::arg("amax"), py::arg("scale"),
+        py::arg("inv_scale"), py::arg("step"), py::arg("fmt") = 0, py::arg("margin") = 0);
   m.def("gemm_plan", &gemm_plan, py::arg("a_mn"), py::arg("b_mn"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);

@@ -14,6 +14,8 @@ struct GemmEpi {
   float alpha;
   int mode;              // 0 none, 1 gelu (writes aux), 2 dgelu (reads aux)
   int accumulate;        // C += result (fp32 output only)
+  const float* inv_scale_a = nullptr;  // fp8: device-side 1/scale of A and B (multiplied into alpha)
+  const float* inv_scale_b = nullptr;
 };
 
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

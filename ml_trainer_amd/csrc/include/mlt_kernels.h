@@ -107,6 +107,23 @@ void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, co
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
                       const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
                       int accumulate, float* ws, unsigned* cnt, hipStream_t st);
+// fp8 GEMM (gemm_tile.hip): A [M][K], B [N][K] both k-contiguous fp8 (fmt 0 = e4m3, 1 = e5m2),
+// K % 128 == 0; alpha *= inv_scale_a[0] * inv_scale_b[0] (device scalars, delayed scaling).
+GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits);
+void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, const uint8_t* A, const uint8_t* B,
+                    void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* inv_scale_a,
+                    const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux,
+                    const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate, float* ws,
+                    unsigned* cnt, hipStream_t st);
+// fp8 quantisation (fp8.hip)
+void launch_cast_fp8(const void* x, bool x_f32, uint8_t* y, int64_t n, const float* scale, float* amax, int fmt,
+                     hipStream_t st);
+void launch_amax(const void* x, bool x_f32, int64_t n, float* amax, hipStream_t st);
+void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, int C, const float* scale, float* amax,
+                               int fmt, hipStream_t st);
+void launch_fp8_update_scale(float* hist, int H, float* amax, float* scale, float* inv_scale, int fmt, int margin,
+                             int64_t* step, hipStream_t st);
+
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,
                         hipStream_t st);

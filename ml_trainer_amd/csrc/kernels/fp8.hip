@@ -1,0 +1,204 @@
+// FP8 (OCP e4m3 / e5m2 -- gfx950 is OCP, not the MI300 fnuz variant) quantisation kernels for
+// the fp8 GEMM path (BASELINE config 5, "large fp8"):
+//   * cast_fp8: bf16 / fp32 -> fp8 with a per-tensor scale read from device memory, saturating,
+//     recording amax(|x|) of the input for delayed scaling (one pass, 16-byte vector loads);
+//   * cast_transpose_fp8: fp32 master weight [R,C] -> fp8 W [R,C] and W^T [C,R] in one pass
+//     (64x64 tiles through LDS) -- forward uses W, dgrad uses W^T so both fp8 GEMM operands are
+//     k-contiguous;
+//   * amax: max |x| (exact current scaling when there is no history yet);
+//   * update_scale: delayed scaling -- push amax into a history window, scale = fmt_max /
+//     (max(history) * 2^margin), inv_scale = 1 / scale, reset the running amax.
+// Conversions use v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32 after clamping to the finite range.
+#include "mlt_common.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+template <int FMT>
+__device__ __forceinline__ float fp8_max() {
+  return FMT == 0 ? 448.f : 57344.f;
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  const float m = fp8_max<FMT>();
+  a = fminf(fmaxf(a, -m), m);
+  b = fminf(fmaxf(b, -m), m);
+  c = fminf(fmaxf(c, -m), m);
+  d = fminf(fmaxf(d, -m), m);
+  int r;
+  if constexpr (FMT == 0) {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+  }
+  return (uint32_t)r;
+}
+
+__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
+  // |x| >= 0: IEEE ordering of non-negative floats equals their integer ordering
+  atomicMax(reinterpret_cast<unsigned*>(addr), __float_as_uint(v));
+}
+
+__device__ __forceinline__ void load8(const uint16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// y[i] = fp8(x[i] * scale); amax = max(amax, |x|). n % 8 == 0, 16-byte aligned.
+template <typename InT, int FMT>
+__global__ __launch_bounds__(256) void cast_fp8_kernel(const InT* __restrict__ x, uint8_t* __restrict__ y, int64_t n8,
+                                                       const float* __restrict__ scale, float* __restrict__ amax) {
+  __shared__ float red[4];
+  const float s = *scale;
+  float mx = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+    uint2 o;
+    o.x = pack4_fp8<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    o.y = pack4_fp8<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    *reinterpret_cast<uint2*>(y + i * 8) = o;
+  }
+  if (amax) {
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
+template <typename InT>
+__global__ __launch_bounds__(256) void amax_kernel(const InT* __restrict__ x, int64_t n8, float* __restrict__ amax) {
+  __shared__ float red[4];
+  float mx = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// fp32 W [R][C] -> fp8 W [R][C] and W^T [C][R]; 64x64 tile per block, R % 4 == 0, C % 4 == 0
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const float* __restrict__ w, uint8_t* __restrict__ y,
+                                                                 uint8_t* __restrict__ yt, int R, int C,
+                                                                 const float* __restrict__ scale,
+                                                                 float* __restrict__ amax) {
+  __shared__ uint8_t tile[64][68];
+  __shared__ float red[4];
+  const float s = *scale;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  float mx = 0.f;
+  // 64 rows x 16 float4 = 1024 items, 4 per thread
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int e = it * 256 + threadIdx.x, r = e >> 4, c4 = (e & 15) * 4;
+    const int gr = r0 + r, gc = c0 + c4;
+    uint32_t packed = 0;
+    if (gr < R && gc < C) {
+      const float4 v = *reinterpret_cast<const float4*>(w + (int64_t)gr * C + gc);
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      packed = pack4_fp8<FMT>(v.x * s, v.y * s, v.z * s, v.w * s);
+      *reinterpret_cast<uint32_t*>(y + (int64_t)gr * C + gc) = packed;
+    }
+    *reinterpret_cast<uint32_t*>(&tile[r][c4]) = packed;
+  }
+  __syncthreads();
+  // transposed: row c of W^T = column c of the tile; 64 rows x 16 groups of 4 bytes
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int e = it * 256 + threadIdx.x, c = e >> 4, r4 = (e & 15) * 4;
+    const int gc = c0 + c, gr = r0 + r4;
+    if (gc < C && gr < R) {
+      const uint32_t v = (uint32_t)tile[r4][c] | ((uint32_t)tile[r4 + 1][c] << 8) | ((uint32_t)tile[r4 + 2][c] << 16) |
+                         ((uint32_t)tile[r4 + 3][c] << 24);
+      *reinterpret_cast<uint32_t*>(yt + (int64_t)gc * R + gr) = v;
+    }
+  }
+  if (amax) {
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
+// hist[H] ring indexed by (*step % H); scale = fmt_max / (max(hist) * 2^margin)
+__global__ void update_scale_kernel(float* __restrict__ hist, int H, float* __restrict__ amax, float* __restrict__ scale,
+                                    float* __restrict__ inv_scale, float fmt_max, float margin_pow,
+                                    int64_t* __restrict__ step) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t t = *step;
+  hist[t % H] = *amax;
+  float m = 0.f;
+  for (int i = 0; i < H; ++i) m = fmaxf(m, hist[i]);
+  if (m > 0.f && isfinite(m)) {
+    const float sc = fmt_max / (m * margin_pow);
+    *scale = sc;
+    *inv_scale = 1.f / sc;
+  }
+  *amax = 0.f;
+  *step = t + 1;
+}
+
+static int grid_for(int64_t n8) {
+  const int64_t b = (n8 + 255) / 256;
+  return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
+void launch_cast_fp8(const void* x, bool x_f32, uint8_t* y, int64_t n, const float* scale, float* amax, int fmt,
+                     hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 <= 0) return;
+  const dim3 g(grid_for(n8)), b(256);
+  if (x_f32) {
+    if (fmt == 0) hipLaunchKernelGGL((cast_fp8_kernel<float, 0>), g, b, 0, st, (const float*)x, y, n8, scale, amax);
+    else hipLaunchKernelGGL((cast_fp8_kernel<float, 1>), g, b, 0, st, (const float*)x, y, n8, scale, amax);
+  } else {
+    if (fmt == 0) hipLaunchKernelGGL((cast_fp8_kernel<uint16_t, 0>), g, b, 0, st, (const uint16_t*)x, y, n8, scale, amax);
+    else hipLaunchKernelGGL((cast_fp8_kernel<uint16_t, 1>), g, b, 0, st, (const uint16_t*)x, y, n8, scale, amax);
+  }
+}
+
+void launch_amax(const void* x, bool x_f32, int64_t n, float* amax, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 <= 0) return;
+  if (x_f32) hipLaunchKernelGGL((amax_kernel<float>), dim3(grid_for(n8)), dim3(256), 0, st, (const float*)x, n8, amax);
+  else hipLaunchKernelGGL((amax_kernel<uint16_t>), dim3(grid_for(n8)), dim3(256), 0, st, (const uint16_t*)x, n8, amax);
+}
+
+void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, int C, const float* scale, float* amax,
+                               int fmt, hipStream_t st) {
+  if (R <= 0 || C <= 0) return;
+  const dim3 g((C + 63) / 64, (R + 63) / 64), b(256);
+  if (fmt == 0) hipLaunchKernelGGL(cast_transpose_fp8_kernel<0>, g, b, 0, st, w, y, yt, R, C, scale, amax);
+  else hipLaunchKernelGGL(cast_transpose_fp8_kernel<1>, g, b, 0, st, w, y, yt, R, C, scale, amax);
+}
+
+void launch_fp8_update_scale(float* hist, int H, float* amax, float* scale, float* inv_scale, int fmt, int margin,
+                             int64_t* step, hipStream_t st) {
+  hipLaunchKernelGGL(update_scale_kernel, dim3(1), dim3(64), 0, st, hist, H, amax, scale, inv_scale,
+                     fmt == 0 ? 448.f : 57344.f, ldexpf(1.f, margin), step);
+}
+
+}  // namespace mlt

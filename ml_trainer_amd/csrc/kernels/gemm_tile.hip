@@ -74,26 +74,40 @@ __device__ __forceinline__ bf16x8 tfrag_mn(const uint8_t* lds, int mn, int kh) {
 }
 
 // ---- per-thread glds sources -----------------------------------------------------------
-// Chunk e = i * 512 + threadIdx.x of an operand image lands at LDS byte e * 16.
-template <int ROWS, bool MN>  // ROWS = extent of the operand's M (or N) side of the tile
-__device__ __forceinline__ const uint16_t* glds_src(const uint16_t* __restrict__ base, int64_t ld, int i, int mn0,
-                                                    int nmn) {
+// Chunk e = i * 512 + threadIdx.x of an operand image lands at LDS byte e * 16. Byte
+// addressing: ES = element size (2 bf16, 1 fp8); a k-contiguous row holds 128 bytes per K-step.
+template <int ROWS, bool MN, int ES>  // ROWS = extent of the operand's M (or N) side of the tile
+__device__ __forceinline__ const uint8_t* glds_src(const uint8_t* __restrict__ base, int64_t ld, int i, int mn0,
+                                                   int nmn) {
   const int e = i * T_NT + threadIdx.x;
-  if (!MN) {  // [ROWS][64 k]: 8 chunks per row
+  if (!MN) {  // [ROWS][128 B]: 8 chunks per row
     const int r = e >> 3, p = e & 7, c = p ^ (r & 7);
     const int row = min(mn0 + r, nmn - 1);
-    return base + (int64_t)row * ld + c * 8;
-  } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row
+    return base + ((int64_t)row * ld) * ES + c * 16;
+  } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row (bf16 only)
     constexpr int CPR = ROWS / 8;
     const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
     const int col = min(mn0 + c * 8, nmn - 8);
-    return base + (int64_t)kk * ld + col;
+    return base + ((int64_t)kk * ld + col) * ES;
   }
 }
 
-template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT>
-__global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __restrict__ A,
-                                                             const uint16_t* __restrict__ B, OutT* __restrict__ C,
+// fp8 operand fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row (l&15), k bytes
+// 32(l>>4) .. +31 = chunks 2(l>>4), 2(l>>4)+1 of the 128-byte row (positional k pairing with B)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ i32x8 tfrag_f8(const uint8_t* lds, int row) {
+  const int lane = threadIdx.x & 63;
+  const int r = row + (lane & 15), c0 = 2 * (lane >> 4);
+  const uint4 lo = *reinterpret_cast<const uint4*>(lds + r * 128 + ((c0 ^ (r & 7)) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(lds + r * 128 + (((c0 + 1) ^ (r & 7)) << 4));
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+// F8A / F8B: -1 = bf16 operands; 0 = fp8 e4m3, 1 = bf8 e5m2 (OCP) through the MX-scaled
+// 16x16x128 MFMA at unit block scales (per-tensor scales are folded into the epilogue alpha).
+template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT, int F8A = -1, int F8B = -1>
+__global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __restrict__ A,
+                                                             const uint8_t* __restrict__ B, OutT* __restrict__ C,
                                                              int M, int N, int K, int64_t lda, int64_t ldb,
                                                              int64_t ldc, GemmEpi epi, float* __restrict__ ws,
                                                              unsigned* __restrict__ cnt, int ksteps) {
@@ -110,16 +124,20 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
   const int m0 = tm * BM, n0 = tn * BN;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = (wid / WARPS_N) * WTM, wn = (wid % WARPS_N) * WTN;
-  const int nk = K / T_BK;
+  constexpr bool F8 = F8A >= 0;
+  constexpr int ES = F8 ? 1 : 2;
+  static_assert(!F8 || (F8B >= 0 && !AM && !BNL), "fp8 operands must both be fp8 and k-contiguous");
+  const int nk = K / (F8 ? 128 : T_BK);
   const int kt0 = blockIdx.y * ksteps, kt1 = min(nk, kt0 + ksteps);
 
-  const uint16_t* asrc[A_CH];
-  const uint16_t* bsrc[B_CH];
+  const uint8_t* asrc[A_CH];
+  const uint8_t* bsrc[B_CH];
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) asrc[i] = glds_src<BM, AM>(A, lda, i, m0, M);
+  for (int i = 0; i < A_CH; ++i) asrc[i] = glds_src<BM, AM, ES>(A, lda, i, m0, M);
 #pragma unroll
-  for (int i = 0; i < B_CH; ++i) bsrc[i] = glds_src<BN, BNL>(B, ldb, i, n0, N);
-  const int64_t astep = AM ? (int64_t)T_BK * lda : T_BK, bstep = BNL ? (int64_t)T_BK * ldb : T_BK;
+  for (int i = 0; i < B_CH; ++i) bsrc[i] = glds_src<BN, BNL, ES>(B, ldb, i, n0, N);
+  // bytes per K-step: a k-contiguous row advances 128 B; an mn-contiguous image 64 k-rows
+  const int64_t astep = AM ? (int64_t)T_BK * lda * ES : 128, bstep = BNL ? (int64_t)T_BK * ldb * ES : 128;
 
   auto stage = [&](int buf, int kt) {
     uint8_t* base = smem + buf * G::BUF;
@@ -146,6 +164,18 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
     if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
     const uint8_t* As = smem + cur * G::BUF;
     const uint8_t* Bs = As + G::A_BYTES;
+    if constexpr (F8) {
+      i32x8 bfr[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = tfrag_f8(Bs, wn + 16 * j);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const i32x8 af = tfrag_f8(As, wm + 16 * i);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], F8A, F8B, 0, 127, 0, 127);
+      }
+    } else
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       bf16x8 bfr[TJ];
@@ -211,6 +241,9 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
 
   // ---- epilogue ----------------------------------------------------------------------------
   constexpr int EPR = G::EPR, EPS = G::EPS, RI = EPR / 16;
+  float alpha = epi.alpha;
+  if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
+  if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (EPR * EPS);
   float bv[TJ];
@@ -228,7 +261,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint16_t* __re
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          cs[(16 * ii + 4 * g + r) * EPS + 16 * j + cl] = acc[RI * h + ii][j][r] * epi.alpha + bv[j];
+          cs[(16 * ii + 4 * g + r) * EPS + 16 * j + cl] = acc[RI * h + ii][j][r] * alpha + bv[j];
     __syncthreads();
 #pragma unroll 4
     for (int it = 0; it < EPR * WTN / 4 / 64; ++it) {
@@ -262,19 +295,61 @@ const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2},
                                {128, 256, 0.92e15 / kCUs, 1},
                                {256, 192, 1.05e15 / kCUs, 1}};
 
-double est_time(int cfg, int splits, int M, int N, int K) {
+// kstep = K elements per 128-byte row step (64 bf16, 128 fp8); speed = MFMA-rate factor
+double est_time(int cfg, int splits, int M, int N, int K, int kstep, double speed) {
   const CfgDesc& c = kCfg[cfg];
   const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
   const int64_t blocks = tiles * splits;
   const int64_t slots = (int64_t)kCUs * c.per_cu;
   const int64_t rounds = (blocks + slots - 1) / slots;
-  const int nk = (K + 63) / 64, ks = (nk + splits - 1) / splits;
-  const double t_block = 2.0 * c.bm * c.bn * 64.0 * ks / (c.rate / c.per_cu) + 1.0e-6;
+  const int nk = (K + kstep - 1) / kstep, ks = (nk + splits - 1) / splits;
+  const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + 1.0e-6;
   double t = rounds * t_block;
   if (splits > 1) t += (double)tiles * splits * c.bm * c.bn * 4.0 * 2.0 / 4.0e12 + 2.0e-6;
   return t;
 }
-}  // namespace
+
+GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy) {
+  GemmPlan p{0, 1, 0, 0, 0};
+  const bool big_ok = K % kstep == 0 && K >= kstep && M >= 64 && N >= 64;
+  const double speed = kstep == 128 ? 1.8 : 1.0;
+  int best_cfg = 0, best_s = 1;
+  if (force_cfg >= 0) {
+    best_cfg = (force_cfg >= 1 && force_cfg < kNumCfg && big_ok) ? force_cfg : 0;
+    best_s = best_cfg ? (force_splits > 0 ? force_splits : 1) : 1;
+  } else if (big_ok) {
+    double best = allow_legacy ? est_time(0, 1, M, N, K, 64, 1.0) : 1e30;
+    const int nk = K / kstep;
+    for (int cfg = 1; cfg < kNumCfg; ++cfg)
+      for (int s = 1; s <= 16; ++s) {
+        if (s > nk) break;
+        const int ks = (nk + s - 1) / s;
+        if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
+        if (s > 1 && ks < 4) continue;
+        const double t = est_time(cfg, s, M, N, K, kstep, speed);
+        if (t < best * 0.97) {
+          best = t;
+          best_cfg = cfg;
+          best_s = s;
+        }
+      }
+    if (force_splits > 0 && best_cfg) best_s = force_splits;
+  }
+  p.cfg = best_cfg;
+  p.splits = best_s;
+  if (best_cfg) {
+    const int nk = K / kstep;
+    if (p.splits > nk) p.splits = nk;
+    p.ksteps = (nk + p.splits - 1) / p.splits;
+    const CfgDesc& c = kCfg[best_cfg];
+    const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    if (p.splits > 1) {
+      p.ws_floats = tiles * p.splits * c.bm * c.bn;
+      p.cnt_ints = tiles;
+    }
+  }
+  return p;
+}
 
 // Split-K tile counters: one zero-initialised device pool (allocated on first use, i.e. in an
 // eager warm-up call, never inside a graph capture), handed out as a ring of slices. Every
@@ -295,55 +370,11 @@ unsigned* split_counters(int64_t need) {
   return s;
 }
 
-GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
-  (void)a_mn;
-  (void)b_mn;
-  GemmPlan p{0, 1, 0, 0, 0};
-  const bool big_ok = K % 64 == 0 && K >= 64 && M >= 64 && N >= 64;
-  int best_cfg = 0, best_s = 1;
-  if (force_cfg >= 0) {
-    best_cfg = (force_cfg >= 1 && force_cfg < kNumCfg && big_ok) ? force_cfg : 0;
-    best_s = best_cfg ? (force_splits > 0 ? force_splits : 1) : 1;
-  } else if (big_ok) {
-    double best = est_time(0, 1, M, N, K);
-    const int nk = K / 64;
-    for (int cfg = 1; cfg < kNumCfg; ++cfg)
-      for (int s = 1; s <= 16; ++s) {
-        if (s > nk) break;
-        const int ks = (nk + s - 1) / s;
-        if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
-        if (s > 1 && ks < 4) continue;
-        const double t = est_time(cfg, s, M, N, K);
-        if (t < best * 0.97) {
-          best = t;
-          best_cfg = cfg;
-          best_s = s;
-        }
-      }
-    if (force_splits > 0 && best_cfg) best_s = force_splits;
-  }
-  p.cfg = best_cfg;
-  p.splits = best_s;
-  if (best_cfg) {
-    const int nk = K / 64;
-    if (p.splits > nk) p.splits = nk;
-    p.ksteps = (nk + p.splits - 1) / p.splits;
-    const CfgDesc& c = kCfg[best_cfg];
-    const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
-    if (p.splits > 1) {
-      p.ws_floats = tiles * p.splits * c.bm * c.bn;
-      p.cnt_ints = tiles;
-    }
-  }
-  return p;
-}
-
-template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT>
-static void launch_tile(const GemmPlan& p, const uint16_t* A, const uint16_t* B, OutT* C, int M, int N, int K,
-                        int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt,
-                        hipStream_t st) {
+template <int BM, int BN, int WARPS_M, bool AM, bool BNL, typename OutT, int F8A, int F8B>
+void launch_tile(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda,
+                 int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt, hipStream_t st) {
   using G = TileGeom<BM, BN, WARPS_M>;
-  auto kern = gemm_tile_kernel<BM, BN, WARPS_M, AM, BNL, OutT>;
+  auto kern = gemm_tile_kernel<BM, BN, WARPS_M, AM, BNL, OutT, F8A, F8B>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
@@ -354,44 +385,61 @@ static void launch_tile(const GemmPlan& p, const uint16_t* A, const uint16_t* B,
                      cnt, p.ksteps);
 }
 
-template <bool AM, bool BNL, typename OutT>
-static void launch_cfg(const GemmPlan& p, const uint16_t* A, const uint16_t* B, OutT* C, int M, int N, int K,
-                       int64_t lda, int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt,
-                       hipStream_t st) {
+template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
+void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda,
+                int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt, hipStream_t st) {
   switch (p.cfg) {
-    case 1: launch_tile<256, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
-    case 2: launch_tile<256, 128, 4, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
-    case 3: launch_tile<128, 256, 2, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
-    case 4: launch_tile<256, 192, 4, AM, BNL, OutT>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 1: launch_tile<256, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 2: launch_tile<256, 128, 4, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 3: launch_tile<128, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 4: launch_tile<256, 192, 4, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     default: break;
   }
 }
 
-void launch_gemm_bf16(const GemmPlan& p, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
+// split-K plan without workspace / counters -> unsplit
+bool resolve_split(GemmPlan& p, float* ws, unsigned*& cnt, int K, int kstep) {
+  if (p.splits > 1 && cnt == nullptr) cnt = split_counters(p.cnt_ints);
+  if (p.splits > 1 && (cnt == nullptr || ws == nullptr)) {
+    p.splits = 1;
+    p.ksteps = K / kstep;
+  }
+  return p.splits > 1;
+}
+}  // namespace
+
+GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
+  (void)a_mn;
+  (void)b_mn;
+  return plan_tiles(M, N, K, force_cfg, force_splits, 64, true);
+}
+
+GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {
+  GemmPlan p = plan_tiles(M, N, K, force_cfg < 1 ? -1 : force_cfg, force_splits, 128, false);
+  if (p.cfg == 0) p.cfg = -1;  // not runnable (K % 128 != 0 or too small)
+  return p;
+}
+
+void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
                       const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
                       int accumulate, float* ws, unsigned* cnt, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate};
-  if (p.cfg == 0) {
+  if (plan.cfg == 0) {
     launch_gemm_bf16_128(a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, e, st);
     return;
   }
-  if (p.splits > 1 && cnt == nullptr) cnt = split_counters(p.cnt_ints);
-  if (p.splits > 1 && (cnt == nullptr || ws == nullptr)) {  // no workspace: run unsplit
-    GemmPlan q = p;
-    q.splits = 1;
-    q.ksteps = K / 64;
-    launch_gemm_bf16(q, a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, alpha,
-                     mode, accumulate, nullptr, nullptr, st);
-    return;
-  }
+  GemmPlan p = plan;
+  resolve_split(p, ws, cnt, K, 64);
+  const uint8_t* a8 = reinterpret_cast<const uint8_t*>(A);
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(B);
 #define MLT_TILE_CASE(AMV, BNV)                                                                                  \
   if (a_mn == AMV && b_mn == BNV) {                                                                              \
     if (out_f32)                                                                                                 \
-      launch_cfg<AMV, BNV, float>(p, A, B, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);                   \
+      launch_cfg<AMV, BNV, float, -1, -1>(p, a8, b8, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);         \
     else                                                                                                         \
-      launch_cfg<AMV, BNV, uint16_t>(p, A, B, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);             \
+      launch_cfg<AMV, BNV, uint16_t, -1, -1>(p, a8, b8, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);   \
     return;                                                                                                      \
   }
   MLT_TILE_CASE(0, 0)
@@ -399,6 +447,29 @@ void launch_gemm_bf16(const GemmPlan& p, int a_mn, int b_mn, bool out_f32, const
   MLT_TILE_CASE(1, 0)
   MLT_TILE_CASE(1, 1)
 #undef MLT_TILE_CASE
+}
+
+void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, const uint8_t* A, const uint8_t* B,
+                    void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* inv_scale_a,
+                    const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux,
+                    const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate, float* ws,
+                    unsigned* cnt, hipStream_t st) {
+  if (M <= 0 || N <= 0 || plan.cfg < 1) return;
+  GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate, inv_scale_a, inv_scale_b};
+  GemmPlan p = plan;
+  resolve_split(p, ws, cnt, K, 128);
+#define MLT_F8_CASE(FA, FB)                                                                                      \
+  if (fmt_a == FA && fmt_b == FB) {                                                                              \
+    if (out_f32)                                                                                                 \
+      launch_cfg<false, false, float, FA, FB>(p, A, B, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);       \
+    else                                                                                                         \
+      launch_cfg<false, false, uint16_t, FA, FB>(p, A, B, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); \
+    return;                                                                                                      \
+  }
+  MLT_F8_CASE(0, 0)
+  MLT_F8_CASE(1, 0)
+  MLT_F8_CASE(0, 1)
+#undef MLT_F8_CASE
 }
 
 }  // namespace mlt
