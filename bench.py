@@ -20,6 +20,9 @@ Scaling modes:
 Usage:  python bench.py --gpus N --steps K --warmup W
   (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
+BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgrad GEMMs with
+delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
+
 BASELINE.json config 4 (BERT-base classifier, seq 512, bf16, DDP): ``--model bert-base``
 (per-GPU batch --batch, default 32; native MFMA GEMM / flash-attention / LayerNorm kernels,
 fused AdamW on flat fp32 masters with bf16 shadows, bucketed RCCL all-reduce overlapped with
@@ -28,6 +31,7 @@ backward for N > 1).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -45,8 +49,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch (weak) / global batch (reference); default 32")
     ap.add_argument("--scaling", choices=["weak", "reference"], default="weak")
-    ap.add_argument("--model", default="default", choices=["default", "tiny", "bert-base", "bert-tiny", "large"])
+    ap.add_argument("--model", default="default",
+                    choices=["default", "tiny", "bert-base", "bert-tiny", "bert-large", "large"])
     ap.add_argument("--seq-len", type=int, default=512)
+    ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (BERT modes)")
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dataset-size", type=int, default=50000)
@@ -82,14 +88,20 @@ def bench_bert(args, world, rank, dev):
     labels = torch.randint(0, cfg.num_labels, (pool, per_gpu), device=dev, generator=g)
     loss_acc = torch.zeros((), device=dev)
 
+    accum = max(1, args.grad_accum)
+
     def run(n, start):
         for i in range(n):
-            j = (start + i) % pool
             opt.zero_grad(set_to_none=False)
-            loss = F.cross_entropy(fwd(ids[j]), labels[j])
-            loss.backward()
+            for a in range(accum):  # gradient accumulation: all-reduce only on the last micro-batch
+                j = (start + i * accum + a) % pool
+                sync = a == accum - 1
+                ctxm = ddp.no_sync() if (world > 1 and not sync) else contextlib.nullcontext()
+                with ctxm:
+                    loss = F.cross_entropy(fwd(ids[j]), labels[j])
+                    (loss / accum if accum > 1 else loss).backward()
+                loss_acc.add_(loss.detach())
             opt.step()
-            loss_acc.add_(loss.detach())
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -107,7 +119,7 @@ def bench_bert(args, world, rank, dev):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    total = per_gpu * world * args.steps
+    total = per_gpu * world * args.steps * accum
     value = total / elapsed
     return {
         "metric": "samples/sec/node",
@@ -120,11 +132,12 @@ def bench_bert(args, world, rank, dev):
         "higher_is_better": True,
         "scaling": "weak" if args.scaling == "weak" else "strong",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8" if cfg.fp8 else "bf16",
         "data": "synthetic token ids (uniform over the vocabulary) resident in HBM, random-init weights",
         "config": {"model": f"BERT classifier {args.model} ({cfg.layers}L/{cfg.hidden}H/{cfg.heads}A, "
                             f"{model.num_parameters():,} params)",
-                   "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": args.seq_len,
+                   "global_batch": per_gpu * world * accum, "per_gpu_batch": per_gpu, "grad_accum": accum,
+                   "seq_len": args.seq_len, "fp8": bool(cfg.fp8),
                    "parallelism": f"dp{world}", "optimizer": "fused AdamW lr=1e-4 wd=0.01 (fp32 master, bf16 shadow)",
                    "tokens_per_s": round(value * args.seq_len, 1),
                    "model_tflops": round(model.flops_per_token(args.seq_len) * value * args.seq_len / 1e12, 1),
@@ -149,9 +162,7 @@ def main():
     if args.batch is None:
         args.batch = 32
 
-    if args.model in ("bert-base", "bert-tiny", "large"):
-        if args.model == "large":
-            raise SystemExit("the fp8 'large' config is not wired into bench.py yet")
+    if args.model in ("bert-base", "bert-tiny", "bert-large", "large"):
         if args.steps == 3000 and args.warmup == 300:  # LeNet-sized defaults -> BERT-sized
             args.steps, args.warmup = 20, 5
         out = bench_bert(args, world, rank, dev)

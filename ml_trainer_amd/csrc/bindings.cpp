@@ -389,14 +389,19 @@ void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::option
                             fmt, cur_stream());
 }
 
-void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, Tensor step, int fmt, int margin) {
-  check_dev(hist, "hist", at::kFloat, 1, 4);
-  check_dev(amax, "amax", at::kFloat, 1, 4);
-  check_dev(scale, "scale", at::kFloat, 1, 4);
-  check_dev(inv_scale, "inv_scale", at::kFloat, 1, 4);
-  check_dev(step, "step", at::kLong, 1, 8);
-  launch_fp8_update_scale(hist.data_ptr<float>(), (int)hist.numel(), amax.data_ptr<float>(), scale.data_ptr<float>(),
-                          inv_scale.data_ptr<float>(), fmt, margin, step.data_ptr<int64_t>(), cur_stream());
+// hist [n, H], amax / scale / inv_scale / fmax [n]
+void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, Tensor fmax, int64_t step,
+                      int margin) {
+  const int64_t n = amax.numel();
+  TORCH_CHECK(hist.dim() == 2 && hist.size(0) >= n && hist.is_contiguous(), "hist must be [n, H]");
+  check_dev(hist, "hist", at::kFloat, n * hist.size(1), 4);
+  check_dev(amax, "amax", at::kFloat, n, 4);
+  check_dev(scale, "scale", at::kFloat, n, 4);
+  check_dev(inv_scale, "inv_scale", at::kFloat, n, 4);
+  check_dev(fmax, "fmax", at::kFloat, n, 4);
+  launch_fp8_update_scale(hist.data_ptr<float>(), (int)hist.size(1), (int)n, amax.data_ptr<float>(),
+                          scale.data_ptr<float>(), inv_scale.data_ptr<float>(), fmax.data_ptr<float>(), margin, step,
+                          cur_stream());
 }
 
 py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {
@@ -899,7 +904,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_cast_transpose", &fp8_cast_transpose, py::arg("w"), py::arg("y"), py::arg("yt"), py::arg("scale"),
         py::arg("amax") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_update_scale", &fp8_update_scale, py::arg("hist"), py::arg("amax"), py::arg("scale"),
-        py::arg("inv_scale"), py::arg("step"), py::arg("fmt") = 0, py::arg("margin") = 0);
+        py::arg("inv_scale"), py::arg("fmax"), py::arg("step"), py::arg("margin") = 0);
   m.def("gemm_plan", &gemm_plan, py::arg("a_mn"), py::arg("b_mn"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);

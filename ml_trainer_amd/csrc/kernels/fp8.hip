@@ -6,8 +6,8 @@
 //     (64x64 tiles through LDS) -- forward uses W, dgrad uses W^T so both fp8 GEMM operands are
 //     k-contiguous;
 //   * amax: max |x| (exact current scaling when there is no history yet);
-//   * update_scale: delayed scaling -- push amax into a history window, scale = fmt_max /
-//     (max(history) * 2^margin), inv_scale = 1 / scale, reset the running amax.
+//   * update_scale: delayed scaling for n tensors at once -- push each amax into its history
+//     window, scale = fmt_max / (max(history) * 2^margin), inv_scale = 1 / scale, reset amax.
 // Conversions use v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32 after clamping to the finite range.
 #include "mlt_common.h"
 #include "mlt_kernels.h"
@@ -143,22 +143,23 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const float* __
   }
 }
 
-// hist[H] ring indexed by (*step % H); scale = fmt_max / (max(hist) * 2^margin)
-__global__ void update_scale_kernel(float* __restrict__ hist, int H, float* __restrict__ amax, float* __restrict__ scale,
-                                    float* __restrict__ inv_scale, float fmt_max, float margin_pow,
-                                    int64_t* __restrict__ step) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const int64_t t = *step;
-  hist[t % H] = *amax;
+// Batched delayed scaling over n tensors: hist[i][step % H] = amax[i];
+// scale[i] = fmax[i] / (max_h hist[i][h] * 2^margin); inv_scale[i] = 1 / scale[i]; amax[i] = 0.
+__global__ void update_scale_kernel(float* __restrict__ hist, int H, int n, float* __restrict__ amax,
+                                    float* __restrict__ scale, float* __restrict__ inv_scale,
+                                    const float* __restrict__ fmax, float margin_pow, int64_t step) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* h = hist + (int64_t)i * H;
+  h[step % H] = amax[i];
   float m = 0.f;
-  for (int i = 0; i < H; ++i) m = fmaxf(m, hist[i]);
+  for (int k = 0; k < H; ++k) m = fmaxf(m, h[k]);
   if (m > 0.f && isfinite(m)) {
-    const float sc = fmt_max / (m * margin_pow);
-    *scale = sc;
-    *inv_scale = 1.f / sc;
+    const float sc = fmax[i] / (m * margin_pow);
+    scale[i] = sc;
+    inv_scale[i] = 1.f / sc;
   }
-  *amax = 0.f;
-  *step = t + 1;
+  amax[i] = 0.f;
 }
 
 static int grid_for(int64_t n8) {
@@ -195,10 +196,11 @@ void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, i
   else hipLaunchKernelGGL(cast_transpose_fp8_kernel<1>, g, b, 0, st, w, y, yt, R, C, scale, amax);
 }
 
-void launch_fp8_update_scale(float* hist, int H, float* amax, float* scale, float* inv_scale, int fmt, int margin,
-                             int64_t* step, hipStream_t st) {
-  hipLaunchKernelGGL(update_scale_kernel, dim3(1), dim3(64), 0, st, hist, H, amax, scale, inv_scale,
-                     fmt == 0 ? 448.f : 57344.f, ldexpf(1.f, margin), step);
+void launch_fp8_update_scale(float* hist, int H, int n, float* amax, float* scale, float* inv_scale, const float* fmax,
+                             int margin, int64_t step, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(update_scale_kernel, dim3((n + 255) / 256), dim3(256), 0, st, hist, H, n, amax, scale, inv_scale,
+                     fmax, ldexpf(1.f, margin), step);
 }
 
 }  // namespace mlt

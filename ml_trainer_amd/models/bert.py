@@ -73,15 +73,13 @@ class BertLayer(nn.Module):
     def forward_native(self, x, lens, B, S):
         from ml_trainer_amd.ops import transformer as T
         if self.c.fp8:
-            from ml_trainer_amd.ops import fp8 as F8
-            a = F8.attention_block_fp8(x, self.qkv, self.out, lens, B, S, self.c.heads)
-            x = T.layer_norm(a, self.ln1.weight, self.ln1.bias, self.c.ln_eps)
-            f = F8.ffn_block_fp8(x, self.ffn1, self.ffn2)
-            return T.layer_norm(f, self.ln2.weight, self.ln2.bias, self.c.ln_eps)
+            from ml_trainer_amd.ops.fp8 import FP8 as impl
+        else:
+            impl = T.BF16
         x = T.attention_ln_block(x, self.qkv.weight, self.qkv.bias, self.out.weight, self.out.bias, self.ln1.weight,
-                                 self.ln1.bias, lens, B, S, self.c.heads, self.c.ln_eps)
+                                 self.ln1.bias, lens, B, S, self.c.heads, self.c.ln_eps, impl)
         return T.ffn_ln_block(x, self.ffn1.weight, self.ffn1.bias, self.ffn2.weight, self.ffn2.bias, self.ln2.weight,
-                              self.ln2.bias, self.c.ln_eps)
+                              self.ln2.bias, self.c.ln_eps, impl)
 
     def forward_reference(self, x, mask, B, S):
         """fp32 torch reference. x [B*S, h]; mask [B, S] bool (True = valid key)."""
@@ -140,6 +138,9 @@ class BertClassifier(nn.Module):
         lens = self._lengths(input_ids, attention_mask)
         if input_ids.is_cuda:
             from ml_trainer_amd.ops import transformer as T
+            if self.config.fp8 and torch.is_grad_enabled():
+                from ml_trainer_amd.ops.fp8 import context
+                context(input_ids.device).update()  # delayed scaling: fold last step's amaxes
             x = T.embeddings(input_ids, token_type_ids, self.word_embeddings.weight, self.position_embeddings.weight,
                              self.token_type_embeddings.weight, S)
             x = T.layer_norm(x, self.emb_ln.weight, self.emb_ln.bias, self.config.ln_eps)

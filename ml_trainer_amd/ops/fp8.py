@@ -1,0 +1,162 @@
+"""FP8 linear layers for the ``large`` config (BASELINE.json config 5: "large config fp8
+(CDNA4 fp8 MFMA)").
+
+Numerics (the standard delayed-scaling recipe, on MI355X's OCP formats):
+
+* forward GEMM  y  = x . W^T  : x e4m3 x W e4m3  (v_mfma_scale_f32_16x16x128_f8f6f4, unit MX
+  block scales; per-tensor scales folded into the epilogue alpha from device memory);
+* dgrad GEMM    dx = dy . W   : dy e5m2 x W^T e4m3 (W^T from the same cast-transpose pass, so
+  both operands are k-contiguous);
+* wgrad GEMM    dW = dy^T . x : bf16 (split-K tile kernel), fp32 output into the master grads;
+* scales: every quantised tensor role (x, W, dy of each linear) owns a meta slot: the cast
+  kernels record amax(|t|) while quantising, and ``Fp8Context.update()`` (once per step, one
+  launch for all slots) pushes it into a 16-step history and sets scale = fmax / max(history).
+  A slot's very first use computes its exact amax first (current scaling), so step 0 is sane.
+* weights are re-quantised (cast + transpose, one pass over the fp32 master) only when the
+  optimizer has updated them (``FlatParams.generation``).
+
+Everything else in the block (bias, GELU, residual, LayerNorm, attention) is unchanged bf16.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from ml_trainer_amd.ops._ext import require_native
+from ml_trainer_amd.utils.flat import FlatParams
+
+E4M3, E5M2 = 0, 1
+_FMAX = {E4M3: 448.0, E5M2: 57344.0}
+_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
+
+
+class Fp8Context:
+    """Device-resident fp8 scaling state for up to ``capacity`` tensor roles."""
+
+    def __init__(self, device: torch.device, capacity: int = 4096, history: int = 16, margin: int = 0):
+        self.device = device
+        self.amax = torch.zeros(capacity, device=device)
+        self.scale = torch.ones(capacity, device=device)
+        self.inv_scale = torch.ones(capacity, device=device)
+        self.fmax = torch.zeros(capacity, device=device)
+        self.hist = torch.zeros(capacity, history, device=device)
+        self.margin = margin
+        self.n = 0
+        self.step = 0
+        self._ready: list = []
+
+    def new_meta(self, fmt: int) -> int:
+        if self.n >= self.amax.numel():
+            raise RuntimeError("fp8 context capacity exhausted")
+        i = self.n
+        self.fmax[i] = _FMAX[fmt]
+        self.n += 1
+        self._ready.append(False)
+        return i
+
+    def update(self) -> None:
+        """Delayed scaling: fold the amaxes recorded since the last call into every slot's scale."""
+        if self.n:
+            require_native().fp8_update_scale(self.hist[:self.n], self.amax[:self.n], self.scale[:self.n],
+                                              self.inv_scale[:self.n], self.fmax[:self.n], self.step, self.margin)
+            self.step += 1
+
+    def _init_exact(self, i: int, x: torch.Tensor) -> None:
+        C = require_native()
+        sl = slice(i, i + 1)
+        self.amax[sl].zero_()
+        C.fp8_amax(x, self.amax[sl])
+        C.fp8_update_scale(self.hist[sl], self.amax[sl], self.scale[sl], self.inv_scale[sl], self.fmax[sl],
+                           self.step, self.margin)
+        self._ready[i] = True
+
+    def cast(self, x: torch.Tensor, i: int, fmt: int) -> torch.Tensor:
+        if not self._ready[i]:
+            self._init_exact(i, x)
+        y = torch.empty(x.shape, dtype=_DT[fmt], device=x.device)
+        require_native().fp8_cast(x, y, self.scale[i:i + 1], self.amax[i:i + 1], fmt)
+        return y
+
+    def inv(self, i: int) -> torch.Tensor:
+        return self.inv_scale[i:i + 1]
+
+
+_CTX: Dict[torch.device, Fp8Context] = {}
+
+
+def context(device: torch.device) -> Fp8Context:
+    device = torch.device(device)
+    if device not in _CTX:
+        _CTX[device] = Fp8Context(device)
+    return _CTX[device]
+
+
+class _WeightState:
+    __slots__ = ("mx", "mw", "mdy", "w8", "w8t", "key")
+
+    def __init__(self, ctx: Fp8Context):
+        self.mx = ctx.new_meta(E4M3)
+        self.mw = ctx.new_meta(E4M3)
+        self.mdy = ctx.new_meta(E5M2)
+        self.w8: Optional[torch.Tensor] = None
+        self.w8t: Optional[torch.Tensor] = None
+        self.key = None
+
+
+def _state(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
+    st = getattr(w, "_mlt_f8", None)
+    if st is None:
+        st = _WeightState(ctx)
+        w._mlt_f8 = st
+    return st
+
+
+def _weight_key(w: torch.Tensor):
+    fp = FlatParams.owner(w)
+    return (fp.generation if fp is not None else w._version, w.data_ptr())
+
+
+def weight_fp8(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
+    """fp8 W and W^T of an fp32 master weight [out, in], re-quantised when the weight changed."""
+    st = _state(w, ctx)
+    key = _weight_key(w)
+    if st.key != key:
+        C = require_native()
+        wd = w.detach()
+        if st.w8 is None:
+            st.w8 = torch.empty(wd.shape, dtype=torch.float8_e4m3fn, device=wd.device)
+            st.w8t = torch.empty(wd.shape[1], wd.shape[0], dtype=torch.float8_e4m3fn, device=wd.device)
+        if not ctx._ready[st.mw]:
+            ctx._init_exact(st.mw, wd)
+        C.fp8_cast_transpose(wd, st.w8, st.w8t, ctx.scale[st.mw:st.mw + 1], ctx.amax[st.mw:st.mw + 1], E4M3)
+        st.key = key
+    return st
+
+
+class Fp8Linear:
+    """Linear arithmetic for ops.transformer blocks: fp8 forward / dgrad, bf16 wgrad."""
+
+    @staticmethod
+    def fwd(x, w, bias=None, gelu_aux=None, res=None):
+        C = require_native()
+        ctx = context(x.device)
+        st = weight_fp8(w, ctx)
+        x8 = ctx.cast(x, st.mx, E4M3)
+        y = torch.empty(x.shape[0], w.shape[0], dtype=torch.bfloat16, device=x.device)
+        C.gemm_f8(x8, st.w8, y, E4M3, E4M3, ctx.inv(st.mx), ctx.inv(st.mw), bias=bias, aux=gelu_aux, res=res,
+                  mode=1 if gelu_aux is not None else 0)
+        return y
+
+    @staticmethod
+    def dgrad(dy, w, out, aux=None, res=None):
+        C = require_native()
+        ctx = context(dy.device)
+        st = weight_fp8(w, ctx)
+        dy8 = ctx.cast(dy, st.mdy, E5M2)
+        C.gemm_f8(dy8, st.w8t, out, E5M2, E4M3, ctx.inv(st.mdy), ctx.inv(st.mw), aux=aux,
+                  mode=2 if aux is not None else 0, res=res)
+        return out
+
+
+FP8 = Fp8Linear()

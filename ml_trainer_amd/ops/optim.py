@@ -122,6 +122,7 @@ class FusedOptimizer(torch.optim.Optimizer):
                     fp.mark_shadow_fresh()  # the kernel rewrote the bf16 copy of every updated weight
             else:
                 _cpu_update(h, float(self._steps[gi]), fp.data, fp.grad, self._s1[gi], self._s2[gi])
+            fp.generation += 1  # weights changed: derived copies (fp8 casts) are stale
         return loss
 
     # ------------------------------------------------------------------

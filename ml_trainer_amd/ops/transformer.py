@@ -19,6 +19,9 @@ Blocks (one autograd node each, so the backward can fuse across ops):
   bias gradient of the block's last linear layer (no separate pass over dy).
 * ``layer_norm``, ``embeddings``.
 
+The linear-layer arithmetic is pluggable (``impl``): ``BF16`` (bf16 operands) or
+``ops.fp8.FP8`` (OCP fp8 forward / dgrad GEMMs with delayed per-tensor scaling; wgrad bf16).
+
 Linear layout conventions (nn.Linear weight [out, in]):
   fwd   y  = x . W^T         gemm(x, W, a_mn=0, b_mn=0)
   dgrad dx = dy . W          gemm(dy, W, a_mn=0, b_mn=1)
@@ -47,9 +50,22 @@ def bf16_weight(p: torch.Tensor) -> torch.Tensor:
     return w
 
 
-def _gemm(C, A, B, out, a_mn, b_mn, **kw):
-    C.gemm(A, B, out, a_mn, b_mn, **kw)
-    return out
+class Bf16Linear:
+    """bf16 operands (bf16 shadows of the fp32 masters), fp32 accumulate, fused epilogues."""
+
+    @staticmethod
+    def fwd(x, w, bias=None, gelu_aux=None, res=None):
+        return linear_fwd(x, bf16_weight(w), bias, gelu_aux=gelu_aux, res=res)
+
+    @staticmethod
+    def dgrad(dy, w, out, aux=None, res=None):
+        """out = dy . W  (* gelu'(aux) when aux is given) (+ res)."""
+        require_native().gemm(dy, bf16_weight(w), out, False, True, aux=aux, mode=2 if aux is not None else 0,
+                              res=res)
+        return out
+
+
+BF16 = Bf16Linear()
 
 
 def linear_fwd(x, w16, bias=None, gelu_aux=None, res=None):
@@ -73,57 +89,52 @@ def colsum(dy):
     return db
 
 
-def _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H):
+def _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl=BF16):
     C = require_native()
-    wqkv16, wo16 = bf16_weight(wqkv), bf16_weight(wo)
-    qkv = linear_fwd(x, wqkv16, bqkv)
+    qkv = impl.fwd(x, wqkv, bqkv)
     attn = torch.empty(B * S, H * 64, dtype=torch.bfloat16, device=x.device)
     lse = torch.empty(B * H * S, dtype=torch.float32, device=x.device)
     C.attn_fwd(qkv, attn, lse, lens, B, S, H, _ATTN_SCALE)
-    y = linear_fwd(attn, wo16, bo, res=x)  # out-proj + bias + residual
-    return y, (x, qkv, attn, lse, wqkv16, wo16)
+    y = impl.fwd(attn, wo, bo, res=x)  # out-proj + bias + residual
+    return y, (x, qkv, attn, lse)
 
 
-def _attn_bwd(saved, lens, B, S, H, dy, dbo=None):
+def _attn_bwd(saved, weights, lens, B, S, H, dy, dbo=None, impl=BF16):
     """Backward of the attention block; `dbo` = precomputed bias grad of the out-proj (fused
     into the LayerNorm backward that produced dy) or None to compute it here."""
     C = require_native()
-    x, qkv, attn, lse, wqkv16, wo16 = saved
+    x, qkv, attn, lse = saved
+    wqkv, wo = weights
     dwo = linear_wgrad(dy, attn)
     if dbo is None:
         dbo = colsum(dy)
-    dattn = torch.empty_like(attn)
-    C.gemm(dy, wo16, dattn, False, True)
+    dattn = impl.dgrad(dy, wo, torch.empty_like(attn))
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
     C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
     dwqkv = linear_wgrad(dqkv, x)
     dbqkv = colsum(dqkv)
-    dx = torch.empty_like(x)
-    C.gemm(dqkv, wqkv16, dx, False, True, res=dy)  # dx = dqkv . Wqkv + dy (residual)
+    dx = impl.dgrad(dqkv, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
     return dx, dwqkv, dbqkv, dwo, dbo
 
 
-def _ffn_fwd(x, w1, b1, w2, b2):
-    w116, w216 = bf16_weight(w1), bf16_weight(w2)
-    pre = torch.empty(x.shape[0], w116.shape[0], dtype=torch.bfloat16, device=x.device)
-    a = linear_fwd(x, w116, b1, gelu_aux=pre)  # a = gelu(pre), pre saved
-    y = linear_fwd(a, w216, b2, res=x)
-    return y, (x, pre, a, w116, w216)
+def _ffn_fwd(x, w1, b1, w2, b2, impl=BF16):
+    pre = torch.empty(x.shape[0], w1.shape[0], dtype=torch.bfloat16, device=x.device)
+    a = impl.fwd(x, w1, b1, gelu_aux=pre)  # a = gelu(pre), pre saved
+    y = impl.fwd(a, w2, b2, res=x)
+    return y, (x, pre, a)
 
 
-def _ffn_bwd(saved, dy, db2=None):
-    C = require_native()
-    x, pre, a, w116, w216 = saved
+def _ffn_bwd(saved, weights, dy, db2=None, impl=BF16):
+    x, pre, a = saved
+    w1, w2 = weights
     dw2 = linear_wgrad(dy, a)
     if db2 is None:
         db2 = colsum(dy)
-    dpre = torch.empty_like(pre)
-    C.gemm(dy, w216, dpre, False, True, aux=pre, mode=2)  # (dy . W2) * gelu'(pre)
+    dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
     dw1 = linear_wgrad(dpre, x)
     db1 = colsum(dpre)
-    dx = torch.empty_like(x)
-    C.gemm(dpre, w116, dx, False, True, res=dy)
+    dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)
     return dx, dw1, db1, dw2, db2
 
 
@@ -156,29 +167,31 @@ _ATTN_SCALE = 1.0 / 8.0  # 1/sqrt(head_dim = 64)
 
 class _AttentionBlock(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wqkv, bqkv, wo, bo, lens, B, S, H):
-        y, saved = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+    def forward(ctx, x, wqkv, bqkv, wo, bo, lens, B, S, H, impl):
+        y, saved = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
         ctx.save_for_backward(*saved)
+        ctx.weights, ctx.impl = (wqkv, wo), impl
         ctx.lens, ctx.dims = lens, (B, S, H)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.contiguous().to(torch.bfloat16)
-        grads = _attn_bwd(ctx.saved_tensors, ctx.lens, *ctx.dims, dy)
-        return grads + (None, None, None, None)
+        grads = _attn_bwd(ctx.saved_tensors, ctx.weights, ctx.lens, *ctx.dims, dy, impl=ctx.impl)
+        return grads + (None, None, None, None, None)
 
 
 class _FFNBlock(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
-        y, saved = _ffn_fwd(x, w1, b1, w2, b2)
+    def forward(ctx, x, w1, b1, w2, b2, impl):
+        y, saved = _ffn_fwd(x, w1, b1, w2, b2, impl)
         ctx.save_for_backward(*saved)
+        ctx.weights, ctx.impl = (w1, w2), impl
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _ffn_bwd(ctx.saved_tensors, dy.contiguous().to(torch.bfloat16))
+        return _ffn_bwd(ctx.saved_tensors, ctx.weights, dy.contiguous().to(torch.bfloat16), impl=ctx.impl) + (None,)
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -199,37 +212,39 @@ class _AttentionLNBlock(torch.autograd.Function):
     gradient (column sums of its dx), so no separate pass over dy."""
 
     @staticmethod
-    def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps):
-        a, s1 = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+    def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps, impl):
+        a, s1 = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
         y, s2 = _ln_fwd(a, gamma, beta, eps)
         ctx.save_for_backward(*s1, *s2)
+        ctx.weights, ctx.impl = (wqkv, wo), impl
         ctx.lens, ctx.dims = lens, (B, S, H)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         t = ctx.saved_tensors
-        da, dg, db, dbo = _ln_bwd(t[6:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
-        dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:6], ctx.lens, *ctx.dims, da, dbo=dbo)
-        return dx, dwqkv, dbqkv, dwo, dbo, dg, db, None, None, None, None, None
+        da, dg, db, dbo = _ln_bwd(t[4:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
+        dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:4], ctx.weights, ctx.lens, *ctx.dims, da, dbo=dbo, impl=ctx.impl)
+        return dx, dwqkv, dbqkv, dwo, dbo, dg, db, None, None, None, None, None, None
 
 
 class _FFNLNBlock(torch.autograd.Function):
     """LN(ffn_block(x)) as one node (FFN2 bias gradient fused into the LayerNorm backward)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, eps):
-        f, s1 = _ffn_fwd(x, w1, b1, w2, b2)
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, eps, impl):
+        f, s1 = _ffn_fwd(x, w1, b1, w2, b2, impl)
         y, s2 = _ln_fwd(f, gamma, beta, eps)
         ctx.save_for_backward(*s1, *s2)
+        ctx.weights, ctx.impl = (w1, w2), impl
         return y
 
     @staticmethod
     def backward(ctx, dy):
         t = ctx.saved_tensors
-        df, dg, db, db2 = _ln_bwd(t[5:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
-        dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:5], df, db2=db2)
-        return dx, dw1, db1, dw2, db2, dg, db, None
+        df, dg, db, db2 = _ln_bwd(t[3:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
+        dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:3], ctx.weights, df, db2=db2, impl=ctx.impl)
+        return dx, dw1, db1, dw2, db2, dg, db, None, None
 
 
 class _Embeddings(torch.autograd.Function):
@@ -260,21 +275,21 @@ class _Embeddings(torch.autograd.Function):
         return None, None, gw, gp, gt, None
 
 
-def attention_block(x, wqkv, bqkv, wo, bo, lens: Optional[torch.Tensor], B: int, S: int, H: int):
-    return _AttentionBlock.apply(x, wqkv, bqkv, wo, bo, lens, B, S, H)
+def attention_block(x, wqkv, bqkv, wo, bo, lens: Optional[torch.Tensor], B: int, S: int, H: int, impl=BF16):
+    return _AttentionBlock.apply(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
 
 
-def ffn_block(x, w1, b1, w2, b2):
-    return _FFNBlock.apply(x, w1, b1, w2, b2)
+def ffn_block(x, w1, b1, w2, b2, impl=BF16):
+    return _FFNBlock.apply(x, w1, b1, w2, b2, impl)
 
 
 def attention_ln_block(x, wqkv, bqkv, wo, bo, gamma, beta, lens: Optional[torch.Tensor], B: int, S: int, H: int,
-                       eps: float):
-    return _AttentionLNBlock.apply(x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps)
+                       eps: float, impl=BF16):
+    return _AttentionLNBlock.apply(x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps, impl)
 
 
-def ffn_ln_block(x, w1, b1, w2, b2, gamma, beta, eps: float):
-    return _FFNLNBlock.apply(x, w1, b1, w2, b2, gamma, beta, eps)
+def ffn_ln_block(x, w1, b1, w2, b2, gamma, beta, eps: float, impl=BF16):
+    return _FFNLNBlock.apply(x, w1, b1, w2, b2, gamma, beta, eps, impl)
 
 
 def layer_norm(x, gamma, beta, eps: float):

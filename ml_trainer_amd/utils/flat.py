@@ -56,6 +56,7 @@ class FlatParams:
                 _OWNER[id(p)] = self
         self.shadow: Optional[torch.Tensor] = None  # bf16 copy of `data` for mixed-precision compute
         self._shadow_ver = -1
+        self.generation = 0  # bumped by every optimizer update (keys caches of derived weight copies)
 
     # ------------------------------------------------------------------
     def segment(self, p: torch.nn.Parameter) -> Tuple[int, int]:

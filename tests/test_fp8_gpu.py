@@ -47,13 +47,17 @@ def test_cast_transpose_and_scale_update(dev):
     assert (y.float() != ref.float()).float().mean().item() < 1e-3
     assert torch.equal(yt.view(torch.uint8), y.view(torch.uint8).t().contiguous())
     torch.testing.assert_close(amax, w.abs().max().view(1))
-    hist = torch.zeros(4, device=dev)
+    hist = torch.zeros(1, 4, device=dev)
     inv = torch.ones(1, device=dev)
-    step = torch.zeros(1, dtype=torch.int64, device=dev)
-    C.fp8_update_scale(hist, amax, scale, inv, step, 0, 0)
+    fmax = torch.tensor([448.0], device=dev)
+    C.fp8_update_scale(hist, amax, scale, inv, fmax, 0, 0)
     torch.testing.assert_close(scale, 448.0 / w.abs().max().view(1))
     torch.testing.assert_close(inv * scale, torch.ones(1, device=dev))
-    assert float(amax) == 0.0 and int(step) == 1
+    assert float(amax) == 0.0
+    # history window: a smaller amax later does not lower the scale until it falls out
+    amax.fill_(1.0)
+    C.fp8_update_scale(hist, amax, scale, inv, fmax, 1, 1)
+    torch.testing.assert_close(scale, 448.0 / (w.abs().max().view(1) * 2))
 
 
 @pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (1, 2), (4, 3)])
@@ -89,3 +93,48 @@ def test_gemm_f8_identity_asymmetric(dev):
     out = torch.empty(M, 64, dtype=torch.float32, device=dev)
     C.gemm_f8(A, B, out, 0, 0, one, one, cfg=1)
     torch.testing.assert_close(out, B.float()[:, :M].t())
+
+
+def _tiny_fp8_pair(dev):
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    torch.manual_seed(0)
+    m8 = BertClassifier(bert_config("bert-tiny", fp8=True)).to(dev)
+    m16 = BertClassifier(bert_config("bert-tiny")).to(dev)
+    m16.load_state_dict(m8.state_dict())
+    return m8, m16
+
+
+def test_fp8_bert_close_to_bf16(dev):
+    import torch.nn.functional as F
+    m8, m16 = _tiny_fp8_pair(dev)
+    ids = torch.randint(5, 1000, (4, 128), device=dev)
+    y = torch.randint(0, 2, (4,), device=dev)
+    o8, o16 = m8(ids), m16(ids)
+    rel = (o8 - o16).norm() / o16.norm()
+    assert rel < 0.1, rel
+    F.cross_entropy(o8, y).backward()
+    F.cross_entropy(o16, y).backward()
+    for (n, p8), p16 in zip(m8.named_parameters(), m16.parameters()):
+        r = (p8.grad - p16.grad).norm() / (p16.grad.norm() + 1e-12)
+        assert r < 0.25, (n, float(r))
+
+
+def test_fp8_bert_trains(dev):
+    import torch.nn.functional as F
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    m8, _ = _tiny_fp8_pair(dev)
+    opt = FusedAdamW(m8.parameters(), lr=3e-4)
+    ids = torch.randint(5, 1000, (8, 128), device=dev)
+    y = torch.randint(0, 2, (8,), device=dev)
+    ids[y == 1, 7] = 3
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = F.cross_entropy(m8(ids), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < 0.5 * losses[0], losses
+    from ml_trainer_amd.ops.fp8 import context
+    ctx = context(ids.device)
+    assert ctx.n > 0 and torch.isfinite(ctx.scale[:ctx.n]).all() and (ctx.scale[:ctx.n] > 0).all()
