@@ -37,9 +37,12 @@ __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d
   return (uint32_t)r;
 }
 
-__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
+// amax is recorded into kAmaxSlots sub-slots (block b -> slot b % kAmaxSlots) so that thousands
+// of blocks do not serialise on one device-scope atomic; update_scale reduces the slots.
+__device__ __forceinline__ void atomic_max_pos(float* slots, float v) {
   // |x| >= 0: IEEE ordering of non-negative floats equals their integer ordering
-  atomicMax(reinterpret_cast<unsigned*>(addr), __float_as_uint(v));
+  atomicMax(reinterpret_cast<unsigned*>(slots + (blockIdx.x + blockIdx.y * gridDim.x) % kAmaxSlots),
+            __float_as_uint(v));
 }
 
 __device__ __forceinline__ void load8(const uint16_t* p, float (&v)[8]) {
@@ -143,15 +146,22 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const float* __
   }
 }
 
-// Batched delayed scaling over n tensors: hist[i][step % H] = amax[i];
-// scale[i] = fmax[i] / (max_h hist[i][h] * 2^margin); inv_scale[i] = 1 / scale[i]; amax[i] = 0.
+// Batched delayed scaling over n tensors: a = max over the amax slots of tensor i;
+// hist[i][step % H] = a; scale[i] = fmax[i] / (max_h hist[i][h] * 2^margin);
+// inv_scale[i] = 1 / scale[i]; slots reset to 0.
 __global__ void update_scale_kernel(float* __restrict__ hist, int H, int n, float* __restrict__ amax,
                                     float* __restrict__ scale, float* __restrict__ inv_scale,
                                     const float* __restrict__ fmax, float margin_pow, int64_t step) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float* h = hist + (int64_t)i * H;
-  h[step % H] = amax[i];
+  float* sl = amax + (int64_t)i * kAmaxSlots;
+  float a = 0.f;
+  for (int k = 0; k < kAmaxSlots; ++k) {
+    a = fmaxf(a, sl[k]);
+    sl[k] = 0.f;
+  }
+  h[step % H] = a;
   float m = 0.f;
   for (int k = 0; k < H; ++k) m = fmaxf(m, h[k]);
   if (m > 0.f && isfinite(m)) {
@@ -159,7 +169,6 @@ __global__ void update_scale_kernel(float* __restrict__ hist, int H, int n, floa
     scale[i] = sc;
     inv_scale[i] = 1.f / sc;
   }
-  amax[i] = 0.f;
 }
 
 static int grid_for(int64_t n8) {

@@ -36,7 +36,8 @@ class Fp8Context:
 
     def __init__(self, device: torch.device, capacity: int = 4096, history: int = 16, margin: int = 0):
         self.device = device
-        self.amax = torch.zeros(capacity, device=device)
+        self.slots = int(require_native().FP8_AMAX_SLOTS)
+        self.amax = torch.zeros(capacity, self.slots, device=device)  # per-tensor amax sub-slots
         self.scale = torch.ones(capacity, device=device)
         self.inv_scale = torch.ones(capacity, device=device)
         self.fmax = torch.zeros(capacity, device=device)
@@ -47,7 +48,7 @@ class Fp8Context:
         self._ready: list = []
 
     def new_meta(self, fmt: int) -> int:
-        if self.n >= self.amax.numel():
+        if self.n >= self.amax.shape[0]:
             raise RuntimeError("fp8 context capacity exhausted")
         i = self.n
         self.fmax[i] = _FMAX[fmt]
@@ -66,7 +67,7 @@ class Fp8Context:
         C = require_native()
         sl = slice(i, i + 1)
         self.amax[sl].zero_()
-        C.fp8_amax(x, self.amax[sl])
+        C.fp8_amax(x, self.amax[i])
         C.fp8_update_scale(self.hist[sl], self.amax[sl], self.scale[sl], self.inv_scale[sl], self.fmax[sl],
                            self.step, self.margin)
         self._ready[i] = True
@@ -75,7 +76,7 @@ class Fp8Context:
         if not self._ready[i]:
             self._init_exact(i, x)
         y = torch.empty(x.shape, dtype=_DT[fmt], device=x.device)
-        require_native().fp8_cast(x, y, self.scale[i:i + 1], self.amax[i:i + 1], fmt)
+        require_native().fp8_cast(x, y, self.scale[i:i + 1], self.amax[i], fmt)
         return y
 
     def inv(self, i: int) -> torch.Tensor:
@@ -129,7 +130,7 @@ def weight_fp8(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
             st.w8t = torch.empty(wd.shape[1], wd.shape[0], dtype=torch.float8_e4m3fn, device=wd.device)
         if not ctx._ready[st.mw]:
             ctx._init_exact(st.mw, wd)
-        C.fp8_cast_transpose(wd, st.w8, st.w8t, ctx.scale[st.mw:st.mw + 1], ctx.amax[st.mw:st.mw + 1], E4M3)
+        C.fp8_cast_transpose(wd, st.w8, st.w8t, ctx.scale[st.mw:st.mw + 1], ctx.amax[st.mw], E4M3)
         st.key = key
     return st
 

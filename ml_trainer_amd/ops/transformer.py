@@ -89,6 +89,46 @@ def colsum(dy):
     return db
 
 
+class _Grads:
+    """Weight / bias gradients of one fused backward.
+
+    When a parameter's ``.grad`` is a view into a FlatParams gradient buffer (fused optimizer /
+    native DDP), the producing kernel accumulates straight into it (GEMM ``accumulate`` epilogue,
+    reduction ``accmask``, embedding atomics): no fp32 temporary, no AccumulateGrad add kernel,
+    and the autograd return value for that parameter is None. The owner is then told the
+    gradient is ready (``FlatParams.notify_grad_ready``) so DDP bucket countdowns still fire.
+    Parameters without a flat gradient get ordinary returned tensors."""
+
+    def __init__(self):
+        self.ready = []
+
+    def sink(self, p):
+        fp = FlatParams.owner(p)
+        g = fp.grad_sink(p) if fp is not None else None
+        if g is not None:
+            self.ready.append(p)
+        return g
+
+    def wgrad(self, p, dy, x):
+        g = self.sink(p)
+        if g is None:
+            return linear_wgrad(dy, x)
+        require_native().gemm(dy, x, g, True, True, accumulate=True)
+        return None
+
+    def colsum(self, p, dy):
+        g = self.sink(p)
+        if g is None:
+            return colsum(dy)
+        require_native().colsum(dy, g, accumulate=True)
+        return None
+
+    def done(self):
+        for p in self.ready:
+            FlatParams.owner(p).notify_grad_ready(p)
+        self.ready = []
+
+
 def _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl=BF16):
     C = require_native()
     qkv = impl.fwd(x, wqkv, bqkv)
@@ -99,21 +139,21 @@ def _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl=BF16):
     return y, (x, qkv, attn, lse)
 
 
-def _attn_bwd(saved, weights, lens, B, S, H, dy, dbo=None, impl=BF16):
-    """Backward of the attention block; `dbo` = precomputed bias grad of the out-proj (fused
-    into the LayerNorm backward that produced dy) or None to compute it here."""
+def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
+    """Backward of the attention block. ``dbo``: "colsum" to reduce dy here, otherwise the
+    out-proj bias gradient already produced by the LayerNorm backward (tensor or None)."""
     C = require_native()
     x, qkv, attn, lse = saved
-    wqkv, wo = weights
-    dwo = linear_wgrad(dy, attn)
-    if dbo is None:
-        dbo = colsum(dy)
+    wqkv, bqkv, wo, bo = params
+    dwo = G.wgrad(wo, dy, attn)
+    if isinstance(dbo, str):
+        dbo = G.colsum(bo, dy)
     dattn = impl.dgrad(dy, wo, torch.empty_like(attn))
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
     C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
-    dwqkv = linear_wgrad(dqkv, x)
-    dbqkv = colsum(dqkv)
+    dwqkv = G.wgrad(wqkv, dqkv, x)
+    dbqkv = G.colsum(bqkv, dqkv)
     dx = impl.dgrad(dqkv, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
     return dx, dwqkv, dbqkv, dwo, dbo
 
@@ -125,15 +165,15 @@ def _ffn_fwd(x, w1, b1, w2, b2, impl=BF16):
     return y, (x, pre, a)
 
 
-def _ffn_bwd(saved, weights, dy, db2=None, impl=BF16):
+def _ffn_bwd(saved, params, dy, G, db2="colsum", impl=BF16):
     x, pre, a = saved
-    w1, w2 = weights
-    dw2 = linear_wgrad(dy, a)
-    if db2 is None:
-        db2 = colsum(dy)
+    w1, b1, w2, b2 = params
+    dw2 = G.wgrad(w2, dy, a)
+    if isinstance(db2, str):
+        db2 = G.colsum(b2, dy)
     dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
-    dw1 = linear_wgrad(dpre, x)
-    db1 = colsum(dpre)
+    dw1 = G.wgrad(w1, dpre, x)
+    db1 = G.colsum(b1, dpre)
     dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)
     return dx, dw1, db1, dw2, db2
 
@@ -148,17 +188,37 @@ def _ln_fwd(x, gamma, beta, eps):
     return y, (x, gamma, mean, rstd)
 
 
-def _ln_bwd(saved, dy, want_dxsum=False):
+def _ln_bwd(saved, beta, dy, G, dxsum_param=None):
+    """LayerNorm backward; with ``dxsum_param`` also the column sums of dx (= that bias's grad).
+    Returns (dx, dgamma|None, dbeta|None, dbias|None)."""
     C = require_native()
     x, gamma, mean, rstd = saved
     D = gamma.numel()
+    dev = x.device
     dx = torch.empty_like(x)
-    part = torch.empty(C.ln_partial_blocks(x.shape[0]) * (3 if want_dxsum else 2) * D, dtype=torch.float32,
-                       device=x.device)
-    dg = torch.empty(D, dtype=torch.float32, device=x.device)
-    db = torch.empty(D, dtype=torch.float32, device=x.device)
-    dxs = torch.empty(D, dtype=torch.float32, device=x.device) if want_dxsum else None
-    C.ln_bwd(dy, x, gamma, mean, rstd, dx, part, dg, db, dxsum=dxs)
+    want = dxsum_param is not None
+    part = torch.empty(C.ln_partial_blocks(x.shape[0]) * (3 if want else 2) * D, dtype=torch.float32, device=dev)
+    sg = FlatParams.owner(gamma)
+    sg = sg.grad_sink(gamma) if sg is not None else None
+    sb = FlatParams.owner(beta)
+    sb = sb.grad_sink(beta) if sb is not None else None
+    acc = sg is not None and sb is not None
+    if acc:
+        G.ready += [gamma, beta]
+        dg = db = None
+        dg_t, db_t = sg, sb
+    else:
+        dg = dg_t = torch.empty(D, dtype=torch.float32, device=dev)
+        db = db_t = torch.empty(D, dtype=torch.float32, device=dev)
+    dxs = dxs_t = None
+    dxs_acc = False
+    if want:
+        so = G.sink(dxsum_param)
+        if so is not None:
+            dxs_t, dxs_acc = so, True
+        else:
+            dxs = dxs_t = torch.empty(D, dtype=torch.float32, device=dev)
+    C.ln_bwd(dy, x, gamma, mean, rstd, dx, part, dg_t, db_t, acc, None, dxsum=dxs_t, dxsum_acc=dxs_acc)
     return dx, dg, db, dxs
 
 
@@ -170,14 +230,16 @@ class _AttentionBlock(torch.autograd.Function):
     def forward(ctx, x, wqkv, bqkv, wo, bo, lens, B, S, H, impl):
         y, saved = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
         ctx.save_for_backward(*saved)
-        ctx.weights, ctx.impl = (wqkv, wo), impl
+        ctx.params, ctx.impl = (wqkv, bqkv, wo, bo), impl
         ctx.lens, ctx.dims = lens, (B, S, H)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        dy = dy.contiguous().to(torch.bfloat16)
-        grads = _attn_bwd(ctx.saved_tensors, ctx.weights, ctx.lens, *ctx.dims, dy, impl=ctx.impl)
+        G = _Grads()
+        grads = _attn_bwd(ctx.saved_tensors, ctx.params, ctx.lens, *ctx.dims, dy.contiguous().to(torch.bfloat16), G,
+                          impl=ctx.impl)
+        G.done()
         return grads + (None, None, None, None, None)
 
 
@@ -186,12 +248,15 @@ class _FFNBlock(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, impl):
         y, saved = _ffn_fwd(x, w1, b1, w2, b2, impl)
         ctx.save_for_backward(*saved)
-        ctx.weights, ctx.impl = (w1, w2), impl
+        ctx.params, ctx.impl = (w1, b1, w2, b2), impl
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _ffn_bwd(ctx.saved_tensors, ctx.weights, dy.contiguous().to(torch.bfloat16), impl=ctx.impl) + (None,)
+        G = _Grads()
+        grads = _ffn_bwd(ctx.saved_tensors, ctx.params, dy.contiguous().to(torch.bfloat16), G, impl=ctx.impl)
+        G.done()
+        return grads + (None,)
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -199,11 +264,14 @@ class _LayerNorm(torch.autograd.Function):
     def forward(ctx, x, gamma, beta, eps):
         y, saved = _ln_fwd(x, gamma, beta, eps)
         ctx.save_for_backward(*saved)
+        ctx.beta = beta
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        dx, dg, db, _ = _ln_bwd(ctx.saved_tensors, dy.contiguous().to(torch.bfloat16))
+        G = _Grads()
+        dx, dg, db, _ = _ln_bwd(ctx.saved_tensors, ctx.beta, dy.contiguous().to(torch.bfloat16), G)
+        G.done()
         return dx, dg, db, None
 
 
@@ -216,15 +284,18 @@ class _AttentionLNBlock(torch.autograd.Function):
         a, s1 = _attn_fwd(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
         y, s2 = _ln_fwd(a, gamma, beta, eps)
         ctx.save_for_backward(*s1, *s2)
-        ctx.weights, ctx.impl = (wqkv, wo), impl
+        ctx.params, ctx.beta, ctx.impl = (wqkv, bqkv, wo, bo), beta, impl
         ctx.lens, ctx.dims = lens, (B, S, H)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         t = ctx.saved_tensors
-        da, dg, db, dbo = _ln_bwd(t[4:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
-        dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:4], ctx.weights, ctx.lens, *ctx.dims, da, dbo=dbo, impl=ctx.impl)
+        G = _Grads()
+        da, dg, db, dbo = _ln_bwd(t[4:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3])
+        dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:4], ctx.params, ctx.lens, *ctx.dims, da, G, dbo=dbo,
+                                               impl=ctx.impl)
+        G.done()
         return dx, dwqkv, dbqkv, dwo, dbo, dg, db, None, None, None, None, None, None
 
 
@@ -236,14 +307,16 @@ class _FFNLNBlock(torch.autograd.Function):
         f, s1 = _ffn_fwd(x, w1, b1, w2, b2, impl)
         y, s2 = _ln_fwd(f, gamma, beta, eps)
         ctx.save_for_backward(*s1, *s2)
-        ctx.weights, ctx.impl = (w1, w2), impl
+        ctx.params, ctx.beta, ctx.impl = (w1, b1, w2, b2), beta, impl
         return y
 
     @staticmethod
     def backward(ctx, dy):
         t = ctx.saved_tensors
-        df, dg, db, db2 = _ln_bwd(t[3:], dy.contiguous().to(torch.bfloat16), want_dxsum=True)
-        dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:3], ctx.weights, df, db2=db2, impl=ctx.impl)
+        G = _Grads()
+        df, dg, db, db2 = _ln_bwd(t[3:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3])
+        dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:3], ctx.params, df, G, db2=db2, impl=ctx.impl)
+        G.done()
         return dx, dw1, db1, dw2, db2, dg, db, None, None
 
 
@@ -258,6 +331,7 @@ class _Embeddings(torch.autograd.Function):
         C.embed_fwd(ids, ttf, bf16_weight(ww), bf16_weight(wp), bf16_weight(wt), out, S)
         ctx.save_for_backward(ids, ttf if ttf is not None else torch.empty(0, dtype=torch.int64))
         ctx.meta = (tt is not None, S, ww.shape, wp.shape, wt.shape)
+        ctx.tables = (ww, wp, wt)
         return out
 
     @staticmethod
@@ -266,13 +340,23 @@ class _Embeddings(torch.autograd.Function):
         ids, ttf = ctx.saved_tensors
         has_tt, S, sw, sp, st = ctx.meta
         dout = dout.contiguous().to(torch.bfloat16)
-        gw = torch.zeros(sw, dtype=torch.float32, device=dout.device)
-        gp = torch.zeros(sp, dtype=torch.float32, device=dout.device)
-        gt = torch.zeros(st, dtype=torch.float32, device=dout.device)
+        G = _Grads()
+        ww, wp, wt = ctx.tables
+        sinks = [G.sink(p) for p in (ww, wp, wt)]
+        if all(s is not None for s in sinks):  # scatter-add straight into the flat gradients
+            gw, gp, gt = sinks
+            ret = (None, None, None)
+        else:
+            G.ready = []
+            gw = torch.zeros(sw, dtype=torch.float32, device=dout.device)
+            gp = torch.zeros(sp, dtype=torch.float32, device=dout.device)
+            gt = torch.zeros(st, dtype=torch.float32, device=dout.device)
+            ret = (gw, gp, gt)
         D = sw[1]
         part = torch.empty(C.ln_partial_blocks(ids.numel()) * 2 * D, dtype=torch.float32, device=dout.device)
         C.embed_bwd(ids, ttf if has_tt else None, dout, gw, gp, gt, part, S)
-        return None, None, gw, gp, gt, None
+        G.done()
+        return (None, None) + ret + (None,)
 
 
 def attention_block(x, wqkv, bqkv, wo, bo, lens: Optional[torch.Tensor], B: int, S: int, H: int, impl=BF16):

@@ -65,6 +65,9 @@ class DistributedDataParallel(nn.Module):
         if mode == "overlap":
             for i, p in enumerate(self.flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            # fused backwards that accumulate straight into the flat gradient notify here instead
+            self._direct_hooks = {id(p): self._make_hook(i) for i, p in enumerate(self.flat.params)}
+            self.flat.grad_ready_hooks.append(lambda p: self._direct_hooks[id(p)](p))
         if broadcast_parameters and self.world_size > 1:
             self.broadcast_state()
 

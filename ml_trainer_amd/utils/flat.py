@@ -57,6 +57,7 @@ class FlatParams:
         self.shadow: Optional[torch.Tensor] = None  # bf16 copy of `data` for mixed-precision compute
         self._shadow_ver = -1
         self.generation = 0  # bumped by every optimizer update (keys caches of derived weight copies)
+        self.grad_ready_hooks: List = []  # called as hook(p) when a fused kernel wrote p's gradient
 
     # ------------------------------------------------------------------
     def segment(self, p: torch.nn.Parameter) -> Tuple[int, int]:
@@ -103,6 +104,22 @@ class FlatParams:
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+
+    # ------------------------------------------------------------------ direct gradient writes
+    def grad_sink(self, p: torch.Tensor) -> Optional[torch.Tensor]:
+        """``p.grad`` when it is this buffer's view of p (a fused backward may then accumulate
+        into it in place), else None."""
+        i = self._index.get(id(p))
+        g = p.grad
+        if i is None or g is None:
+            return None
+        if g.data_ptr() != self.grad.data_ptr() + self.offsets[i] * self.grad.element_size():
+            return None
+        return g
+
+    def notify_grad_ready(self, p: torch.Tensor) -> None:
+        for h in self.grad_ready_hooks:
+            h(p)
 
     # ------------------------------------------------------------------ bf16 shadow
     @staticmethod

@@ -284,3 +284,27 @@ def test_bert_tiny_trains(dev):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_direct_flat_gradients_match_returned(dev):
+    """Fused backwards accumulate straight into FlatParams gradients (no AccumulateGrad); the
+    result must equal the returned-gradient path, accumulate across two backwards, and notify."""
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m1 = BertClassifier(bert_config("bert-tiny")).to(dev)
+    m2 = BertClassifier(bert_config("bert-tiny")).to(dev)
+    m2.load_state_dict(m1.state_dict())
+    fp = FlatParams(m2.parameters())
+    seen = []
+    fp.grad_ready_hooks.append(lambda p: seen.append(id(p)))
+    ids = torch.randint(5, 1000, (2, 128), device=dev)
+    y = torch.tensor([0, 1], device=dev)
+    F.cross_entropy(m1(ids), y).backward()
+    fp.zero_grad()
+    for _ in range(2):
+        F.cross_entropy(m2(ids), y).backward()
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(p2.grad, 2 * p1.grad, rtol=1e-3, atol=1e-5, msg=n)
+    direct = {id(p) for n, p in m2.named_parameters() if not n.startswith(("pooler", "classifier"))}
+    assert direct <= set(seen)
