@@ -61,15 +61,19 @@ def main(args):
     import torch
     from ml_trainer_amd.models import build_model
     from ml_trainer_amd.trainer import Trainer
-    if args.model in ("default", "tiny"):
-        datasets = build_datasets(args)
-    else:
-        from ml_trainer_amd.data.text import SyntheticTextClassification
-        datasets = (SyntheticTextClassification(args.synthetic_size or 4096, seq_len=args.seq_len, seed=args.seed),
-                    SyntheticTextClassification(max((args.synthetic_size or 4096) // 8, 1), seq_len=args.seq_len,
-                                                seed=args.seed + 1))
     torch.manual_seed(args.seed)
     model = build_model(args.model)
+    if args.model in ("default", "tiny", "lenet"):
+        datasets = build_datasets(args)
+    else:  # BERT configs: synthetic token classification (no network for GLUE downloads)
+        from ml_trainer_amd.data.text import SyntheticTextClassification
+        c = model.config
+        seq = min(args.seq_len, c.max_position)
+        n = args.synthetic_size or 4096
+        datasets = (SyntheticTextClassification(n, seq_len=seq, vocab_size=c.vocab_size, num_labels=c.num_labels,
+                                                seed=args.seed, learnable=True),
+                    SyntheticTextClassification(max(n // 8, 1), seq_len=seq, vocab_size=c.vocab_size,
+                                                num_labels=c.num_labels, seed=args.seed + 1, learnable=True))
     config = {
         "seed": args.seed,
         "scheduler": args.scheduler,

@@ -82,3 +82,20 @@ def test_watchdog_fires_and_beats():
     time.sleep(0.6)
     w.stop()
     assert fired and w.fired
+
+
+def test_cli_bert_tiny_cpu(tmp_path):
+    """main.py with a BERT config: synthetic token classification through the same Trainer."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "mo"
+    r = subprocess.run([sys.executable, os.path.join(root, "main.py"), "--model", "bert-tiny", "--synthetic",
+                        "--synthetic_size", "32", "--seq_len", "32", "--epochs", "1", "--batch_size", "8",
+                        "--optimizer", "adamw", "--metric", "accuracy", "--no_parallel", "--no_progress",
+                        "--model_dir", str(out)], capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (out / "model.pth").exists() and (out / "history.pkl").exists()
+    import torch
+    sd = torch.load(out / "model.pth", weights_only=True)
+    assert "layers.0.qkv.weight" in sd
