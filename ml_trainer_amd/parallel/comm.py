@@ -32,14 +32,13 @@ def create_native_comm(process_group=None, device: Optional[torch.device] = None
     if not dist.is_available() or not dist.is_initialized():
         return None
     world = dist.get_world_size(process_group)
-    if world < 2:
-        return None
+    if world < 2 or dist.get_backend(process_group) != "nccl":
+        return None  # gloo (CPU / tests) keeps torch.distributed; RCCL needs one GPU per rank
     from ml_trainer_amd.ops._ext import require_native
     C = require_native()
     rank = dist.get_rank(process_group)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     obj = [C.Communicator.unique_id() if rank == 0 else None]
     src = 0 if process_group is None else dist.get_global_rank(process_group, 0)
-    dist.broadcast_object_list(obj, src=src, group=process_group, device=dev if dist.get_backend(process_group) ==
-                               "nccl" else None)
+    dist.broadcast_object_list(obj, src=src, group=process_group, device=dev)
     return C.Communicator(obj[0], world, rank, dev.index)

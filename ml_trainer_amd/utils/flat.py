@@ -10,8 +10,9 @@ its ``.grad`` a view into a matching gradient buffer. Consequences:
   needs no copy-in/copy-out (``parallel/ddp.py``);
 * checkpointing the state is a single D2H copy.
 
-Segments start at multiples of ``align`` elements (16 B for fp32) so kernels
-can use float4 accesses on any parameter.
+Segments start at multiples of ``align`` elements (default 16: 64 B of fp32, 32 B of the
+bf16 shadow) so kernels can use 16-byte vector accesses on any parameter and on its bf16
+shadow view (the bf16 GEMM / embedding kernels require 16-byte aligned operands).
 """
 from __future__ import annotations
 
@@ -30,7 +31,7 @@ def _round_up(x: int, a: int) -> int:
 
 class FlatParams:
     def __init__(self, params: Iterable[torch.nn.Parameter], device: Optional[torch.device] = None,
-                 align: int = 4, reverse: bool = False, dtype: torch.dtype = torch.float32):
+                 align: int = 16, reverse: bool = False, dtype: torch.dtype = torch.float32):
         ps = [p for p in params if p.requires_grad]
         if reverse:
             ps = ps[::-1]

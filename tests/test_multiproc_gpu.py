@@ -1,0 +1,89 @@
+"""Two ranks sharing the one GPU of the test box (gloo process group; RCCL needs one GPU per
+rank): the data-parallel paths that are not the in-graph RCCL one -- the LeNet engine's
+torch.distributed fallback step and the native DDP wrapper around the BERT blocks with direct
+flat-gradient writes (grad_ready notifications) -- must keep the ranks bit-identical."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import dist_env, free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _lenet_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.parallel.sampler import shard_indices
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(rank)  # different init per rank: broadcast must fix it
+    m = MLModel().to(dev)
+    flat = FlatParams(m.parameters())
+    dist.broadcast(flat.data, src=0)
+    opt = build_optimizer("sgd", m.parameters(), lr=1e-2, momentum=0.9, flat=flat)
+    eng = LeNetStepEngine(m, flat, max_batch=16, optimizer=opt, world_size=world)
+    assert eng.comm is None  # gloo: torch.distributed fallback
+    g = torch.Generator().manual_seed(3)
+    N = 256
+    data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=g)
+    targets = torch.randint(0, 10, (N,), generator=g)
+    eng.set_dataset(data, targets, batch_size=16)
+    idx = shard_indices(N, world, rank, shuffle=True, seed=0, epoch=0)
+    eng.start_epoch(torch.as_tensor(idx, dtype=torch.int32))
+    eng.train_steps(16, 6, use_graph=True)
+    torch.cuda.synchronize()
+    torch.save({"p": flat.data.cpu(), "ctrl": eng.ctrl.cpu()}, os.path.join(out_dir, f"l{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def _bert_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(rank)
+    m = BertClassifier(bert_config("bert-tiny")).to(dev)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=1.0, first_bucket_mb=0.5)
+    opt = FusedAdamW(m.parameters(), lr=1e-3, flat=ddp.flat)
+    g = torch.Generator().manual_seed(11 + rank)
+    ids = torch.randint(5, 1000, (2, 128), generator=g).to(dev)
+    y = torch.randint(0, 2, (2,), generator=g).to(dev)
+    for _ in range(3):
+        opt.zero_grad(set_to_none=False)
+        F.cross_entropy(ddp(ids), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    torch.save({"p": ddp.flat.data.cpu(), "g": ddp.flat.grad.cpu()}, os.path.join(out_dir, f"b{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(fn, args=(world, free_port(), d), nprocs=world, join=True)
+        return [torch.load(os.path.join(d, f), weights_only=True) for f in sorted(os.listdir(d))]
+
+
+def test_lenet_engine_two_ranks_stay_in_sync():
+    r = _run(_lenet_worker)
+    assert torch.equal(r[0]["p"], r[1]["p"])
+    assert r[0]["ctrl"].tolist() == [6, 6]
+
+
+def test_bert_ddp_direct_grads_two_ranks():
+    r = _run(_bert_worker)
+    assert torch.equal(r[0]["p"], r[1]["p"])  # all-reduced grads -> identical updates
+    assert torch.equal(r[0]["g"], r[1]["g"])
+    assert r[0]["g"].abs().sum() > 0
