@@ -252,8 +252,9 @@ def main():
         elapsed, total_samples = float(t_max.item()), float(s_sum.item())
     else:
         total_samples = float(samples)
-    # sanity: training actually ran (finite loss accumulated on device)
+    # sanity: training actually ran (finite loss accumulated on device); transport healthy
     loss_sum = float(engine.stats[0].item())
+    engine.check_transport()
     value = total_samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     out = {
@@ -274,6 +275,8 @@ def main():
                    "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
                    "hipgraph_steps": 0 if args.no_graph else args.steps_per_graph,
+                   "dp_transport": engine.dp_transport,
+                   "transport_ms": getattr(engine, "transport_times_ms", None),
                    "loss_finite": math.isfinite(loss_sum)},
     }
     if rank == 0:

@@ -623,6 +623,27 @@ class PyComm {
   Communicator c_;
 };
 
+class PyXgmi {
+ public:
+  PyXgmi(int64_t cap, int world, int rank, int device, int blocks) : x_(cap, world, rank, device, blocks) {}
+  py::bytes handle() const { return py::bytes(x_.handle()); }
+  void open(const std::vector<py::bytes>& hs) {
+    std::vector<std::string> v;
+    for (const auto& h : hs) v.push_back(std::string(h));
+    x_.open(v);
+  }
+  void all_reduce(Tensor t, bool average) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat, "xgmi all_reduce: fp32 device");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "xgmi all_reduce: 16-byte aligned tensor");
+    x_.launch(t.data_ptr<float>(), t.numel(), average ? 1.f / x_.world() : 1.f, cur_stream());
+  }
+  unsigned error() const { return x_.error(); }
+  XgmiAllReduce& raw() { return x_; }
+
+ private:
+  XgmiAllReduce x_;
+};
+
 // Pinned-host staging slots exposed as CPU uint8 tensors (collate straight into them).
 class PyPrefetcher {
  public:
@@ -784,6 +805,18 @@ class LeNetEngine {
   // Data-parallel step (mode & LENET_REDUCE): after the backward kernels, all-reduce the
   // flat gradient (AVG) over the native communicator and apply the flat optimizer with lr /
   // step read from device memory -- all inside the same stream (and graph).
+  void set_xgmi(py::object x) {
+    if (x.is_none()) {
+      xgmi_ = nullptr;
+      xgmi_keep_ = py::none();
+    } else {
+      xgmi_ = &x.cast<PyXgmi&>().raw();
+      TORCH_CHECK(xgmi_->ready() && xgmi_->capacity() >= O_.n, "xgmi all-reduce not opened / too small");
+      xgmi_keep_ = x;
+    }
+    graphs_.clear();
+  }
+
   void set_comm(py::object comm) {
     if (comm.is_none()) {
       comm_ = nullptr;
@@ -807,14 +840,17 @@ class LeNetEngine {
 
   void run(int mode, int B) {
     check_mode(mode, B);
-    launch_step(cfg_, mode, B, P_, A_, O_, comm_, cur_stream());
+    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream());
   }
 
   static void launch_step(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
-                          Communicator* comm, hipStream_t s) {
+                          Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s) {
     launch_lenet(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
     if (mode & LENET_REDUCE) {
-      if (comm && comm->size() > 1) comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
+      if (xgmi && xgmi->world() > 1)
+        xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s);  // one-shot over xGMI (latency-bound bucket)
+      else if (comm && comm->size() > 1)
+        comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
       // ctrl[0] = steps taken (already advanced by the backward kernel) -> Adam t; ctrl[1] -> lr table index
       launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
                         nullptr, nullptr, s);
@@ -833,8 +869,9 @@ class LeNetEngine {
     const LeNetOpt O = O_;
     const int cfg = cfg_;
     Communicator* comm = comm_;
+    XgmiAllReduce* xgmi = xgmi_;
     g->capture([&](hipStream_t s) {
-      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, s);
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s);
     });
     graphs_[key(mode, B, nsteps)] = std::move(g);
   }
@@ -867,6 +904,8 @@ class LeNetEngine {
   Tensor ctrl_keep_;
   Communicator* comm_ = nullptr;
   py::object comm_keep_ = py::none();
+  XgmiAllReduce* xgmi_ = nullptr;
+  py::object xgmi_keep_ = py::none();
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
 };
 
@@ -934,6 +973,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("all_to_all", &PyComm::all_to_all, py::arg("input"), py::arg("output"))
       .def("async_error", &PyComm::async_error)
       .def("abort", &PyComm::abort);
+  py::class_<PyXgmi>(m, "XgmiAllReduce")
+      .def(py::init<int64_t, int, int, int, int>(), py::arg("capacity"), py::arg("world"), py::arg("rank"),
+           py::arg("device"), py::arg("blocks") = 64)
+      .def("handle", &PyXgmi::handle)
+      .def("open", &PyXgmi::open)
+      .def("all_reduce", &PyXgmi::all_reduce, py::arg("tensor"), py::arg("average") = true)
+      .def("error", &PyXgmi::error);
   py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)
@@ -946,6 +992,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int, int, py::dict>())
       .def("set_aug", &LeNetEngine::set_aug)
       .def("set_comm", &LeNetEngine::set_comm)
+      .def("set_xgmi", &LeNetEngine::set_xgmi)
       .def("clear_aug", &LeNetEngine::clear_aug)
       .def("set_ctrl", &LeNetEngine::set_ctrl)
       .def("set_opt", &LeNetEngine::set_opt)

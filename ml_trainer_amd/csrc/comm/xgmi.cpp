@@ -1,0 +1,89 @@
+// Host side of the one-shot xGMI all-reduce (kernels/allreduce.hip).
+#include <cstring>
+#include <stdexcept>
+
+#include "mlt_comm.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+static void hcheck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static size_t region_bytes(int64_t cap, int world, int blocks, size_t* flags_off) {
+  size_t off = ((size_t)2 * cap * sizeof(float) + 255) & ~(size_t)255;
+  *flags_off = off;
+  return off + (size_t)2 * blocks * world * sizeof(uint64_t);
+}
+
+XgmiAllReduce::XgmiAllReduce(int64_t cap_floats, int world, int rank, int device, int blocks)
+    : cap_((cap_floats + 3) & ~(int64_t)3), world_(world), rank_(rank), device_(device), blocks_(blocks) {
+  if (world < 1 || world > kXgmiMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad world/rank");
+  if (blocks < 1 || blocks > 1024) throw std::runtime_error("xgmi: bad block count");
+  size_t foff = 0;
+  bytes_ = region_bytes(cap_, world, blocks, &foff);
+  hcheck(hipSetDevice(device), "hipSetDevice");
+  hcheck(hipExtMallocWithFlags(&region_, bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  hcheck(hipMemset(region_, 0, bytes_), "hipMemset(region)");
+  hcheck(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(unsigned)), "hipMalloc(err)");
+  hcheck(hipMemset(err_, 0, sizeof(unsigned)), "hipMemset(err)");
+  hcheck(hipMalloc(reinterpret_cast<void**>(&seqs_), sizeof(uint64_t) * blocks), "hipMalloc(seqs)");
+  hcheck(hipMemset(seqs_, 0, sizeof(uint64_t) * blocks), "hipMemset(seqs)");
+  hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  peers_host_ = new XgmiPeers();
+  std::memset(peers_host_, 0, sizeof(XgmiPeers));
+}
+
+XgmiAllReduce::~XgmiAllReduce() {
+  for (int q = 0; q < world_; ++q)
+    if (q != rank_ && peer_base_[q]) (void)hipIpcCloseMemHandle(peer_base_[q]);
+  if (region_) (void)hipFree(region_);
+  if (err_) (void)hipFree(err_);
+  if (seqs_) (void)hipFree(seqs_);
+  delete static_cast<XgmiPeers*>(peers_host_);
+}
+
+std::string XgmiAllReduce::handle() const {
+  hipIpcMemHandle_t h;
+  hcheck(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void XgmiAllReduce::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::runtime_error("xgmi: need one handle per rank");
+  hcheck(hipSetDevice(device_), "hipSetDevice");
+  XgmiPeers* P = static_cast<XgmiPeers*>(peers_host_);
+  size_t foff = 0;
+  region_bytes(cap_, world_, blocks_, &foff);
+  for (int q = 0; q < world_; ++q) {
+    void* base = nullptr;
+    if (q == rank_) {
+      base = region_;
+    } else {
+      if (handles[q].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("xgmi: bad handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles[q].data(), sizeof(h));
+      hcheck(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      peer_base_[q] = base;
+    }
+    P->data[q] = static_cast<float*>(base);
+    P->flags[q] = reinterpret_cast<uint64_t*>(static_cast<char*>(base) + foff);
+  }
+  opened_ = true;
+}
+
+void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st) {
+  if (!opened_) throw std::runtime_error("xgmi: open() the peer handles first");
+  if (n > cap_) throw std::runtime_error("xgmi: vector larger than the region capacity");
+  launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale, err_,
+                        st);
+}
+
+unsigned XgmiAllReduce::error() const {
+  unsigned e = 0;
+  hcheck(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "hipMemcpy(err)");
+  return e;
+}
+
+}  // namespace mlt

@@ -11,6 +11,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 namespace mlt {
 
@@ -41,6 +42,37 @@ class Communicator {
  private:
   ncclComm_t comm_ = nullptr;
   int nranks_ = 0, rank_ = 0, device_ = 0;
+};
+
+// One-shot all-reduce over xGMI (see kernels/allreduce.hip). Region = uncached device memory
+// shared with the peers through IPC handles (dmabuf); exchange the handle() bytes out of band
+// (Python passes them through the torch.distributed store) and call open() on every rank.
+class XgmiAllReduce {
+ public:
+  XgmiAllReduce(int64_t cap_floats, int world, int rank, int device, int blocks);
+  ~XgmiAllReduce();
+  XgmiAllReduce(const XgmiAllReduce&) = delete;
+  XgmiAllReduce& operator=(const XgmiAllReduce&) = delete;
+  std::string handle() const;
+  void open(const std::vector<std::string>& handles);
+  bool ready() const { return opened_; }
+  // in-place average (scale = 1/W) or sum of grad[0:n) across the ranks (every rank must make
+  // the same sequence of calls)
+  void launch(float* grad, int64_t n, float scale, hipStream_t st);
+  unsigned error() const;  // nonzero after a peer wait timed out
+  int world() const { return world_; }
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int64_t cap_;
+  int world_, rank_, device_, blocks_;
+  void* region_ = nullptr;
+  size_t bytes_ = 0;
+  void* peer_base_[8] = {nullptr};
+  unsigned* err_ = nullptr;
+  uint64_t* seqs_ = nullptr;
+  bool opened_ = false;
+  void* peers_host_ = nullptr;  // XgmiPeers
 };
 
 }  // namespace mlt

@@ -125,6 +125,15 @@ void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, i
 void launch_fp8_update_scale(float* hist, int H, int n, float* amax, float* scale, float* inv_scale, const float* fmax,
                              int margin, int64_t step, hipStream_t st);
 
+// one-shot xGMI all-reduce (allreduce.hip): peer region pointers indexed by rank
+constexpr int kXgmiMaxRanks = 8;
+struct XgmiPeers {
+  float* data[kXgmiMaxRanks];
+  uint64_t* flags[kXgmiMaxRanks];
+};
+void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
+                           uint64_t* seqs, float scale, unsigned* err, hipStream_t st);
+
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,
                         hipStream_t st);

@@ -1,0 +1,95 @@
+// One-shot all-reduce over xGMI for latency-bound gradient buckets (the LeNet step's single
+// 248 KB bucket; SURVEY.md N12 "custom xGMI one-shot all-reduce for sub-MB buckets").
+//
+// Every rank owns an uncached (fine-grained) region, IPC-mapped into all peers:
+//   data [2][cap] fp32        -- double-buffered by step parity
+//   flags[2][G][W] uint64     -- flags[p][b][q] = last step at which rank q published slice b
+// Block b of every rank owns slice b of the vector:
+//   1. copy its slice of the local gradient into data[p] of its own region, fence (system);
+//   2. store seq into flags[p][b][me] of EVERY peer's region (remote release stores);
+//   3. spin on its own flags[p][b][*] until all W peers published seq (system acquire loads,
+//      bounded by a 2 s wall-clock timeout that raises an error word instead of hanging);
+//   4. sum slice b over the W regions in rank order (same order on every rank -> bit-identical
+//      results everywhere), scale (1/W for AVG), write the local gradient.
+// No second barrier: a rank can only reach step s+2 (and overwrite parity p) after it saw all
+// peers publish step s+1, and a peer publishes s+1 only after its step-s kernel -- including
+// its reads of parity p -- completed (stream order). seq is a per-block device launch counter
+// (monotonic, never reset), so the kernel is replay-safe inside multi-step hipGraphs.
+#include "mlt_common.h"
+#include "mlt_kernels.h"
+
+namespace mlt {
+
+__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__ grad, int64_t n, XgmiPeers P,
+                                                             int rank, int W, int64_t cap,
+                                                             uint64_t* __restrict__ seqs, float scale,
+                                                             unsigned* __restrict__ err) {
+  const int G = gridDim.x, b = blockIdx.x;
+  const uint64_t seq = seqs[b] + 1;  // per-block launch counter: identical on every block and rank
+  const int p = (int)(seq & 1);
+  const int64_t chunk = ((n + G - 1) / G + 3) & ~(int64_t)3;  // float4 granules
+  const int64_t lo = (int64_t)b * chunk, hi = min(n, lo + chunk);
+  float* mine = P.data[rank] + p * cap;
+  // 1. publish this block's slice
+  for (int64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+    if (i + 4 <= hi) {
+      *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(grad + i);
+    } else {
+      for (int64_t j = i; j < hi; ++j) mine[j] = grad[j];
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  // 2. signal every peer
+  if (threadIdx.x < W) {
+    uint64_t* f = P.flags[threadIdx.x] + ((int64_t)p * G + b) * W + rank;
+    __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. wait for all peers' slice b of this step
+  if (threadIdx.x < W) {
+    uint64_t* f = P.flags[rank] + ((int64_t)p * G + b) * W + threadIdx.x;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+      if (wall_clock64() - t0 > 200000000LL) {  // 2 s at the 100 MHz constant clock
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // 4. reduce in rank order
+  for (int64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+    if (i + 4 <= hi) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < W; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(P.data[q] + p * cap + i);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      s.x *= scale;
+      s.y *= scale;
+      s.z *= scale;
+      s.w *= scale;
+      *reinterpret_cast<float4*>(grad + i) = s;
+    } else {
+      for (int64_t j = i; j < hi; ++j) {
+        float s = 0.f;
+        for (int q = 0; q < W; ++q) s += P.data[q][p * cap + j];
+        grad[j] = s * scale;
+      }
+    }
+  }
+  if (threadIdx.x == 0) seqs[b] = seq;  // read again only by the next launch (stream order)
+}
+
+void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
+                           uint64_t* seqs, float scale, unsigned* err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs, scale,
+                     err);
+}
+
+}  // namespace mlt

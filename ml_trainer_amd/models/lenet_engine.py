@@ -65,16 +65,10 @@ class LeNetStepEngine:
         self.eng.set_ctrl(self.ctrl)
         self.offsets = [flat.segment(p)[0] for p in params]
         self.comm = None
+        self.xgmi = None
+        self.dp_transport = "none" if self.world_size == 1 else "torch.distributed"
         if self.world_size > 1:
-            from ml_trainer_amd.parallel.comm import create_native_comm
-            try:
-                self.comm = create_native_comm(process_group, self.device)
-            except RuntimeError as e:  # RCCL bring-up failed: keep the torch.distributed path
-                import warnings
-                warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
-                self.comm = None
-            if self.comm is not None:
-                self.eng.set_comm(self.comm)
+            self._setup_transport(process_group)
         self.optimizer = None
         self.lr_table: Optional[torch.Tensor] = None
         self._use_table = False
@@ -84,6 +78,53 @@ class LeNetStepEngine:
             self.set_optimizer(optimizer)
 
     # ------------------------------------------------------------------ setup
+    def _setup_transport(self, process_group) -> None:
+        """Gradient all-reduce transport for the data-parallel step, chosen by measurement:
+        the one-shot xGMI kernel vs RCCL (both enqueued from C++, so both live inside the step's
+        hipGraph); torch.distributed when neither is available."""
+        import warnings
+        import torch.distributed as dist
+        from ml_trainer_amd.parallel.comm import create_native_comm, create_xgmi_allreduce
+        try:
+            self.comm = create_native_comm(process_group, self.device)
+        except RuntimeError as e:  # RCCL bring-up failed: keep the torch.distributed path
+            warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
+            self.comm = None
+        if self.comm is None:
+            return
+        self.xgmi = create_xgmi_allreduce(process_group, self.flat.numel, self.device)
+        use_xgmi = False
+        if self.xgmi is not None:
+            t = self.flat.grad.clone()
+            times = []
+            for fn in (lambda: self.xgmi.all_reduce(t, True), lambda: self.comm.all_reduce(t, "avg")):
+                for _ in range(5):
+                    fn()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(50):
+                    fn()
+                e.record()
+                e.synchronize()
+                times.append(s.elapsed_time(e) / 50)
+            decision = torch.tensor([1.0 if times[0] < times[1] else 0.0] + times, device=self.device)
+            dist.broadcast(decision, src=0 if process_group is None else dist.get_global_rank(process_group, 0),
+                           group=process_group)
+            use_xgmi = bool(decision[0].item() > 0.5)
+            self.transport_times_ms = {"xgmi": float(decision[1]), "rccl": float(decision[2])}
+        if use_xgmi:
+            self.eng.set_xgmi(self.xgmi)
+            self.dp_transport = "xgmi-oneshot"
+        else:
+            self.eng.set_comm(self.comm)
+            self.dp_transport = "rccl"
+
+    def check_transport(self) -> None:
+        """Raise if the one-shot all-reduce ever timed out waiting for a peer (its kernel never
+        hangs: after 2 s it flags the error and continues with incomplete data)."""
+        if self.dp_transport == "xgmi-oneshot" and self.xgmi is not None and self.xgmi.error():
+            raise RuntimeError("xGMI all-reduce: a peer did not arrive within the timeout; gradients are invalid")
+
     def set_optimizer(self, optimizer, lr_table_len: int = 0) -> None:
         self.optimizer = optimizer
         s1, s2 = optimizer.state_buffers(0)
@@ -143,7 +184,7 @@ class LeNetStepEngine:
 
     @property
     def in_graph_collective(self) -> bool:
-        return self.comm is not None
+        return self.dp_transport in ("rccl", "xgmi-oneshot")
 
     def _train_mode(self) -> int:
         C = self.C

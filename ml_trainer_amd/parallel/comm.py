@@ -42,3 +42,62 @@ def create_native_comm(process_group=None, device: Optional[torch.device] = None
     src = 0 if process_group is None else dist.get_global_rank(process_group, 0)
     dist.broadcast_object_list(obj, src=src, group=process_group, device=dev)
     return C.Communicator(obj[0], world, rank, dev.index)
+
+
+def xgmi_enabled() -> bool:
+    return os.environ.get("MLT_XGMI_AR", "1") != "0"
+
+
+def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optional[torch.device] = None,
+                          allow_gloo: bool = False):
+    """One-shot xGMI all-reduce (csrc/kernels/allreduce.hip) for vectors of <= ``capacity`` fp32.
+
+    Collective. IPC handles of every rank's uncached region travel through the process group;
+    a self-test (sum of rank-dependent vectors, bit-exact, bounded wait) must pass on EVERY rank
+    or all ranks get None and keep RCCL. Ranks must share one node (world <= 8)."""
+    import torch.distributed as dist
+    if not xgmi_enabled() or not torch.cuda.is_available() or not dist.is_initialized():
+        return None
+    world = dist.get_world_size(process_group)
+    if world < 2 or world > 8:
+        return None
+    if dist.get_backend(process_group) != "nccl" and not allow_gloo:
+        return None
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    rank = dist.get_rank(process_group)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    coll_dev = dev if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+    x, ok = None, True
+    try:
+        x = C.XgmiAllReduce(int(capacity), world, rank, dev.index)
+        h = x.handle()
+    except RuntimeError:
+        ok, h = False, b""
+    hs = [None] * world
+    dist.all_gather_object(hs, h, group=process_group)
+    if ok and all(len(v) > 0 for v in hs):
+        try:
+            x.open(hs)
+        except RuntimeError:
+            ok = False
+    else:
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=coll_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
+    if int(flag.item()) == 0:
+        return None
+    # self-test: two launches (both buffer parities), exact small-integer sums
+    n = max(4, min(int(capacity), 1 << 16))
+    good = True
+    for it in range(2):
+        t = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97).add_(rank + 1 + it)
+        x.all_reduce(t, average=False)
+        ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
+            world * (world + 1) // 2 + it * world)
+        torch.cuda.synchronize(dev)
+        good = good and bool(torch.equal(t, ref))
+    good = good and x.error() == 0
+    flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=coll_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
+    return x if int(flag.item()) == 1 else None

@@ -424,6 +424,7 @@ class Trainer:
             eng.train_steps(last, 1, use_graph=self.opts.use_graph, steps_per_graph=1)
             bar.update(1)
         loss, acc = eng.read_stats(n)  # the ONE host sync of the epoch
+        eng.check_transport()
         bar.set_postfix(loss=loss, metric=acc if self.metric else None)
         bar.close()
         self.global_step += n
