@@ -115,7 +115,8 @@ def bench_bert(args, world, rank, dev):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu") \
+        if world > 1 else torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -155,10 +156,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # rehearsal knobs for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
+    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
+    backend = os.environ.get("MLT_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", 0 if same_dev else local_rank)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if args.batch is None:
         args.batch = 32
 
@@ -243,7 +250,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    tot = torch.tensor([elapsed, float(samples)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([elapsed, float(samples)], dtype=torch.float64,
+                       device=dev if backend == "nccl" else torch.device("cpu"))
     if world > 1:
         t_max = tot[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)

@@ -90,9 +90,12 @@ class LeNetStepEngine:
         except RuntimeError as e:  # RCCL bring-up failed: keep the torch.distributed path
             warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
             self.comm = None
-        if self.comm is None:
-            return
         self.xgmi = create_xgmi_allreduce(process_group, self.flat.numel, self.device)
+        if self.comm is None:
+            if self.xgmi is not None:  # no RCCL (gloo rehearsal): the one-shot kernel alone
+                self.eng.set_xgmi(self.xgmi)
+                self.dp_transport = "xgmi-oneshot"
+            return
         use_xgmi = False
         if self.xgmi is not None:
             t = self.flat.grad.clone()

@@ -49,13 +49,15 @@ def xgmi_enabled() -> bool:
 
 
 def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optional[torch.device] = None,
-                          allow_gloo: bool = False):
+                          allow_gloo: Optional[bool] = None):
     """One-shot xGMI all-reduce (csrc/kernels/allreduce.hip) for vectors of <= ``capacity`` fp32.
 
     Collective. IPC handles of every rank's uncached region travel through the process group;
     a self-test (sum of rank-dependent vectors, bit-exact, bounded wait) must pass on EVERY rank
     or all ranks get None and keep RCCL. Ranks must share one node (world <= 8)."""
     import torch.distributed as dist
+    if allow_gloo is None:  # rehearsal of the multi-GPU path with several ranks on one GPU (tests)
+        allow_gloo = os.environ.get("MLT_XGMI_ALLOW_GLOO") == "1"
     if not xgmi_enabled() or not torch.cuda.is_available() or not dist.is_initialized():
         return None
     world = dist.get_world_size(process_group)
