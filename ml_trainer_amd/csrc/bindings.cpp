@@ -357,7 +357,7 @@ void fp8_cast(Tensor x, Tensor y, Tensor scale, c10::optional<Tensor> amax, int 
   check_dev(scale, "scale", at::kFloat, 1, 4);
   float* am = nullptr;
   if (amax.has_value()) {
-    check_dev(*amax, "amax", at::kFloat, kAmaxSlots, 4);
+    check_dev(*amax, "amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
     am = amax->data_ptr<float>();
   }
   launch_cast_fp8(x.data_ptr(), x.scalar_type() == at::kFloat, reinterpret_cast<uint8_t*>(y.data_ptr()), x.numel(),
@@ -368,7 +368,7 @@ void fp8_amax(Tensor x, Tensor amax) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
               "fp8_amax x");
   TORCH_CHECK(x.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "fp8_amax alignment");
-  check_dev(amax, "amax", at::kFloat, kAmaxSlots, 4);
+  check_dev(amax, "amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
   launch_amax(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), amax.data_ptr<float>(), cur_stream());
 }
 
@@ -381,7 +381,7 @@ void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::option
   check_dev(scale, "scale", at::kFloat, 1, 4);
   float* am = nullptr;
   if (amax.has_value()) {
-    check_dev(*amax, "amax", at::kFloat, kAmaxSlots, 4);
+    check_dev(*amax, "amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
     am = amax->data_ptr<float>();
   }
   launch_cast_transpose_fp8(w.data_ptr<float>(), reinterpret_cast<uint8_t*>(y.data_ptr()),
@@ -394,8 +394,8 @@ void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, 
                       int margin) {
   TORCH_CHECK(hist.dim() == 2 && hist.is_contiguous(), "hist must be [n, H]");
   const int64_t n_slots = amax.numel();
-  TORCH_CHECK(n_slots % kAmaxSlots == 0, "amax must be [n, ", kAmaxSlots, "]");
-  const int64_t nt = n_slots / kAmaxSlots;
+  TORCH_CHECK(n_slots % (kAmaxSlots * kAmaxStride) == 0, "amax must be [n, ", kAmaxSlots * kAmaxStride, "]");
+  const int64_t nt = n_slots / (kAmaxSlots * kAmaxStride);
   check_dev(amax, "amax", at::kFloat, n_slots, 4);
   check_dev(scale, "scale", at::kFloat, nt, 4);
   TORCH_CHECK(hist.size(0) >= nt, "hist rows");
@@ -945,7 +945,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_cast_transpose", &fp8_cast_transpose, py::arg("w"), py::arg("y"), py::arg("yt"), py::arg("scale"),
         py::arg("amax") = py::none(), py::arg("fmt") = 0);
-  m.attr("FP8_AMAX_SLOTS") = kAmaxSlots;
+  m.attr("FP8_AMAX_SLOTS") = kAmaxSlots * kAmaxStride;  // floats of amax state per tensor
   m.def("fp8_update_scale", &fp8_update_scale, py::arg("hist"), py::arg("amax"), py::arg("scale"),
         py::arg("inv_scale"), py::arg("fmax"), py::arg("step"), py::arg("margin") = 0);
   m.def("gemm_plan", &gemm_plan, py::arg("a_mn"), py::arg("b_mn"), py::arg("M"), py::arg("N"), py::arg("K"),

@@ -115,8 +115,9 @@ void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, co
                     const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux,
                     const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate, float* ws,
                     unsigned* cnt, hipStream_t st);
-// fp8 quantisation (fp8.hip); every amax argument points at kAmaxSlots floats
-constexpr int kAmaxSlots = 64;
+// fp8 quantisation (fp8.hip); every amax argument points at kAmaxSlots slots spaced
+// kAmaxStride floats apart (kAmaxSlots * kAmaxStride floats per tensor)
+constexpr int kAmaxSlots = 64, kAmaxStride = 32;
 void launch_cast_fp8(const void* x, bool x_f32, uint8_t* y, int64_t n, const float* scale, float* amax, int fmt,
                      hipStream_t st);
 void launch_amax(const void* x, bool x_f32, int64_t n, float* amax, hipStream_t st);

@@ -39,10 +39,14 @@ __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d
 
 // amax is recorded into kAmaxSlots sub-slots (block b -> slot b % kAmaxSlots) so that thousands
 // of blocks do not serialise on one device-scope atomic; update_scale reduces the slots.
+// Slots sit kAmaxStride floats apart (one 128-B line each), and a block only issues the
+// atomic when its maximum beats the slot's current value -- after the first few blocks almost
+// none do, so the tail of thousands of same-line device-scope atomics disappears.
 __device__ __forceinline__ void atomic_max_pos(float* slots, float v) {
   // |x| >= 0: IEEE ordering of non-negative floats equals their integer ordering
-  atomicMax(reinterpret_cast<unsigned*>(slots + (blockIdx.x + blockIdx.y * gridDim.x) % kAmaxSlots),
-            __float_as_uint(v));
+  unsigned* a = reinterpret_cast<unsigned*>(slots + ((blockIdx.x + blockIdx.y * gridDim.x) % kAmaxSlots) * kAmaxStride);
+  const unsigned u = __float_as_uint(v);
+  if (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < u) atomicMax(a, u);
 }
 
 __device__ __forceinline__ void load8(const uint16_t* p, float (&v)[8]) {
@@ -155,11 +159,11 @@ __global__ void update_scale_kernel(float* __restrict__ hist, int H, int n, floa
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float* h = hist + (int64_t)i * H;
-  float* sl = amax + (int64_t)i * kAmaxSlots;
+  float* sl = amax + (int64_t)i * kAmaxSlots * kAmaxStride;
   float a = 0.f;
   for (int k = 0; k < kAmaxSlots; ++k) {
-    a = fmaxf(a, sl[k]);
-    sl[k] = 0.f;
+    a = fmaxf(a, sl[k * kAmaxStride]);
+    sl[k * kAmaxStride] = 0.f;
   }
   h[step % H] = a;
   float m = 0.f;
