@@ -22,6 +22,8 @@
 //
 // Epilogue: each wave stages 64-row halves of its sub-tile through a padded LDS image and
 // writes 4 consecutive columns per lane (bias, GELU / dGELU, residual, accumulate fused).
+#include <cstdlib>
+
 #include "mlt_common.h"
 #include "mlt_gemm.h"
 #include "mlt_kernels.h"
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
                                                              const uint8_t* __restrict__ B, OutT* __restrict__ C,
                                                              int M, int N, int K, int64_t lda, int64_t ldb,
                                                              int64_t ldc, GemmEpi epi, float* __restrict__ ws,
-                                                             unsigned* __restrict__ cnt, int ksteps) {
+                                                             unsigned* __restrict__ cnt, int ksteps, int group_m) {
   using G = TileGeom<BM, BN, WARPS_M>;
   constexpr int WARPS_N = 8 / WARPS_M, WTM = BM / WARPS_M, WTN = BN / WARPS_N, TI = WTM / 16, TJ = WTN / 16;
   constexpr int A_CH = G::A_BYTES / 16 / T_NT, B_CH = G::B_BYTES / 16 / T_NT;
@@ -120,7 +122,17 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
 
   const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
   const int id = xcd_remap(blockIdx.x, tiles);
-  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  // grouped raster: runs of `group_m` tile-rows are walked column by column, so the ~32 blocks
+  // an XCD runs at once share a few A row-panels AND a few B column-panels in its L2
+  const int tiles_m = tiles / tiles_n;
+  int tm, tn;
+  {
+    const int gm = group_m > 0 ? group_m : tiles_m;
+    const int per_group = gm * tiles_n, grp = id / per_group, first_m = grp * gm;
+    const int gsize = min(tiles_m - first_m, gm), r = id - grp * per_group;
+    tm = first_m + r % gsize;
+    tn = r / gsize;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = (wid / WARPS_N) * WTM, wn = (wid % WARPS_N) * WTN;
@@ -381,8 +393,12 @@ void launch_tile(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C,
     attr_set = true;
   }
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  static const int group_m = [] {
+    const char* v = getenv("MLT_GEMM_GROUP_M");
+    return v ? atoi(v) : 8;
+  }();
   hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), G::SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws,
-                     cnt, p.ksteps);
+                     cnt, p.ksteps, group_m);
 }
 
 template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
