@@ -34,7 +34,8 @@ using LeNetDefault = LeNetDims<6, 16, 120, 84, 10>;
 using LeNetTiny = LeNetDims<4, 8, 64, 32, 10>;
 
 constexpr int kTaps1 = 76;        // conv1 wgrad partial: 75 taps + bias
-constexpr int kSlabStride = 128;  // floats per (sample, oc) slab: 512 B, so no two writers share a cache line
+constexpr int kSlabStride = 128;  // floats per (sample group, oc) slab: 512 B, so no two writers share a cache line
+constexpr int kSpb1 = 1;          // samples per conv1-wgrad block (slabs per oc = ceil(B / kSpb1)); 4 measured slower
 
 // ---------------------------------------------------------------------------
 // K1: [augment] + conv1 + bias + ReLU + maxpool2x2.  One block per (sample, out-channel).
@@ -480,9 +481,9 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
 // ---------------------------------------------------------------------------
 // K5: all weight gradients (+ the fused optimizer update when single-process),
 // role-split over blockIdx.x:
-//   [0, B*C1)               conv1 wgrad partial for (sample, oc) -> slab1[b][oc][76]; the LAST
-//                           arriving block of each oc reduces its B slabs (fixed order) into the
-//                           final grad (+ update)
+//   [0, ceil(B/4)*C1)       conv1 wgrad partial for (4-sample group, oc) -> slab1[g][oc][76]; the
+//                           LAST arriving block of each oc reduces its ceil(B/4) slabs (fixed
+//                           order, one round of loads) into the final grad (+ update)
 //   [.., + C2*C1)           conv2 wgrad for (oc, ic) over the whole batch (+ bias when ic == 0)
 //   [.., + nb3 + nb4 + nb5) fc wgrads (+ bias), one float4 of a weight row per thread
 // The last block of the whole launch advances the device step counters.
@@ -501,33 +502,48 @@ struct OptCtx {
   float lr, t;
 };
 
-__device__ __forceinline__ void apply_opt4(const LeNetOpt& O, const OptCtx& oc, int64_t flat_idx, float4 g) {
-  O.g[flat_idx + 0] = g.x;  // keep the gradient visible (inspection / checkpoints)
-  O.g[flat_idx + 1] = g.y;
-  O.g[flat_idx + 2] = g.z;
-  O.g[flat_idx + 3] = g.w;
-  if (!oc.on) return;
-  float4 p = *reinterpret_cast<float4*>(O.p + flat_idx);
-  float4 a = O.s1 ? *reinterpret_cast<float4*>(O.s1 + flat_idx) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 c = O.s2 ? *reinterpret_cast<float4*>(O.s2 + flat_idx) : make_float4(0.f, 0.f, 0.f, 0.f);
-  opt_update(O.h, oc.lr, oc.t, p.x, g.x, a.x, c.x);
-  opt_update(O.h, oc.lr, oc.t, p.y, g.y, a.y, c.y);
-  opt_update(O.h, oc.lr, oc.t, p.z, g.z, a.z, c.z);
-  opt_update(O.h, oc.lr, oc.t, p.w, g.w, a.w, c.w);
-  *reinterpret_cast<float4*>(O.p + flat_idx) = p;
-  if (O.s1) *reinterpret_cast<float4*>(O.s1 + flat_idx) = a;
-  if (O.s2) *reinterpret_cast<float4*>(O.s2 + flat_idx) = c;
+// optimizer state of one float4 / scalar, loaded before the gradient is ready so the loads
+// overlap the gradient computation instead of adding a dependent round trip after it
+struct Opt4 {
+  float4 p, a, c;
+};
+struct Opt1 {
+  float p, a, c;
+};
+__device__ __forceinline__ Opt4 opt_prefetch4(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
+  Opt4 r{};
+  if (!oc.on) return r;
+  r.p = *reinterpret_cast<const float4*>(O.p + i);
+  r.a = O.s1 ? *reinterpret_cast<const float4*>(O.s1 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  r.c = O.s2 ? *reinterpret_cast<const float4*>(O.s2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  return r;
 }
-
-__device__ __forceinline__ void apply_opt1(const LeNetOpt& O, const OptCtx& oc, int64_t flat_idx, float g) {
-  O.g[flat_idx] = g;
+__device__ __forceinline__ Opt1 opt_prefetch1(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
+  Opt1 r{};
+  if (!oc.on) return r;
+  r.p = O.p[i];
+  r.a = O.s1 ? O.s1[i] : 0.f;
+  r.c = O.s2 ? O.s2[i] : 0.f;
+  return r;
+}
+__device__ __forceinline__ void apply_pre4(const LeNetOpt& O, const OptCtx& oc, int64_t i, float4 g, Opt4 st) {
+  *reinterpret_cast<float4*>(O.g + i) = g;  // keep the gradient visible (inspection / checkpoints)
   if (!oc.on) return;
-  float p = O.p[flat_idx];
-  float a = O.s1 ? O.s1[flat_idx] : 0.f, c = O.s2 ? O.s2[flat_idx] : 0.f;
-  opt_update(O.h, oc.lr, oc.t, p, g, a, c);
-  O.p[flat_idx] = p;
-  if (O.s1) O.s1[flat_idx] = a;
-  if (O.s2) O.s2[flat_idx] = c;
+  opt_update(O.h, oc.lr, oc.t, st.p.x, g.x, st.a.x, st.c.x);
+  opt_update(O.h, oc.lr, oc.t, st.p.y, g.y, st.a.y, st.c.y);
+  opt_update(O.h, oc.lr, oc.t, st.p.z, g.z, st.a.z, st.c.z);
+  opt_update(O.h, oc.lr, oc.t, st.p.w, g.w, st.a.w, st.c.w);
+  *reinterpret_cast<float4*>(O.p + i) = st.p;
+  if (O.s1) *reinterpret_cast<float4*>(O.s1 + i) = st.a;
+  if (O.s2) *reinterpret_cast<float4*>(O.s2 + i) = st.c;
+}
+__device__ __forceinline__ void apply_pre1(const LeNetOpt& O, const OptCtx& oc, int64_t i, float g, Opt1 st) {
+  O.g[i] = g;
+  if (!oc.on) return;
+  opt_update(O.h, oc.lr, oc.t, st.p, g, st.a, st.c);
+  O.p[i] = st.p;
+  if (O.s1) O.s1[i] = st.a;
+  if (O.s2) O.s2[i] = st.c;
 }
 
 template <int NCOLS>
@@ -538,9 +554,12 @@ __device__ __forceinline__ void fc_wgrad_block(int blk, int nrows, int B, const 
   const int item = blk * 256 + threadIdx.x;
   if (item >= nrows * NV) return;
   const int j = item / NV, v = item - j * NV;
+  const Opt4 pw = opt_prefetch4(O, oc, offW + 4 * (int64_t)item);
+  const Opt1 pb = v == 0 ? opt_prefetch1(O, oc, offb + j) : Opt1{};
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float bacc = 0.f;
   const float4* x4 = reinterpret_cast<const float4*>(X);
+#pragma unroll 4
   for (int b0 = 0; b0 < B; b0 += 8) {
     float d[8];
     float4 xv[8];
@@ -560,8 +579,8 @@ __device__ __forceinline__ void fc_wgrad_block(int blk, int nrows, int B, const 
       bacc += d[u];
     }
   }
-  apply_opt4(O, oc, offW + 4 * (int64_t)item, acc);
-  if (v == 0) apply_opt1(O, oc, offb + j, bacc);
+  apply_pre4(O, oc, offW + 4 * (int64_t)item, acc, pw);
+  if (v == 0) apply_pre1(O, oc, offb + j, bacc, pb);
 }
 
 template <class D>
@@ -570,8 +589,10 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
   constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
   constexpr int NB3 = (F1 * (FLAT / 4) + 255) / 256, NB4 = (F2 * (F1 / 4) + 255) / 256,
                 NB5 = (NC * (F2 / 4) + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float lds[8192];
-  const int nA = B * C1, nblk = nA + C2 * C1 + NB3 + NB4 + NB5;
+  __shared__ __attribute__((aligned(16))) float lds[kSpb1 * (3072 + 2 * 196) + 3 * kTaps1 + 4 > 8192
+                                                        ? kSpb1 * (3072 + 2 * 196) + 3 * kTaps1 + 4
+                                                        : 8192];
+  const int nA = (B + kSpb1 - 1) / kSpb1 * C1, nblk = nA + C2 * C1 + NB3 + NB4 + NB5;
   int blk = blockIdx.x;
   const int t = threadIdx.x;
   // The step counters are read by every block here and advanced by the last block of the launch.
@@ -585,31 +606,42 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     if (O.lr_ptr) oc.lr = O.lr_ptr[O.lr_table ? sie : 0];
   }
   if (blk < nA) {
-    // conv1: dW1[oc, ic, kh, kw] partial over this sample's 196 pooled cells.
-    const int b = blk / C1, ocn = blk - b * C1;
-    float* xs = lds;                                     // [3][32][32]
-    float* gs = lds + 3072;                              // [196]
-    float* red = lds + 3072 + 256;                       // [3][76]
-    int* pos = reinterpret_cast<int*>(lds + 3072 + 512);  // [196] arg-max position cy*32+cx
-    int* flag = reinterpret_cast<int*>(lds + 3072 + 768);
-    const float4* src = reinterpret_cast<const float4*>(P.x + (int64_t)b * 3072);
-    float4 xv[3];
+    // conv1: dW1[oc, ic, kh, kw] partial over kSpb1 samples x 196 pooled cells.
+    const int bg = blk / C1, ocn = blk - bg * C1, nbg = (B + kSpb1 - 1) / kSpb1;
+    const Opt1 pst = t < kTaps1 ? opt_prefetch1(O, oc, t < 75 ? O.off[0] + ocn * 75 + t : O.off[1] + ocn) : Opt1{};
+    float* xs = lds;                                                // [kSpb1][3][32][32]
+    float* gs = lds + kSpb1 * 3072;                                 // [kSpb1][196]
+    int* pos = reinterpret_cast<int*>(gs + kSpb1 * 196);            // [kSpb1][196] cy*32+cx
+    float* red = reinterpret_cast<float*>(pos + kSpb1 * 196);       // [3][76]
+    int* flag = reinterpret_cast<int*>(red + 3 * kTaps1);
+    float4 xv[kSpb1][3];
+    float gv[kSpb1];
+    int kv[kSpb1];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) xv[i] = src[t + i * 256];
-    float gv = 0.f;
-    int kv = 0;
-    if (t < 196) {
-      const int64_t o = (int64_t)(b * C1 + ocn) * 196 + t;
-      gv = P.g1[o];
-      kv = P.i1[o];
+    for (int j = 0; j < kSpb1; ++j) {  // all loads of the block's samples in flight together
+      const int b = bg * kSpb1 + j;
+      const bool ok = b < B;
+      const float4* src = reinterpret_cast<const float4*>(P.x + (int64_t)(ok ? b : 0) * 3072);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xv[j][i] = ok ? src[t + i * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
+      gv[j] = 0.f;
+      kv[j] = 4;
+      if (ok && t < 196) {
+        const int64_t o = (int64_t)(b * C1 + ocn) * 196 + t;
+        gv[j] = P.g1[o];
+        kv[j] = P.i1[o];
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(xs)[t + i * 256] = xv[i];
-    if (t < 196) {
-      const int k = kv < 4 ? kv : 0;
-      const int py = t / 14, px = t - py * 14;
-      gs[t] = gv;
-      pos[t] = (2 * py + (k >> 1)) * 32 + 2 * px + (k & 1);
+    for (int j = 0; j < kSpb1; ++j) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(xs + j * 3072)[t + i * 256] = xv[j][i];
+      if (t < 196) {
+        const int k = kv[j] < 4 ? kv[j] : 0;
+        const int py = t / 14, px = t - py * 14;
+        gs[j * 196 + t] = kv[j] < 4 ? gv[j] : 0.f;  // dead cells (and padding samples) add nothing
+        pos[j * 196 + t] = (2 * py + (k >> 1)) * 32 + 2 * px + (k & 1);
+      }
     }
     __syncthreads();
     if (t < 3 * kTaps1) {
@@ -617,12 +649,17 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
       float acc = 0.f;
       if (tap < 75) {
         const int ic = tap / 25, kh = (tap % 25) / 5, kw = tap % 5;
-        const float* xc = xs + ic * 1024 + kh * 32 + kw;
+#pragma unroll
+        for (int j = 0; j < kSpb1; ++j) {
+          const float* xc = xs + j * 3072 + ic * 1024 + kh * 32 + kw;
 #pragma unroll 8
-        for (int c = s; c < 196; c += 3) acc = fmaf(gs[c], xc[pos[c]], acc);
+          for (int c = s; c < 196; c += 3) acc = fmaf(gs[j * 196 + c], xc[pos[j * 196 + c]], acc);
+        }
       } else {
+#pragma unroll
+        for (int j = 0; j < kSpb1; ++j)
 #pragma unroll 8
-        for (int c = s; c < 196; c += 3) acc += gs[c];
+          for (int c = s; c < 196; c += 3) acc += gs[j * 196 + c];
       }
       red[s * kTaps1 + tap] = acc;
     }
@@ -630,30 +667,30 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     // Write-through (sc1) slab stores: the reducer on any XCD reads them from memory with sc1
     // loads, so neither an agent release nor an acquire fence is needed (Guideline 16, R1).
     if (t < kTaps1)
-      __hip_atomic_store(&P.slab1[(int64_t)(b * C1 + ocn) * kSlabStride + t],
+      __hip_atomic_store(&P.slab1[(int64_t)(bg * C1 + ocn) * kSlabStride + t],
                          red[t] + red[kTaps1 + t] + red[2 * kTaps1 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
     if (t == 0) {
       const unsigned prev = __hip_atomic_fetch_add(&P.counters[ocn], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == (unsigned)(B - 1);
+      const int last = prev == (unsigned)(nbg - 1);
       if (last) __hip_atomic_store(&P.counters[ocn], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
     __syncthreads();
     if (*flag) {
-      // reduce the B slabs of this oc in a fixed order (bitwise reproducible); sc1 loads only
+      // reduce the slabs of this oc in a fixed order (bitwise reproducible); sc1 loads only
       if (t < 3 * kTaps1) {
         const int tap = t % kTaps1, s = t / kTaps1;
         float acc = 0.f;
-        for (int b0 = s; b0 < B; b0 += 3 * 8) {
+        for (int b0 = s; b0 < nbg; b0 += 3 * 8) {
           float v[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const int bb = b0 + 3 * u;
-            v[u] = bb < B ? __hip_atomic_load(&P.slab1[(int64_t)(bb * C1 + ocn) * kSlabStride + tap], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
-                          : 0.f;
+            v[u] = bb < nbg ? __hip_atomic_load(&P.slab1[(int64_t)(bb * C1 + ocn) * kSlabStride + tap], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : 0.f;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) acc += v[u];
@@ -663,8 +700,7 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
       __syncthreads();
       if (t < kTaps1) {
         const float g = red[t] + red[kTaps1 + t] + red[2 * kTaps1 + t];
-        if (t < 75) apply_opt1(O, oc, O.off[0] + ocn * 75 + t, g);
-        else apply_opt1(O, oc, O.off[1] + ocn, g);
+        apply_pre1(O, oc, t < 75 ? O.off[0] + ocn * 75 + t : O.off[1] + ocn, g, pst);
       }
     }
   } else if (blk < nA + C2 * C1) {
@@ -677,6 +713,9 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     float* red = gs + 2 * kWgChunk * 25;               // [9][26]
     constexpr int NT = 26;                             // 25 taps + bias
     const int tap = t % NT, s = t / NT;                // 9 slices (234 threads)
+    const bool owner = t < 25 || (t == 25 && ic == 0);
+    const Opt1 pst = owner ? opt_prefetch1(O, oc, t < 25 ? O.off[2] + (ocn * C1 + ic) * 25 + t : O.off[3] + ocn)
+                           : Opt1{};
     float acc = 0.f;
     for (int b0 = 0; b0 < B; b0 += kWgChunk) {
       const int nb = (B - b0) < kWgChunk ? (B - b0) : kWgChunk;
@@ -730,8 +769,7 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     if (t < NT) {
       float v = 0.f;
       for (int i = 0; i < 9; ++i) v += red[i * NT + t];
-      if (t < 25) apply_opt1(O, oc, O.off[2] + (ocn * C1 + ic) * 25 + t, v);
-      else if (ic == 0) apply_opt1(O, oc, O.off[3] + ocn, v);
+      if (owner) apply_pre1(O, oc, t < 25 ? O.off[2] + (ocn * C1 + ic) * 25 + t : O.off[3] + ocn, v, pst);
     }
   } else {
     int bf = blk - nA - C2 * C1;
@@ -776,7 +814,7 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     hipLaunchKernelGGL(lenet_conv2_dgrad<D>, dim3(B, D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2, P.i1, P.g1);
     constexpr int NB3 = (D::F1 * (D::FLAT / 4) + 255) / 256, NB4 = (D::F2 * (D::F1 / 4) + 255) / 256,
                   NB5 = (D::NC * (D::F2 / 4) + 255) / 256;
-    const int nblk = B * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
+    const int nblk = (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
     hipLaunchKernelGGL(lenet_wgrad<D>, dim3(nblk), dim3(256), 0, st, mode, P, O, B, A.ctrl);
   }
 }
