@@ -49,6 +49,11 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
   const int b = blockIdx.x, oc = blockIdx.y, t = threadIdx.x;
   __shared__ __attribute__((aligned(16))) float xs[3 * 1024];
   __shared__ __attribute__((aligned(16))) uint4 rawimg[192];
+  // filter + bias first: block-uniform scalar loads that overlap the ctrl -> perm -> image chain
+  float wr[75];
+#pragma unroll
+  for (int i = 0; i < 75; ++i) wr[i] = w1[oc * 75 + i];
+  const float bias = b1[oc];
   if (aug.data) {
     const int64_t step = aug.ctrl[0], sie = aug.ctrl[1];
     int64_t pos = sie * aug.batch_stride + b;
@@ -89,8 +94,6 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
   __syncthreads();
   if (t >= 196) return;
   const int py = t / 14, px = t - py * 14, y0 = 2 * py, x0 = 2 * px;
-  const float* w = w1 + oc * 75;
-  const float bias = b1[oc];
   float a00 = bias, a01 = bias, a10 = bias, a11 = bias;
 #pragma unroll
   for (int ic = 0; ic < 3; ++ic) {
@@ -102,7 +105,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
       if (r < 5) {
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const float wv = w[ic * 25 + r * 5 + kw];
+          const float wv = wr[ic * 25 + r * 5 + kw];
           a00 = fmaf(wv, in[kw], a00);
           a01 = fmaf(wv, in[kw + 1], a01);
         }
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
       if (r >= 1) {
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const float wv = w[ic * 25 + (r - 1) * 5 + kw];
+          const float wv = wr[ic * 25 + (r - 1) * 5 + kw];
           a10 = fmaf(wv, in[kw], a10);
           a11 = fmaf(wv, in[kw + 1], a11);
         }
@@ -327,6 +330,8 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
   __shared__ __attribute__((aligned(16))) float slog[64];
   __shared__ __attribute__((aligned(16))) float scratch[SCR];
 
+  // the label is needed only by the CE phase, but loading it now keeps it off the dependent chain
+  const int64_t tgt_pre = (mode & LENET_CE) ? P.targets[b] : 0;
   L1 l1;
   L2 l2;
   L3 l3;
@@ -358,7 +363,7 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
       const float e = lane < NC ? expf(z - mx) : 0.f;
       const float s = wave_sum(e);
       const float lse = mx + logf(s);
-      const int64_t tgt = P.targets[b];
+      const int64_t tgt = tgt_pre;
       const bool valid = tgt >= 0 && tgt < NC;
       const unsigned long long am_mask = __ballot(lane < NC && z == mx);
       const int am = __ffsll((long long)am_mask) - 1;
