@@ -847,9 +847,13 @@ class LeNetEngine {
                           Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s) {
     launch_lenet(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
     if (mode & LENET_REDUCE) {
-      if (xgmi && xgmi->world() > 1)
-        xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s);  // one-shot over xGMI (latency-bound bucket)
-      else if (comm && comm->size() > 1)
+      if (xgmi && xgmi->world() > 1) {
+        // one-shot over xGMI (latency-bound bucket) with the optimizer fused into its epilogue
+        XgmiPostOpt post{O.p, O.s1, O.s2, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl};
+        xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s, &post);
+        return;
+      }
+      if (comm && comm->size() > 1)
         comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
       // ctrl[0] = steps taken (already advanced by the backward kernel) -> Adam t; ctrl[1] -> lr table index
       launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,

@@ -73,11 +73,11 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
   opened_ = true;
 }
 
-void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st) {
+void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st, const XgmiPostOpt* post) {
   if (!opened_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (n > cap_) throw std::runtime_error("xgmi: vector larger than the region capacity");
   launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale, err_,
-                        st);
+                        post, st);
 }
 
 unsigned XgmiAllReduce::error() const {

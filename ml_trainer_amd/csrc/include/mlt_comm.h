@@ -58,7 +58,7 @@ class XgmiAllReduce {
   bool ready() const { return opened_; }
   // in-place average (scale = 1/W) or sum of grad[0:n) across the ranks (every rank must make
   // the same sequence of calls)
-  void launch(float* grad, int64_t n, float scale, hipStream_t st);
+  void launch(float* grad, int64_t n, float scale, hipStream_t st, const struct XgmiPostOpt* post = nullptr);
   unsigned error() const;  // nonzero after a peer wait timed out
   int world() const { return world_; }
   int64_t capacity() const { return cap_; }

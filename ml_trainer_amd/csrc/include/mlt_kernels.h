@@ -132,8 +132,17 @@ struct XgmiPeers {
   float* data[kXgmiMaxRanks];
   uint64_t* flags[kXgmiMaxRanks];
 };
+// optional fused flat-optimizer update of the reduced slice (same semantics as
+// launch_flat_optim with lr / step from device memory)
+struct XgmiPostOpt {
+  float *p, *s1, *s2;
+  OptHyper h;
+  const float* lr_ptr;
+  const int64_t* lr_index_ptr;
+  const int64_t* step_ptr;
+};
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
-                           uint64_t* seqs, float scale, unsigned* err, hipStream_t st);
+                           uint64_t* seqs, float scale, unsigned* err, const XgmiPostOpt* post, hipStream_t st);
 
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,

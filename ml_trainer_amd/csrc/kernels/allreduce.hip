@@ -15,15 +15,19 @@
 // peers publish step s+1, and a peer publishes s+1 only after its step-s kernel -- including
 // its reads of parity p -- completed (stream order). seq is a per-block device launch counter
 // (monotonic, never reset), so the kernel is replay-safe inside multi-step hipGraphs.
+// With POST the averaged gradient slice is consumed right away by the flat optimizer update
+// (the data-parallel step then needs no separate optimizer launch).
 #include "mlt_common.h"
 #include "mlt_kernels.h"
+#include "mlt_optim.h"
 
 namespace mlt {
 
+template <bool POST>
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__ grad, int64_t n, XgmiPeers P,
                                                              int rank, int W, int64_t cap,
                                                              uint64_t* __restrict__ seqs, float scale,
-                                                             unsigned* __restrict__ err) {
+                                                             unsigned* __restrict__ err, XgmiPostOpt O) {
   const int G = gridDim.x, b = blockIdx.x;
   const uint64_t seq = seqs[b] + 1;  // per-block launch counter: identical on every block and rank
   const int p = (int)(seq & 1);
@@ -58,7 +62,24 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
     }
   }
   __syncthreads();
-  // 4. reduce in rank order
+  // 4. reduce in rank order (+ optimizer update)
+  float lr = 0.f, tstep = 0.f;
+  bool has_s1 = false, has_s2 = false;
+  if constexpr (POST) {
+    lr = O.lr_ptr ? O.lr_ptr[O.lr_index_ptr ? (*O.lr_index_ptr - 1) : 0] : O.h.lr;
+    tstep = (float)(*O.step_ptr);
+    has_s2 = O.h.kind == OPT_ADAM || O.h.kind == OPT_ADAMW || O.h.kind == OPT_ADAMAX;
+    has_s1 = has_s2 || O.h.kind == OPT_ADAGRAD || (O.h.kind == OPT_SGD && O.h.momentum != 0.f);
+  }
+  auto post1 = [&](int64_t j, float gj) {
+    if constexpr (POST) {
+      float pv = O.p[j], av = has_s1 ? O.s1[j] : 0.f, bv = has_s2 ? O.s2[j] : 0.f;
+      opt_update(O.h, lr, tstep, pv, gj, av, bv);
+      O.p[j] = pv;
+      if (has_s1) O.s1[j] = av;
+      if (has_s2) O.s2[j] = bv;
+    }
+  };
   for (int64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
     if (i + 4 <= hi) {
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -74,11 +95,24 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
       s.z *= scale;
       s.w *= scale;
       *reinterpret_cast<float4*>(grad + i) = s;
+      if constexpr (POST) {
+        float4 pv = *reinterpret_cast<const float4*>(O.p + i);
+        float4 av = has_s1 ? *reinterpret_cast<const float4*>(O.s1 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 bv = has_s2 ? *reinterpret_cast<const float4*>(O.s2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        opt_update(O.h, lr, tstep, pv.x, s.x, av.x, bv.x);
+        opt_update(O.h, lr, tstep, pv.y, s.y, av.y, bv.y);
+        opt_update(O.h, lr, tstep, pv.z, s.z, av.z, bv.z);
+        opt_update(O.h, lr, tstep, pv.w, s.w, av.w, bv.w);
+        *reinterpret_cast<float4*>(O.p + i) = pv;
+        if (has_s1) *reinterpret_cast<float4*>(O.s1 + i) = av;
+        if (has_s2) *reinterpret_cast<float4*>(O.s2 + i) = bv;
+      }
     } else {
       for (int64_t j = i; j < hi; ++j) {
         float s = 0.f;
         for (int q = 0; q < W; ++q) s += P.data[q][p * cap + j];
         grad[j] = s * scale;
+        post1(j, s * scale);
       }
     }
   }
@@ -86,10 +120,14 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
 }
 
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
-                           uint64_t* seqs, float scale, unsigned* err, hipStream_t st) {
+                           uint64_t* seqs, float scale, unsigned* err, const XgmiPostOpt* post, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs, scale,
-                     err);
+  if (post)
+    hipLaunchKernelGGL(xgmi_allreduce_kernel<true>, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs,
+                       scale, err, *post);
+  else
+    hipLaunchKernelGGL(xgmi_allreduce_kernel<false>, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs,
+                       scale, err, XgmiPostOpt{});
 }
 
 }  // namespace mlt
