@@ -66,6 +66,7 @@ class PinnedPrefetcher {
  private:
   std::vector<void*> slots_;
   std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> before_;
   hipStream_t copy_stream_ = nullptr;
   size_t slot_bytes_;
   int depth_;

@@ -43,9 +43,11 @@ PinnedPrefetcher::PinnedPrefetcher(size_t slot_bytes, int depth, int device)
   hip_check(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate(copy)");
   slots_.resize(depth, nullptr);
   events_.resize(depth, nullptr);
+  before_.resize(depth, nullptr);
   for (int i = 0; i < depth; ++i) {
     hip_check(hipHostMalloc(&slots_[i], slot_bytes, hipHostMallocDefault), "hipHostMalloc");
     hip_check(hipEventCreateWithFlags(&events_[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&before_[i], hipEventDisableTiming), "hipEventCreate");
   }
 }
 
@@ -55,6 +57,7 @@ PinnedPrefetcher::~PinnedPrefetcher() {
       hipEventSynchronize(events_[i]);
       hipEventDestroy(events_[i]);
     }
+    if (before_[i]) hipEventDestroy(before_[i]);
     if (slots_[i]) hipHostFree(slots_[i]);
   }
   if (copy_stream_) hipStreamDestroy(copy_stream_);
@@ -65,14 +68,12 @@ void PinnedPrefetcher::copy_to_device(int i, void* dst, size_t bytes, hipStream_
   if (bytes > slot_bytes_) throw std::invalid_argument("prefetch copy larger than slot");
   // The copy stream must not overwrite `dst` while compute still reads the
   // previous batch there: order the copy after everything queued on compute.
-  hipEvent_t before;
-  hip_check(hipEventCreateWithFlags(&before, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventRecord(before, compute), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(copy_stream_, before, 0), "hipStreamWaitEvent");
+  // (per-slot event: re-recording it is safe, the copy stream's wait captured the prior record)
+  hip_check(hipEventRecord(before_[i], compute), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(copy_stream_, before_[i], 0), "hipStreamWaitEvent");
   hip_check(hipMemcpyAsync(dst, slots_[i], bytes, hipMemcpyHostToDevice, copy_stream_), "hipMemcpyAsync");
   hip_check(hipEventRecord(events_[i], copy_stream_), "hipEventRecord");
   hip_check(hipStreamWaitEvent(compute, events_[i], 0), "hipStreamWaitEvent");
-  hipEventDestroy(before);
 }
 
 bool PinnedPrefetcher::slot_ready(int i) { return hipEventQuery(events_[i]) == hipSuccess; }

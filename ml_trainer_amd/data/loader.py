@@ -71,9 +71,88 @@ class DeviceDataset:
         self.device = device
 
 
+class NativePinnedPrefetcher:
+    """Batches staged through the native pinned-host ring (csrc/runtime/runtime.cpp
+    ``PinnedPrefetcher``): ``depth`` persistent hipHostMalloc slots, hipMemcpyAsync on a
+    dedicated copy stream ordered after the compute stream's prior work, and an event the
+    compute stream waits on -- no per-batch pinned allocation, no host synchronisation
+    except reusing a slot whose previous copy is still in flight."""
+
+    def __init__(self, loader: DataLoader, device: torch.device, depth: int = 3):
+        from ml_trainer_amd.ops._ext import require_native
+        self.C = require_native()
+        self.loader = loader
+        self.device = device
+        self.depth = max(2, int(depth))
+        self.pf = None
+        self.dev_bufs = []
+
+    def __len__(self) -> int:
+        return len(self.loader)
+
+    def _layout(self, x: torch.Tensor, y: torch.Tensor):
+        xb = x.numel() * x.element_size()
+        yo = (xb + 255) // 256 * 256
+        return xb, yo, yo + y.numel() * y.element_size()
+
+    def _ensure(self, nbytes: int) -> None:
+        if self.pf is None or self.pf.slot_bytes < nbytes:
+            self.pf = self.C.PinnedPrefetcher(int(nbytes), self.depth, self.device.index or 0)
+            self.dev_bufs = [torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+                             for _ in range(self.depth)]
+
+    def _stage(self, k: int, batch):
+        x, y = batch
+        y = y if isinstance(y, torch.Tensor) else torch.as_tensor(y)
+        x, y = x.contiguous(), y.contiguous()
+        xb, yo, total = self._layout(x, y)
+        self._ensure(total)
+        self.pf.wait(k)  # the slot's previous H2D copy must be done before we overwrite it
+        slot = self.pf.slot(k)
+        slot[:xb].copy_(x.view(-1).view(torch.uint8))
+        slot[yo:total].copy_(y.view(-1).view(torch.uint8))
+        dev = self.dev_bufs[k]
+        self.pf.copy_to_device(k, dev, total)  # compute stream waits on this copy
+        xd = dev[:xb].view(x.dtype).view(x.shape)
+        yd = dev[yo:total].view(y.dtype).view(y.shape)
+        return xd, yd
+
+    def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
+        # slot k is re-staged only after the batch that used it has been handed out; copy_to_device
+        # orders the new copy after all compute already queued (which includes that batch's use)
+        it = iter(self.loader)
+        pending = []
+        k = 0
+        for _ in range(self.depth - 1):
+            try:
+                pending.append(self._stage(k % self.depth, next(it)))
+                k += 1
+            except StopIteration:
+                break
+        while pending:
+            out = pending.pop(0)
+            try:
+                pending.append(self._stage(k % self.depth, next(it)))
+                k += 1
+            except StopIteration:
+                pass
+            yield out
+
+
 class DevicePrefetcher:
     """Iterate a host ``DataLoader`` with batches staged ``depth`` ahead through
-    pinned memory and copied on a side stream (torch streams are HIP streams)."""
+    pinned memory and copied on a side stream (torch streams are HIP streams).
+    On a GPU with the native extension this delegates to NativePinnedPrefetcher
+    (``MLT_NATIVE_PREFETCH=0`` keeps the torch pinned-memory path)."""
+
+    def __new__(cls, loader: DataLoader, device: torch.device, depth: int = 2):
+        import os
+        device = torch.device(device)
+        if device.type == "cuda" and os.environ.get("MLT_NATIVE_PREFETCH", "1") != "0":
+            from ml_trainer_amd.ops._ext import native_available
+            if native_available():
+                return NativePinnedPrefetcher(loader, device, depth=max(depth, 2) + 1)
+        return super().__new__(cls)
 
     def __init__(self, loader: DataLoader, device: torch.device, depth: int = 2):
         self.loader = loader

@@ -322,3 +322,27 @@ def test_pinned_prefetcher(dev):
         pf.copy_to_device(i % 3, dst, 4096)
         torch.cuda.current_stream().synchronize()
         assert int(dst[0]) == i + 1 and int(dst[-1]) == i + 1
+
+
+def test_device_prefetcher_uses_native_ring(dev):
+    """DevicePrefetcher on a GPU goes through the native pinned ring; every batch arrives intact
+    even though the consumer's (slow, queued) compute reads a slot the ring later refills."""
+    from torch.utils.data import DataLoader, TensorDataset
+    from ml_trainer_amd.data.loader import DevicePrefetcher, NativePinnedPrefetcher
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(200, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (200,), generator=g)
+    loader = DataLoader(TensorDataset(x, y), batch_size=16, shuffle=False)
+    pf = DevicePrefetcher(loader, dev, depth=2)
+    assert isinstance(pf, NativePinnedPrefetcher)
+    sums, labels = [], []
+    for xd, yd in pf:
+        assert xd.device.type == "cuda" and xd.dtype == torch.float32 and yd.dtype == torch.int64
+        for _ in range(20):  # keep the compute stream busy so the copies race ahead if unordered
+            xd = xd * 1.0
+        sums.append(xd.double().sum(dim=(1, 2, 3)))
+        labels.append(yd.clone())
+    torch.cuda.synchronize()
+    assert torch.allclose(torch.cat(sums).cpu(), x.double().sum(dim=(1, 2, 3)))
+    assert torch.equal(torch.cat(labels).cpu(), y)
+    assert len(torch.cat(labels)) == 200  # includes the short last batch
