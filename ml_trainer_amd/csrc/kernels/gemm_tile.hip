@@ -23,6 +23,7 @@
 // Epilogue: each wave stages 64-row halves of its sub-tile through a padded LDS image and
 // writes 4 consecutive columns per lane (bias, GELU / dGELU, residual, accumulate fused).
 #include <cstdlib>
+#include <type_traits>
 
 #include "mlt_common.h"
 #include "mlt_gemm.h"
@@ -91,6 +92,23 @@ __device__ __forceinline__ const uint8_t* glds_src(const uint8_t* __restrict__ b
     const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
     const int col = min(mn0 + c * 8, nmn - 8);
     return base + ((int64_t)kk * ld + col) * ES;
+  }
+}
+
+// the same source as a 32-bit byte offset from the operand base (ping-pong kernel: a uniform
+// 64-bit base in SGPRs + a 32-bit per-lane offset is the glds SADDR form, half the VGPRs)
+template <int ROWS, bool MN, int ES>
+__device__ __forceinline__ uint32_t glds_off(int64_t ld, int i, int mn0, int nmn) {
+  const int e = i * T_NT + threadIdx.x;
+  if (!MN) {
+    const int r = e >> 3, p = e & 7, c = p ^ (r & 7);
+    const int row = min(mn0 + r, nmn - 1);
+    return (uint32_t)(row * ld * ES + c * 16);
+  } else {
+    constexpr int CPR = ROWS / 8;
+    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
+    const int col = min(mn0 + c * 8, nmn - 8);
+    return (uint32_t)((kk * ld + col) * ES);
   }
 }
 
@@ -288,6 +306,293 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
 }
 
 // ---------------------------------------------------------------------------------------------
+// Ping-pong 256x256 kernel (config 5): the two waves that share a SIMD alternate between an
+// MFMA cluster and a load section, and operand DMAs stay in flight across barriers.
+//
+//   * waves 0-3 (group 0) and 4-7 (group 1) sit on the four SIMDs in pairs; group 1 executes
+//     one extra s_barrier up front, so while one group runs the 16 MFMAs of a phase the other
+//     issues its fragment ds_reads and its share of the next DMA (cdna_hip_programming.md §5,
+//     "The 256^2 8-phase template"; T3-T5);
+//   * a K-tile (64 bf16 / 128 fp8 of K) is four phases, one per 64x32 quadrant of the wave's
+//     output (rows {qm*128 + wr*64 ..+64}, cols {qn*128 + wc*32 ..+32}), visited in the order
+//     (0,0) (0,1) (1,1) (1,0) so each phase reads either the A or the B fragments (or both);
+//   * the LDS image of a K-tile is four 16 KiB half-tiles [A0 A1 B0 B1] (128 rows or columns
+//     each), two K-tiles resident (even buffer E, odd buffer O). Each phase stages ONE
+//     half-tile (2 glds per thread): the half whose last ds_read was the previous phase
+//     (WAR: those reads were retired by an lgkmcnt(0) before that phase's first barrier):
+//        phase: 1      2      3      4      5      6      7      8
+//        reads: E q0   E q1   E q2   E q3   O q0   O q1   O q2   O q3
+//        stage: O.B0   E.A0   E.B1   E.A1   E.B0   O.A0   O.B1   O.A1
+//               (t+1)  (t+2)  (t+2)  (t+2)  (t+2)  (t+3)  (t+3)  (t+3)
+//   * RAW: phase 4 waits vmcnt(6) (the three newest half-tiles stay in flight) which retires
+//     all of O; phase 8 likewise retires all of E; the waits precede the phase's first barrier
+//     and the buffer is read one phase later (one barrier more than the stagger needs);
+//   * raw s_barrier (inline asm) -- __syncthreads would drain vmcnt(0) every phase.
+// ---------------------------------------------------------------------------------------------
+#define MLT_PP_SYNC_READS()                                              \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");      \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+  } while (0)
+#define MLT_PP_BARRIER()                                                 \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    asm volatile("s_barrier" ::: "memory");                              \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+  } while (0)
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+template <bool AM, bool BNL, typename OutT, int F8A = -1, int F8B = -1>
+__global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restrict__ A,
+                                                          const uint8_t* __restrict__ B, OutT* __restrict__ C,
+                                                          int M, int N, int K, int64_t lda, int64_t ldb,
+                                                          int64_t ldc, GemmEpi epi, float* __restrict__ ws,
+                                                          unsigned* __restrict__ cnt, int ksteps, int group_m) {
+  constexpr int BM = 256, BN = 256, HALF = 16384, BUF = 4 * HALF, NF = 32;
+  constexpr bool F8 = F8A >= 0;
+  constexpr int ES = F8 ? 1 : 2;
+  static_assert(!F8 || (F8B >= 0 && !AM && !BNL), "fp8 operands must both be fp8 and k-contiguous");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
+  const int id = xcd_remap(blockIdx.x, tiles);
+  int tm, tn;
+  {
+    const int tiles_m = tiles / tiles_n;
+    const int gm = group_m > 0 ? group_m : tiles_m;
+    const int per_group = gm * tiles_n, grp = id / per_group, first_m = grp * gm;
+    const int gsize = min(tiles_m - first_m, gm), r = id - grp * per_group;
+    tm = first_m + r % gsize;
+    tn = r / gsize;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = K / (F8 ? 128 : T_BK);
+  const int kt0 = blockIdx.y * ksteps, kt1 = min(nk, kt0 + ksteps);
+
+  // glds sources of the four half-tiles (0 A0, 1 A1, 2 B0, 3 B1), two 16-B chunks per thread
+  // each: 32-bit offsets from the uniform operand bases (the host guarantees < 4 GiB spans)
+  uint32_t src[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    src[0][i] = glds_off<128, AM, ES>(lda, i, m0, M);
+    src[1][i] = glds_off<128, AM, ES>(lda, i, m0 + 128, M);
+    src[2][i] = glds_off<128, BNL, ES>(ldb, i, n0, N);
+    src[3][i] = glds_off<128, BNL, ES>(ldb, i, n0 + 128, N);
+  }
+  const int64_t astep = AM ? (int64_t)T_BK * lda * ES : 128, bstep = BNL ? (int64_t)T_BK * ldb * ES : 128;
+  auto stage = [&](auto hc, int buf, int kt) {
+    constexpr int h = decltype(hc)::value;
+    const uint8_t* base = h < 2 ? A + (int64_t)kt * astep : B + (int64_t)kt * bstep;
+    uint8_t* dst = smem + buf * BUF + h * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(base + src[h][i]), (lds_void*)(dst + (i * T_NT + wid * 64) * 16),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2];
+  i32x8 af8[4], bf8[2];
+  auto read_a = [&](const uint8_t* h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (F8) {
+        af8[i] = tfrag_f8(h, wr * 64 + 16 * i);
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          af[i][kh] = AM ? tfrag_mn<256>(h, wr * 64 + 16 * i, kh) : tfrag_k(h, wr * 64 + 16 * i, kh);
+      }
+    }
+  };
+  auto read_b = [&](const uint8_t* h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (F8) {
+        bf8[j] = tfrag_f8(h, wc * 32 + 16 * j);
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          bfr[j][kh] = BNL ? tfrag_mn<256>(h, wc * 32 + 16 * j, kh) : tfrag_k(h, wc * 32 + 16 * j, kh);
+      }
+    }
+  };
+  auto mma = [&](auto qmc, auto qnc) {
+    constexpr int qm = decltype(qmc)::value, qn = decltype(qnc)::value, f0 = (qm * 2 + qn) * 8;
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[f0 + i * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af8[i], bf8[j], acc[f0 + i * 2 + j],
+                                                                                  F8A, F8B, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[f0 + i * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kh], bfr[j][kh], acc[f0 + i * 2 + j], 0, 0, 0);
+    }
+    // pin the cluster between its barriers: IR-level passes ignore sched_barrier and may sink
+    // MFMAs past the (volatile-asm) barrier, which stretches operand live ranges into spills
+#pragma unroll
+    for (int f = 0; f < 8; ++f) asm volatile("" ::"v"(acc[f0 + f]));
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one phase: reads of quadrant q from `rb`, stage half `sh` of K-tile `skt` into buffer `sbuf`,
+  // optional counted DMA wait, barrier, MFMA cluster, barrier
+  auto phase = [&](auto qc, auto shc, const uint8_t* rb, int sbuf, int skt, bool do_stage, int wait, bool compute) {
+    constexpr int q = decltype(qc)::value;
+    if (compute) {
+      if constexpr (q == 0) {
+        read_b(rb + 2 * HALF);
+        read_a(rb);
+      } else if constexpr (q == 1) {
+        read_b(rb + 3 * HALF);
+      } else if constexpr (q == 2) {
+        read_a(rb + HALF);
+      } else {
+        read_b(rb + 2 * HALF);
+      }
+    }
+    if (do_stage) stage(shc, sbuf, skt);
+    if (wait == 6)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (wait == 0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    MLT_PP_SYNC_READS();
+    if (compute) {
+      if constexpr (q == 0) mma(IC<0>{}, IC<0>{});
+      else if constexpr (q == 1) mma(IC<0>{}, IC<1>{});
+      else if constexpr (q == 2) mma(IC<1>{}, IC<1>{});
+      else mma(IC<1>{}, IC<0>{});
+    }
+    MLT_PP_BARRIER();
+  };
+
+  // prologue: K-tile kt0 -> E (all four halves), kt0+1 -> O (A0, B1, A1; B0 comes in phase 1)
+  if (kt0 < kt1) {
+    stage(IC<0>{}, 0, kt0);
+    stage(IC<3>{}, 0, kt0);
+    stage(IC<1>{}, 0, kt0);
+    stage(IC<2>{}, 0, kt0);
+  }
+  if (kt0 + 1 < kt1) {
+    stage(IC<0>{}, 1, kt0 + 1);
+    stage(IC<3>{}, 1, kt0 + 1);
+    stage(IC<1>{}, 1, kt0 + 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  MLT_PP_BARRIER();
+  const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // group 1: wave-uniform branch
+  if (late) MLT_PP_BARRIER();
+  const uint8_t* E = smem;
+  const uint8_t* O = smem + BUF;
+  for (int t = kt0; t < kt1; t += 2) {
+    const bool o1 = t + 1 < kt1, e2 = t + 2 < kt1, o3 = t + 3 < kt1;
+    phase(IC<0>{}, IC<2>{}, E, 1, t + 1, o1, -1, true);
+    phase(IC<1>{}, IC<0>{}, E, 0, t + 2, e2, -1, true);
+    phase(IC<2>{}, IC<3>{}, E, 0, t + 2, e2, -1, true);
+    phase(IC<3>{}, IC<1>{}, E, 0, t + 2, e2, e2 ? 6 : 0, true);
+    phase(IC<0>{}, IC<2>{}, O, 0, t + 2, e2, -1, o1);
+    phase(IC<1>{}, IC<0>{}, O, 1, t + 3, o3, -1, o1);
+    phase(IC<2>{}, IC<3>{}, O, 1, t + 3, o3, -1, o1);
+    phase(IC<3>{}, IC<1>{}, O, 1, t + 3, o3, o3 ? 6 : 0, o1);
+  }
+  if (!late) MLT_PP_BARRIER();  // both groups have now executed the same number of barriers
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- split-K: slab publish / last-arriver reduction (as gemm_tile_kernel) ------------------
+  if (gridDim.y > 1) {
+    constexpr int SLAB = BM * BN;
+    const int64_t fo = ((int64_t)wid * NF * 64 + lane) * 4;
+    float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB + fo;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) *reinterpret_cast<f32x4*>(slab + f * 256) = acc[f];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(cnt + id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = tk == gridDim.y - 1;
+      if (last) __hip_atomic_store(cnt + id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    {
+      const float* sl = ws + (int64_t)id * SLAB + fo;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f] = *reinterpret_cast<const f32x4*>(sl + f * 256);
+    }
+    for (int z = 1; z < (int)gridDim.y; ++z) {
+      const float* sl = ws + ((int64_t)z * tiles + id) * SLAB + fo;
+      f32x4 v[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) v[f] = *reinterpret_cast<const f32x4*>(sl + f * 256);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f] += v[f];
+    }
+  }
+
+  // ---- epilogue: one 64x32 quadrant per pass through a padded per-wave LDS image -----------
+  constexpr int EPS = 36;
+  float alpha = epi.alpha;
+  if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
+  if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
+  const int g = lane >> 4, cl = lane & 15;
+  float* cs = reinterpret_cast<float*>(smem) + wid * (64 * EPS);
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+    const int qm = qd >> 1, qn = qd & 1;
+    const int gm0 = m0 + qm * 128 + wr * 64, gn0 = n0 + qn * 128 + wc * 32;
+    float bv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gn = gn0 + 16 * j + cl;
+      bv[j] = (epi.bias && gn < N) ? epi.bias[gn] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[(16 * i + 4 * g + r) * EPS + 16 * j + cl] = acc[qd * 8 + i * 2 + j][r] * alpha + bv[j];
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int e = it * 64 + lane, row = e >> 3, c4 = (e & 7) * 4;
+      const int gm = gm0 + row, gn = gn0 + c4;
+      if (gm >= M || gn >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(cs + row * EPS + c4);
+      float vv[4] = {v.x, v.y, v.z, v.w};
+      epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
+    }
+  }
+}
+#undef MLT_PP_SYNC_READS
+#undef MLT_PP_BARRIER
+
+// ---------------------------------------------------------------------------------------------
 // host: planning + dispatch
 // ---------------------------------------------------------------------------------------------
 void launch_gemm_bf16_128(int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B, void* C, int M,
@@ -300,12 +605,13 @@ struct CfgDesc {
   double rate;  // sustained FLOP/s per CU (relative model, measured ordering)
   int per_cu;   // resident blocks per CU
 };
-constexpr int kNumCfg = 5;
+constexpr int kNumCfg = 6;
 const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2},
                                {256, 256, 1.15e15 / kCUs, 1},
                                {256, 128, 0.92e15 / kCUs, 1},
                                {128, 256, 0.92e15 / kCUs, 1},
-                               {256, 192, 1.05e15 / kCUs, 1}};
+                               {256, 192, 1.05e15 / kCUs, 1},
+                               {256, 256, 1.15e15 / kCUs, 1}};  // 5: ping-pong (rate calibrated below)
 
 // kstep = K elements per 128-byte row step (64 bf16, 128 fp8); speed = MFMA-rate factor
 double est_time(int cfg, int splits, int M, int N, int K, int kstep, double speed) {
@@ -402,6 +708,25 @@ void launch_tile(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C,
 }
 
 template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
+void launch_pp(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda,
+               int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt, hipStream_t st) {
+  constexpr int SMEM = 2 * 4 * 16384;  // two K-tiles; the epilogue image (8 x 64 x 36 fp32) fits inside
+  auto kern = gemm_pp_kernel<AM, BNL, OutT, F8A, F8B>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  static const int group_m = [] {
+    const char* v = getenv("MLT_GEMM_GROUP_M");
+    return v ? atoi(v) : 8;
+  }();
+  hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt,
+                     p.ksteps, group_m);
+}
+
+template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
 void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda,
                 int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt, hipStream_t st) {
   switch (p.cfg) {
@@ -409,6 +734,7 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
     case 2: launch_tile<256, 128, 4, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 3: launch_tile<128, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 4: launch_tile<256, 192, 4, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 5: launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     default: break;
   }
 }

@@ -60,7 +60,7 @@ def test_cast_transpose_and_scale_update(dev):
     torch.testing.assert_close(scale, 448.0 / (w.abs().max().view(1) * 2))
 
 
-@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (1, 2), (4, 3)])
+@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (1, 2), (4, 3), (5, 3)])
 @pytest.mark.parametrize("fmts", [(0, 0), (1, 0), (0, 1)])
 def test_gemm_f8(dev, cfg, splits, fmts):
     C = require_native()

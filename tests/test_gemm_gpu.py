@@ -80,7 +80,8 @@ def test_colsum(dev):
     torch.testing.assert_close(out, X.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (1, 3), (2, 4), (3, 2), (4, 2)])
+@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (1, 3), (2, 4), (3, 2), (4, 2),
+                                        (5, 3), (5, 5)])
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_tile_kernels(dev, cfg, splits, a_mn, b_mn):
     """256-wide global_load_lds kernels (gemm_tile.hip), forced config / split-K, with M/N tails
@@ -132,7 +133,41 @@ def test_identity_asymmetric_tile(dev):
     M = 256
     A = torch.eye(M, dtype=torch.bfloat16, device=dev)
     B = (torch.arange(M * 128, device=dev).view(128, M) % 251).to(torch.bfloat16)
-    for cfg in (1, 2, 3, 4):
+    for cfg in (1, 2, 3, 4, 5):
         out = torch.empty(M, 128, dtype=torch.float32, device=dev)
         C.gemm(A, B, out, False, False, cfg=cfg)
         torch.testing.assert_close(out, B.float().t())
+
+
+@pytest.mark.parametrize("K", [64, 128, 704, 832])
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (1, 1)])
+def test_pingpong_odd_and_short_k(dev, K, a_mn, b_mn):
+    """Config 5 (ping-pong, 2 K-tiles per iteration): odd K-tile counts, 1-2 K-tiles, tails."""
+    C = require_native()
+    M, N = 296, 520
+    g = torch.Generator().manual_seed(K + a_mn)
+    A = _mk((K, M) if a_mn else (M, K), dev, g)
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    out = torch.empty(M, N, device=dev)
+    C.gemm(A, B, out, bool(a_mn), bool(b_mn), cfg=5)
+    torch.testing.assert_close(out, _ref(A, B, a_mn, b_mn), rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_pingpong_matches_tile_kernel_bitwise(dev, a_mn, b_mn):
+    """Race screen: the ping-pong schedule (DMAs in flight across barriers, staggered wave
+    groups) must give bit-identical fp32 results to the 2-phase 256x256 kernel, which
+    accumulates the same products in the same order -- repeated, on a full-chip grid."""
+    C = require_native()
+    M = N = 2048
+    K = 2048
+    g = torch.Generator().manual_seed(11 + 2 * a_mn + b_mn)
+    A = _mk((K, M) if a_mn else (M, K), dev, g)
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    ref = torch.empty(M, N, device=dev)
+    C.gemm(A, B, ref, bool(a_mn), bool(b_mn), cfg=1)
+    out = torch.empty(M, N, device=dev)
+    for _ in range(10):
+        out.fill_(float("nan"))
+        C.gemm(A, B, out, bool(a_mn), bool(b_mn), cfg=5)
+        assert torch.equal(out, ref)
