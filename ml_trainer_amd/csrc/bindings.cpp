@@ -409,7 +409,7 @@ void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, 
 
 py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {
   const GemmPlan p = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
-  return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats);
+  return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);
 }
 
 void colsum(Tensor X, Tensor out, bool accumulate) {
@@ -942,8 +942,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("gemm_f8_plan", [](int64_t M, int64_t N, int64_t K, int cfg, int splits) {
     const GemmPlan p = plan_gemm_f8((int)M, (int)N, (int)K, cfg, splits);
-    return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats);
+    return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);
   }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cfg") = -1, py::arg("splits") = 0);
+  m.def("set_gemm_split_mode", &set_gemm_split_mode, py::arg("mode"));
   m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("fmt") = 0);
   m.def("fp8_amax", &fp8_amax);

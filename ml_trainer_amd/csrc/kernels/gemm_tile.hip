@@ -222,7 +222,10 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   }
 
   // ---- split-K: slab publish / last-arriver reduction --------------------------------------
-  if (gridDim.y > 1) {
+  // (no counters = external mode: every split stores its raw fp32 partial tile row-major into
+  // ws[split][M][N] through the epilogue below and splitk_reduce_kernel finishes the job)
+  const bool ext = gridDim.y > 1 && cnt == nullptr;
+  if (gridDim.y > 1 && !ext) {
     constexpr int SLAB = BM * BN;
     float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB;
 #pragma unroll
@@ -274,13 +277,15 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   float alpha = epi.alpha;
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
+  if (ext) alpha = 1.f;
+  float* const wsz = ws + (int64_t)blockIdx.y * M * N;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (EPR * EPS);
   float bv[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int gn = n0 + wn + 16 * j + cl;
-    bv[j] = (epi.bias && gn < N) ? epi.bias[gn] : 0.f;
+    bv[j] = (epi.bias && gn < N && !ext) ? epi.bias[gn] : 0.f;
   }
 #pragma unroll
   for (int h = 0; h < TI / RI; ++h) {
@@ -299,10 +304,46 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
       const int gm = m0 + wm + EPR * h + row, gn = n0 + wn + c4;
       if (gm >= M || gn >= N) continue;
       const float4 v = *reinterpret_cast<const float4*>(cs + row * EPS + c4);
+      if (ext) {
+        *reinterpret_cast<float4*>(wsz + (int64_t)gm * N + gn) = v;
+        continue;
+      }
       float vv[4] = {v.x, v.y, v.z, v.w};
       epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
     }
   }
+}
+
+// External split-K reduction: out = epilogue(alpha * sum_z ws[z] + bias), summed in split order
+// (bit-identical to the in-kernel last-arriver path), one float4 of a row per thread -- the
+// whole chip reduces, instead of one block per tile reading every slab of its tile serially.
+template <typename OutT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                            OutT* __restrict__ C, int64_t ldc, GemmEpi epi) {
+  const int64_t total = (int64_t)M * N / 4;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= total) return;
+  const float4* w = reinterpret_cast<const float4*>(ws);
+  float4 s = w[q];
+#pragma unroll 4
+  for (int z = 1; z < S; ++z) {
+    const float4 v = w[(int64_t)z * total + q];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  float alpha = epi.alpha;
+  if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
+  if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
+  const int64_t e = q * 4;
+  const int gm = (int)(e / N), gn = (int)(e % N);
+  float vv[4] = {s.x * alpha, s.y * alpha, s.z * alpha, s.w * alpha};
+  if (epi.bias) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) vv[k] += epi.bias[gn + k];
+  }
+  epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -516,7 +557,8 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   __syncthreads();
 
   // ---- split-K: slab publish / last-arriver reduction (as gemm_tile_kernel) ------------------
-  if (gridDim.y > 1) {
+  const bool ext = gridDim.y > 1 && cnt == nullptr;
+  if (gridDim.y > 1 && !ext) {
     constexpr int SLAB = BM * BN;
     const int64_t fo = ((int64_t)wid * NF * 64 + lane) * 4;
     float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB + fo;
@@ -558,6 +600,8 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   float alpha = epi.alpha;
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
+  if (ext) alpha = 1.f;
+  float* const wsz = ws + (int64_t)blockIdx.y * M * N;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (64 * EPS);
 #pragma unroll
@@ -568,7 +612,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int gn = gn0 + 16 * j + cl;
-      bv[j] = (epi.bias && gn < N) ? epi.bias[gn] : 0.f;
+      bv[j] = (epi.bias && gn < N && !ext) ? epi.bias[gn] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -584,6 +628,10 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       const int gm = gm0 + row, gn = gn0 + c4;
       if (gm >= M || gn >= N) continue;
       const float4 v = *reinterpret_cast<const float4*>(cs + row * EPS + c4);
+      if (ext) {
+        *reinterpret_cast<float4*>(wsz + (int64_t)gm * N + gn) = v;
+        continue;
+      }
       float vv[4] = {v.x, v.y, v.z, v.w};
       epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
     }
@@ -613,6 +661,32 @@ const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2},
                                {256, 192, 1.05e15 / kCUs, 1},
                                {256, 256, 1.15e15 / kCUs, 1}};  // 5: ping-pong (rate calibrated below)
 
+// split-K combine override: -1 planner, 0 in-kernel, 1 external (env MLT_GEMM_SPLIT_EXT, or
+// set_gemm_split_mode() from tests / benchmarks)
+int g_split_mode = -2;
+int gemm_split_mode() {
+  if (g_split_mode == -2) {
+    const char* v = getenv("MLT_GEMM_SPLIT_EXT");
+    g_split_mode = v ? atoi(v) : -1;
+  }
+  return g_split_mode;
+}
+
+// Cost of combining split-K partials (fitted to benchmarks/wgrad_bench.py on MI355X). In-kernel:
+// the last-arriving block of each tile reads every slab of its tile on its own -- measured
+// ~40 GB/s effective for that one block, i.e. serial. External: every split writes a row-major
+// partial (overlapped with the other splits' compute) and one grid-wide reduce launch sums them
+// at ~6 TB/s (+ a launch). `ext` receives the cheaper choice.
+double split_cost(int cfg, int splits, int M, int N, int* ext) {
+  const CfgDesc& c = kCfg[cfg];
+  const double slab = (double)c.bm * c.bn * 4.0;
+  const double t_in = splits * slab / 40.0e9 + 1.0e-6;
+  const double t_ext = (double)M * N * 4.0 * (splits + 1.0) / 6.0e12 + 3.0e-6;
+  const bool use_ext = N % 4 == 0 && t_ext < t_in;
+  if (ext) *ext = use_ext ? 1 : 0;
+  return use_ext ? t_ext : t_in;
+}
+
 // kstep = K elements per 128-byte row step (64 bf16, 128 fp8); speed = MFMA-rate factor
 double est_time(int cfg, int splits, int M, int N, int K, int kstep, double speed) {
   const CfgDesc& c = kCfg[cfg];
@@ -623,7 +697,7 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
   const int nk = (K + kstep - 1) / kstep, ks = (nk + splits - 1) / splits;
   const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + 1.0e-6;
   double t = rounds * t_block;
-  if (splits > 1) t += (double)tiles * splits * c.bm * c.bn * 4.0 * 2.0 / 4.0e12 + 2.0e-6;
+  if (splits > 1) t += split_cost(cfg, splits, M, N, nullptr);
   return t;
 }
 
@@ -662,8 +736,16 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
     const CfgDesc& c = kCfg[best_cfg];
     const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     if (p.splits > 1) {
-      p.ws_floats = tiles * p.splits * c.bm * c.bn;
-      p.cnt_ints = tiles;
+      split_cost(best_cfg, p.splits, M, N, &p.ext);
+      const int mode = gemm_split_mode();
+      if (mode >= 0) p.ext = (mode > 0 && N % 4 == 0) ? 1 : 0;
+      if (p.ext) {
+        p.ws_floats = (int64_t)p.splits * M * N;
+        p.cnt_ints = 0;
+      } else {
+        p.ws_floats = tiles * p.splits * c.bm * c.bn;
+        p.cnt_ints = tiles;
+      }
     }
   }
   return p;
@@ -741,6 +823,14 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
 
 // split-K plan without workspace / counters -> unsplit
 bool resolve_split(GemmPlan& p, float* ws, unsigned*& cnt, int K, int kstep) {
+  if (p.splits > 1 && p.ext) {
+    cnt = nullptr;  // external mode is signalled to the kernels by the missing counters
+    if (ws == nullptr) {
+      p.splits = 1;
+      p.ksteps = K / kstep;
+    }
+    return p.splits > 1;
+  }
   if (p.splits > 1 && cnt == nullptr) cnt = split_counters(p.cnt_ints);
   if (p.splits > 1 && (cnt == nullptr || ws == nullptr)) {
     p.splits = 1;
@@ -748,7 +838,17 @@ bool resolve_split(GemmPlan& p, float* ws, unsigned*& cnt, int K, int kstep) {
   }
   return p.splits > 1;
 }
+
+template <typename OutT>
+void launch_split_reduce(const GemmPlan& p, const float* ws, OutT* C, int M, int N, int64_t ldc, const GemmEpi& e,
+                         hipStream_t st) {
+  const int64_t q = (int64_t)M * N / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel<OutT>, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st, ws, p.splits, M,
+                     N, C, ldc, e);
+}
 }  // namespace
+
+void set_gemm_split_mode(int mode) { g_split_mode = mode; }
 
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
   (void)a_mn;
@@ -773,7 +873,7 @@ void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, co
     return;
   }
   GemmPlan p = plan;
-  resolve_split(p, ws, cnt, K, 64);
+  const bool ext = resolve_split(p, ws, cnt, K, 64) && p.ext;
   const uint8_t* a8 = reinterpret_cast<const uint8_t*>(A);
   const uint8_t* b8 = reinterpret_cast<const uint8_t*>(B);
 #define MLT_TILE_CASE(AMV, BNV)                                                                                  \
@@ -782,6 +882,8 @@ void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, co
       launch_cfg<AMV, BNV, float, -1, -1>(p, a8, b8, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);         \
     else                                                                                                         \
       launch_cfg<AMV, BNV, uint16_t, -1, -1>(p, a8, b8, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);   \
+    if (ext && out_f32) launch_split_reduce<float>(p, ws, (float*)C, M, N, ldc, e, st);                          \
+    if (ext && !out_f32) launch_split_reduce<uint16_t>(p, ws, (uint16_t*)C, M, N, ldc, e, st);                   \
     return;                                                                                                      \
   }
   MLT_TILE_CASE(0, 0)
@@ -799,13 +901,15 @@ void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, co
   if (M <= 0 || N <= 0 || plan.cfg < 1) return;
   GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate, inv_scale_a, inv_scale_b};
   GemmPlan p = plan;
-  resolve_split(p, ws, cnt, K, 128);
+  const bool ext = resolve_split(p, ws, cnt, K, 128) && p.ext;
 #define MLT_F8_CASE(FA, FB)                                                                                      \
   if (fmt_a == FA && fmt_b == FB) {                                                                              \
     if (out_f32)                                                                                                 \
       launch_cfg<false, false, float, FA, FB>(p, A, B, (float*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);       \
     else                                                                                                         \
       launch_cfg<false, false, uint16_t, FA, FB>(p, A, B, (uint16_t*)C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); \
+    if (ext && out_f32) launch_split_reduce<float>(p, ws, (float*)C, M, N, ldc, e, st);                          \
+    if (ext && !out_f32) launch_split_reduce<uint16_t>(p, ws, (uint16_t*)C, M, N, ldc, e, st);                   \
     return;                                                                                                      \
   }
   MLT_F8_CASE(0, 0)

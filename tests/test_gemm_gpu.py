@@ -171,3 +171,34 @@ def test_pingpong_matches_tile_kernel_bitwise(dev, a_mn, b_mn):
         out.fill_(float("nan"))
         C.gemm(A, B, out, bool(a_mn), bool(b_mn), cfg=5)
         assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("cfg", [1, 4, 5])
+def test_split_k_external_reduce_bitwise(dev, cfg):
+    """External split-K combine (row-major partials + grid-wide reduce launch) sums the slabs in
+    the same split order as the in-kernel last arriver: identical bits, every epilogue."""
+    C = require_native()
+    M, N, K = 768, 520, 4096
+    g = torch.Generator().manual_seed(cfg)
+    A = _mk((K, M), dev, g)
+    B = _mk((K, N), dev, g)
+    bias = torch.randn(N, device=dev)
+    res = _mk((M, N), dev, g)
+    outs = {}
+    try:
+        for mode in (0, 1):
+            C.set_gemm_split_mode(mode)
+            assert C.gemm_plan(True, True, M, N, K, cfg, 6)[4] == mode
+            o32 = torch.full((M, N), 0.25, device=dev)
+            C.gemm(A, B, o32, True, True, accumulate=True, cfg=cfg, splits=6)
+            o16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            C.gemm(A, B, o16, True, True, bias=bias, aux=aux, mode=1, cfg=cfg, splits=6)
+            o16r = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            C.gemm(A, B, o16r, True, True, res=res, alpha=0.5, cfg=cfg, splits=6)
+            outs[mode] = (o32, o16, aux, o16r)
+    finally:
+        C.set_gemm_split_mode(-1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(outs[1][0], A.float().t() @ B.float() + 0.25, rtol=2e-3, atol=2e-2)
