@@ -33,6 +33,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int AH = 64;  // head dim
 constexpr int AB = 64;  // query / key block
@@ -544,6 +545,349 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ring-staged backward (MLT_ATTN_RING, default on). The register-staged kernels above hold
+// ~180 VGPRs, i.e. 2 waves per SIMD, and wait at the end of every 64-row step for tile loads
+// issued at its start: one HBM/L2 round trip exposed per step. Here the streamed tiles (Q, dO
+// and the LSE / delta rows for dK/dV; K, V for dQ) go HBM -> LDS by global_load_lds into a
+// 4-deep ring, so three steps are in flight while one is computed; a counted vmcnt + raw
+// s_barrier retires one stage per step (cdna_hip_programming.md §5 "Pipelining across
+// barriers"); all LDS lives in ONE __shared__ array (the second-object trap, §5 item 4a).
+// The math and its order are those of the kernels above: bit-identical gradients.
+// ---------------------------------------------------------------------------
+constexpr int kRing = 4;
+constexpr int kTile = AB * 128;  // one 64 x 64 bf16 tile
+
+// glds of a 64x64 bf16 tile into the (row & 7)-swizzled image tile_off() reads: lane-linear
+// LDS destination, swizzle on the per-lane source; rows past nrows_valid re-read the last valid
+// row (their products are masked by the callers). 2 glds per thread (256 threads).
+__device__ __forceinline__ void glds_tile(uint8_t* lds, const uint16_t* __restrict__ g, int64_t ld, int64_t row0,
+                                          int nrows_valid, int col0) {
+  const int wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = (e & 7) ^ (r & 7);
+    const int row = min(r, nrows_valid - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(g + (row0 + row) * ld + col0 + c * 8),
+                                     (lds_void*)(lds + (i * 256 + wid * 64) * 16), 16, 0, 0);
+  }
+}
+
+// ds_read_b64_tr_b16 as inline asm for the ring kernels: through the builtin, hipcc cannot tell
+// the read from the in-flight LDS-DMA writes and puts an s_waitcnt vmcnt(0) in front of it, which
+// drains the whole ring every step. The asm read is invisible to the compiler's waitcnt pass, so
+// its consumers go through frag_tr_wait (lgkmcnt(0) + "+v" dependence + sched_barrier, rule 18).
+__device__ __forceinline__ s16x4 ds_tr_asm(const uint8_t* lds) {
+  s16x4 r;
+  const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>((lds_s16x4*)lds);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ bf16x8 frag_tr_asm(const uint8_t* lds, int r0, int r1, int col) {
+  const int lane = threadIdx.x & 63, i = lane & 15, q = i >> 2, p = i & 3;
+  const int cc = col + 4 * p, chunk = cc >> 3, half = (cc & 7) * 2;
+  const s16x4 lo = ds_tr_asm(lds + tile_off(r0 + q, chunk) + half);
+  const s16x4 hi = ds_tr_asm(lds + tile_off(r1 + q, chunk) + half);
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+template <int N>
+__device__ __forceinline__ void frag_tr_wait(bf16x8 (&f)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(f[k]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void ring_wait(int after) {  // `after` stages issued after the wanted one
+  if (after >= 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 5) : "memory");
+  else if (after == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void ring_wait4(int after) {  // dQ ring: 4 glds per stage
+  if (after >= 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (after == 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NK>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t* __restrict__ qkv,
+                                                                 const uint16_t* __restrict__ dout,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 const int* __restrict__ lens,
+                                                                 uint16_t* __restrict__ dqkv, int S, int H,
+                                                                 float scale) {
+  constexpr int STAGE = 2 * kTile + 2 * AB * 4;  // Q tile, dO tile, lse[64], delta[64]
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
+  int kbk, h, b;
+  block_coords(S, 64 * NK, H, kbk, h, b);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  const int k0b = kbk * (64 * NK);
+  if (k0b >= len) {  // fully masked key block: zero gradients
+    for (int e = threadIdx.x; e < 64 * NK * AH; e += 256) {
+      const int kk = k0b + e / AH, d = e % AH;
+      if (kk < S) {
+        dqkv[(base + kk) * ld + D + h * AH + d] = 0;
+        dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
+      }
+    }
+    return;
+  }
+  const float sl2 = scale * 1.4426950408889634f;
+  const int nqb = (S + AB - 1) / AB;
+  // stage = 5 glds per thread: 2 (Q) + 2 (dO) + 1 (waves 0/2: LSE row, waves 1/3: delta row)
+  auto issue = [&](int slot, int qb) {
+    uint8_t* st = smem + slot * STAGE;
+    const int q0 = qb * AB, nv = min(AB, S - q0);
+    glds_tile(st, qkv, ld, base + q0, nv, h * AH);
+    glds_tile(st + kTile, dout, (int64_t)D, base + q0, nv, h * AH);
+    const int qq = q0 + min(lane, nv - 1);
+    const float* src = (wid & 1) ? delta + (base + qq) * H + h : lse + ((int64_t)b * H + h) * S + qq;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + 2 * kTile + (wid & 1) * AB * 4), 4, 0, 0);
+  };
+  int key[NK];
+  bf16x8 kf[NK][2], vf[NK][2];
+#pragma unroll
+  for (int n = 0; n < NK; ++n) {
+    key[n] = k0b + n * 64 + wid * 16 + i;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      kf[n][kh] = key[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + key[n]) * ld + D + h * AH + kh * 32 + 8 * g)
+                             : bf16x8{};
+      vf[n][kh] = key[n] < S
+                      ? *reinterpret_cast<const bf16x8*>(qkv + (base + key[n]) * ld + 2 * D + h * AH + kh * 32 + 8 * g)
+                      : bf16x8{};
+    }
+  }
+  // the ring prologue goes out after the register loads above, so waiting for those is a
+  // counted vmcnt that leaves the DMAs in flight
+#pragma unroll
+  for (int s0 = 0; s0 < kRing - 1; ++s0)
+    if (s0 < nqb) issue(s0, s0);
+  f32x4 dk[NK][4], dv[NK][4];
+#pragma unroll
+  for (int n = 0; n < NK; ++n)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dk[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  for (int qb = 0; qb < nqb; ++qb) {
+    ring_wait(min(kRing - 2, nqb - 1 - qb));
+    raw_barrier();  // stage qb visible to all waves; everyone is done with slot (qb - 1) % kRing
+    if (qb + kRing - 1 < nqb) issue((qb + kRing - 1) % kRing, qb + kRing - 1);
+    const uint8_t* Qs = smem + (qb % kRing) * STAGE;
+    const uint8_t* Os = Qs + kTile;
+    const float* lse_s = reinterpret_cast<const float*>(Qs + 2 * kTile);
+    const float* del_s = lse_s + AB;
+    const int q0 = qb * AB;
+    f32x4 p[NK][4], ds[NK][4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x4 sv[NK], dp[NK];
+#pragma unroll
+      for (int n = 0; n < NK; ++n) {
+        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const bf16x8 qa = frag_row(Qs, qt * 16, kh), oa = frag_row(Os, qt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          sv[n] = mfma(qa, kf[n][kh], sv[n]);
+          dp[n] = mfma(oa, vf[n][kh], dp[n]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NK; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qt * 16 + 4 * g + r;
+          const bool ok = key[n] < len && q0 + ql < S;
+          const float pv = ok ? exp2f(sv[n][r] * sl2 - lse_s[ql]) : 0.f;
+          p[n][qt][r] = pv;
+          ds[n][qt][r] = pv * (dp[n][r] - del_s[ql]);
+        }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pb[NK], sb[NK];
+#pragma unroll
+      for (int n = 0; n < NK; ++n) {
+        pb[n] = pack_acc(p[n][2 * ks], p[n][2 * ks + 1]);
+        sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
+      }
+      bf16x8 tf[8];  // dO^T (d = 0..3), Q^T (d = 0..3)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        tf[d] = frag_tr_asm(Os, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+        tf[4 + d] = frag_tr_asm(Qs, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+      }
+      frag_tr_wait(tf);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          dv[n][d] = mfma(tf[d], pb[n], dv[n][d]);
+          dk[n][d] = mfma(tf[4 + d], sb[n], dk[n][d]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NK; ++n) {
+    if (key[n] < S) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint16_t* kp = dqkv + (base + key[n]) * ld + D + h * AH + d * 16 + 4 * g;
+        uint16_t* vp = dqkv + (base + key[n]) * ld + 2 * D + h * AH + d * 16 + 4 * g;
+        ushort4 uk, uv;
+        uk.x = f32_to_bf16(dk[n][d][0] * scale);
+        uk.y = f32_to_bf16(dk[n][d][1] * scale);
+        uk.z = f32_to_bf16(dk[n][d][2] * scale);
+        uk.w = f32_to_bf16(dk[n][d][3] * scale);
+        uv.x = f32_to_bf16(dv[n][d][0]);
+        uv.y = f32_to_bf16(dv[n][d][1]);
+        uv.z = f32_to_bf16(dv[n][d][2]);
+        uv.w = f32_to_bf16(dv[n][d][3]);
+        *reinterpret_cast<ushort4*>(kp) = uk;
+        *reinterpret_cast<ushort4*>(vp) = uv;
+      }
+    }
+  }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* __restrict__ qkv,
+                                                               const uint16_t* __restrict__ dout,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta,
+                                                               const int* __restrict__ lens,
+                                                               uint16_t* __restrict__ dqkv, int S, int H, float scale) {
+  constexpr int STAGE = 2 * kTile;  // K tile, V tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
+  int qb, h, b;
+  block_coords(S, 64 * NQ, H, qb, h, b);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  (void)lane;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int nkb = (len + AB - 1) / AB;
+  auto issue = [&](int slot, int kb) {
+    uint8_t* st = smem + slot * STAGE;
+    const int k0 = kb * AB, nv = min(AB, S - k0);
+    glds_tile(st, qkv, ld, base + k0, nv, D + h * AH);
+    glds_tile(st + kTile, qkv, ld, base + k0, nv, 2 * D + h * AH);
+  };
+  int q[NQ];
+  bf16x8 qf[NQ][2], of[NQ][2];
+  float lq[NQ], dl[NQ];
+  f32x4 acc[NQ][4];
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
+                           : bf16x8{};
+      of[n][kh] = q[n] < S
+                      ? *reinterpret_cast<const bf16x8*>(dout + (base + q[n]) * (int64_t)D + h * AH + kh * 32 + 8 * g)
+                      : bf16x8{};
+    }
+    lq[n] = q[n] < S ? lse[((int64_t)b * H + h) * S + q[n]] : 0.f;
+    dl[n] = q[n] < S ? delta[(base + q[n]) * H + h] : 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s0 = 0; s0 < kRing - 1; ++s0)
+    if (s0 < nkb) issue(s0, s0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    ring_wait4(min(kRing - 2, nkb - 1 - kb));
+    raw_barrier();
+    if (kb + kRing - 1 < nkb) issue((kb + kRing - 1) % kRing, kb + kRing - 1);
+    const uint8_t* Ks = smem + (kb % kRing) * STAGE;
+    const uint8_t* Vs = Ks + kTile;
+    f32x4 ds[NQ][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 sv[NQ], dp[NQ];
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const bf16x8 ka = frag_row(Ks, kt * 16, kh), va = frag_row(Vs, kt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          sv[n] = mfma(ka, qf[n][kh], sv[n]);
+          dp[n] = mfma(va, of[n][kh], dp[n]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * AB + kt * 16 + 4 * g + r;
+          const float pv = key < len ? exp2f(sv[n][r] * sl2 - lq[n]) : 0.f;
+          ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+        }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 sb[NQ];
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
+      bf16x8 tf[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) tf[d] = frag_tr_asm(Ks, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+      frag_tr_wait(tf);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[n][d] = mfma(tf[d], sb[n], acc[n][d]);
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    if (q[n] < S) {
+      uint16_t* qp = dqkv + (base + q[n]) * ld + h * AH;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        ushort4 u;
+        u.x = f32_to_bf16(acc[n][d][0] * scale);
+        u.y = f32_to_bf16(acc[n][d][1] * scale);
+        u.z = f32_to_bf16(acc[n][d][2] * scale);
+        u.w = f32_to_bf16(acc[n][d][3] * scale);
+        *reinterpret_cast<ushort4*>(qp + d * 16 + 4 * g) = u;
+      }
+    }
+  }
+}
+
 // 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
 // MLT_ATTN_FWD_GROUPS / MLT_ATTN_DKDV_GROUPS / MLT_ATTN_DQ_GROUPS = 1|2 override the choice
 // Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dK/dV 1 group (2 groups need
@@ -571,6 +915,22 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
                      (int64_t)B * S, H);
   const dim3 g2((S + 127) / 128 * H * B), g1((S + 63) / 64 * H * B);
+  const char* rv = getenv("MLT_ATTN_RING");
+  if (!(rv && rv[0] == '0')) {
+    if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
+      hipLaunchKernelGGL(attn_bwd_dkdv_ring_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
+                         scale);
+    else
+      hipLaunchKernelGGL(attn_bwd_dkdv_ring_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
+                         scale);
+    if (attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2)
+      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
+                         scale);
+    else
+      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
+                         scale);
+    return;
+  }
   if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
   else
