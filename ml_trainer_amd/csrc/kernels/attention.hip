@@ -38,6 +38,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int AH = 64;  // head dim
 constexpr int AB = 64;  // query / key block
 
+// raw v_exp_f32 (2^x): exp2f wraps it in a denormal-range fix-up (compare, select, two
+// ldexp) that the probabilities here never need; exp2(-inf) = 0 doubles as the mask
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -194,13 +198,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
       const float mn = fmaxf(m[n], bm);
-      const float alpha = exp2f(m[n] - mn);  // m = -inf on the first block -> 0
+      const float alpha = fast_exp2(m[n] - mn);  // m = -inf on the first block -> 0
       float ps = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[n][kt][r] - mn);
+          const float p = fast_exp2(s[n][kt][r] - mn);
           s[n][kt][r] = p;
           ps += p;
         }
@@ -366,15 +370,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
           dp[n] = mfma(oa, vf[n][kh], dp[n]);
         }
       }
+      const float4 l4 = *reinterpret_cast<const float4*>(&lse_s[cur][qt * 16 + 4 * g]);
+      const float4 d4 = *reinterpret_cast<const float4*>(&del_s[cur][qt * 16 + 4 * g]);
+      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
       for (int n = 0; n < NK; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = qt * 16 + 4 * g + r;
           const bool ok = key[n] < len && q0 + ql < S;
-          const float pv = ok ? exp2f(sv[n][r] * sl2 - lse_s[cur][ql]) : 0.f;
+          const float pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
           p[n][qt][r] = pv;
-          ds[n][qt][r] = pv * (dp[n][r] - del_s[cur][ql]);
+          ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
         }
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS  (k = queries, two 32-query steps)
@@ -505,7 +512,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb * AB + kt * 16 + 4 * g + r;
-          const float pv = key < len ? exp2f(sv[n][r] * sl2 - lq[n]) : 0.f;
+          const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
           ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
         }
     }
@@ -555,7 +562,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
 // barriers"); all LDS lives in ONE __shared__ array (the second-object trap, §5 item 4a).
 // The math and its order are those of the kernels above: bit-identical gradients.
 // ---------------------------------------------------------------------------
-constexpr int kRing = 4;
 constexpr int kTile = AB * 128;  // one 64 x 64 bf16 tile
 
 // glds of a 64x64 bf16 tile into the (row & 7)-swizzled image tile_off() reads: lane-linear
@@ -621,7 +627,7 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int NK>
+template <int NK, int kRing>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                  const uint16_t* __restrict__ dout,
                                                                  const float* __restrict__ lse,
@@ -675,6 +681,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
                       : bf16x8{};
     }
   }
+  float sl2k[NK], kinf[NK];  // masked keys: scale 0 and +inf shift -> exp2(-inf) = 0
+#pragma unroll
+  for (int n = 0; n < NK; ++n) {
+    sl2k[n] = key[n] < len ? sl2 : 0.f;
+    kinf[n] = key[n] < len ? 0.f : INFINITY;
+  }
   // the ring prologue goes out after the register loads above, so waiting for those is a
   // counted vmcnt that leaves the DMAs in flight
 #pragma unroll
@@ -697,6 +709,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
     const float* lse_s = reinterpret_cast<const float*>(Qs + 2 * kTile);
     const float* del_s = lse_s + AB;
     const int q0 = qb * AB;
+    const bool qfull = q0 + AB <= S;
     f32x4 p[NK][4], ds[NK][4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -715,16 +728,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
           dp[n] = mfma(oa, vf[n][kh], dp[n]);
         }
       }
+      const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
+      const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
+      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+      if (qfull) {  // key mask folded into per-lane constants: x = s * sl2k - (lse + kinf)
 #pragma unroll
-      for (int n = 0; n < NK; ++n)
+        for (int n = 0; n < NK; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = qt * 16 + 4 * g + r;
-          const bool ok = key[n] < len && q0 + ql < S;
-          const float pv = ok ? exp2f(sv[n][r] * sl2 - lse_s[ql]) : 0.f;
-          p[n][qt][r] = pv;
-          ds[n][qt][r] = pv * (dp[n][r] - del_s[ql]);
-        }
+          for (int r = 0; r < 4; ++r) {
+            const float pv = fast_exp2(sv[n][r] * sl2k[n] - (lr[r] + kinf[n]));
+            p[n][qt][r] = pv;
+            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
+          }
+      } else {
+#pragma unroll
+        for (int n = 0; n < NK; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = qt * 16 + 4 * g + r;
+            const bool ok = key[n] < len && q0 + ql < S;
+            const float pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
+            p[n][qt][r] = pv;
+            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
+          }
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -774,7 +801,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
   }
 }
 
-template <int NQ>
+template <int NQ, int kRing>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                const uint16_t* __restrict__ dout,
                                                                const float* __restrict__ lse,
@@ -851,7 +878,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb * AB + kt * 16 + 4 * g + r;
-          const float pv = key < len ? exp2f(sv[n][r] * sl2 - lq[n]) : 0.f;
+          const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
           ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
         }
     }
@@ -915,20 +942,31 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
                      (int64_t)B * S, H);
   const dim3 g2((S + 127) / 128 * H * B), g1((S + 63) / 64 * H * B);
+  // MLT_ATTN_RING: 0 = register-staged kernels, 3 / 4 = ring depth (default 4)
   const char* rv = getenv("MLT_ATTN_RING");
-  if (!(rv && rv[0] == '0')) {
-    if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
-      hipLaunchKernelGGL(attn_bwd_dkdv_ring_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
-                         scale);
+  const int ring = rv ? atoi(rv) : 4;
+  if (ring == 3 || ring == 4) {
+    const bool k2 = attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2, q2 = attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2;
+#define MLT_RING_LAUNCH(RD)                                                                                         \
+  {                                                                                                                 \
+    if (k2)                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
+                         dqkv, S, H, scale);                                                                        \
+    else                                                                                                            \
+      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
+                         dqkv, S, H, scale);                                                                        \
+    if (q2)                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
+                         S, H, scale);                                                                              \
+    else                                                                                                            \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
+                         S, H, scale);                                                                              \
+  }
+    if (ring == 3)
+      MLT_RING_LAUNCH(3)
     else
-      hipLaunchKernelGGL(attn_bwd_dkdv_ring_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
-                         scale);
-    if (attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2)
-      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
-                         scale);
-    else
-      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H,
-                         scale);
+      MLT_RING_LAUNCH(4)
+#undef MLT_RING_LAUNCH
     return;
   }
   if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)

@@ -326,8 +326,8 @@ def test_attention_bwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
     lse = torch.empty(B * H * S, device=dev)
     C.attn_fwd(qkv, out, lse, lens, B, S, H, scale)
     dout = _bf((B * S, D), g)
-    res = []
-    for ring in ("0", "1"):
+    res = {}
+    for ring in ("0", "3", "4"):
         monkeypatch.setenv("MLT_ATTN_RING", ring)
         for grp in ("1", "2"):
             monkeypatch.setenv("MLT_ATTN_DKDV_GROUPS", grp)
@@ -335,5 +335,6 @@ def test_attention_bwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
             dqkv = torch.full_like(qkv, float("nan"))
             delta = torch.empty(B * S * H, device=dev)
             C.attn_bwd(qkv, out, dout, lse, delta, lens, dqkv, B, S, H, scale)
-            res.append(dqkv)
-    assert torch.equal(res[0], res[2]) and torch.equal(res[1], res[3])
+            res[ring, grp] = dqkv
+    for grp in ("1", "2"):
+        assert torch.equal(res["0", grp], res["3", grp]) and torch.equal(res["0", grp], res["4", grp])
