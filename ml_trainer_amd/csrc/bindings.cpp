@@ -499,26 +499,27 @@ void embed_fwd(Tensor ids, c10::optional<Tensor> tt, Tensor Ww, Tensor Wp, Tenso
                    rows, (int)S, (int)D, Ww.size(0), (int)Wt.size(0), cur_stream());
 }
 
-void embed_bwd(Tensor ids, c10::optional<Tensor> tt, Tensor DX, Tensor gw, Tensor gp, Tensor gt, Tensor part,
-               int64_t S) {
-  const int64_t rows = ids.numel(), D = gw.size(1);
+void embed_bwd(Tensor sid, Tensor perm, c10::optional<Tensor> tt, Tensor DX, Tensor gw, Tensor gp, Tensor gt,
+               Tensor part, int64_t S) {
+  const int64_t rows = sid.numel(), D = gw.size(1);
   TORCH_CHECK(D % 256 == 0 && D <= 1024, "embedding width");
   TORCH_CHECK(S > 0 && rows % S == 0 && S <= gp.size(0), "sequence length vs position table");
-  check_dev(ids, "ids", at::kLong, rows, 8);
+  check_dev(sid, "sorted ids", at::kLong, rows, 8);
+  check_dev(perm, "perm", at::kLong, rows, 8);
   const int64_t* tp = nullptr;
   if (tt.has_value()) {
     check_dev(*tt, "token_type", at::kLong, rows, 8);
     tp = tt->data_ptr<int64_t>();
   }
   check_bf16_2d(DX, "DX", rows, D);
-  check_dev(gw, "gw", at::kFloat, gw.size(0) * D);
-  check_dev(gp, "gp", at::kFloat, gp.size(0) * D);
+  check_dev(gw, "gw", at::kFloat, gw.size(0) * D, 16);
+  check_dev(gp, "gp", at::kFloat, gp.size(0) * D, 16);
   check_dev(gt, "gt", at::kFloat, gt.size(0) * D);
   TORCH_CHECK(gt.size(0) <= 2, "at most 2 token types");
-  check_dev(part, "part", at::kFloat, (int64_t)ln_bwd_partial_blocks(rows) * 2 * D);
-  launch_embed_bwd(ids.data_ptr<int64_t>(), tp, bf16_ptr(DX), gw.data_ptr<float>(), gp.data_ptr<float>(),
-                   gt.data_ptr<float>(), part.data_ptr<float>(), rows, (int)S, (int)D, gw.size(0), (int)gt.size(0),
-                   cur_stream());
+  check_dev(part, "part", at::kFloat, S * 2 * D, 16);
+  launch_embed_bwd(sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), tp, bf16_ptr(DX), gw.data_ptr<float>(),
+                   gp.data_ptr<float>(), gt.data_ptr<float>(), part.data_ptr<float>(), rows, (int)S, (int)D,
+                   gw.size(0), (int)gt.size(0), cur_stream());
 }
 
 static const int* lens_ptr(const c10::optional<Tensor>& lens, int64_t B) {

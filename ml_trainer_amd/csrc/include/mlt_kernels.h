@@ -168,8 +168,11 @@ void launch_ln_bwd(const uint16_t* DY, const uint16_t* X, const float* gamma, co
 void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww, const uint16_t* Wp,
                       const uint16_t* Wt, uint16_t* out, int64_t rows, int S, int D, int64_t vocab, int ntype,
                       hipStream_t st);
-void launch_embed_bwd(const int64_t* ids, const int64_t* tt, const uint16_t* DX, float* gw, float* gp, float* gt,
-                      float* part, int64_t rows, int S, int D, int64_t vocab, int ntype, hipStream_t st);
+// sid / perm: the token ids sorted stably and the sorting permutation (deterministic, atomic-free
+// word-table scatter); part: S x 2D floats of per-position token-type partial sums
+void launch_embed_bwd(const int64_t* sid, const int64_t* perm, const int64_t* tt, const uint16_t* DX, float* gw,
+                      float* gp, float* gt, float* part, int64_t rows, int S, int D, int64_t vocab, int ntype,
+                      hipStream_t st);
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* lens, int B, int S, int H,
                      float scale, hipStream_t st);
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,

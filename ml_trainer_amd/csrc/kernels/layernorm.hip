@@ -267,49 +267,82 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 
 // word / position grads: fp32 atomics (the vocabulary rows hit are sparse and spread);
 // token-type grads: per-block partials over the (few) type rows, reduced in fixed order.
+// Embedding backward without atomics (bitwise reproducible):
+//  * word rows: the token ids arrive sorted (stable, host-side torch.sort) with the permutation;
+//    one wave per sorted entry, and the wave that starts a run of equal ids sums that run's
+//    gradient rows in token order and adds the sum to its table row (one writer per row);
+//  * positions / token types: one wave per position sums the B rows of that position in batch
+//    order into gp, and leaves the per-type sums as a partial row for reduce_rows.
 template <int VPL>
-__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
-                                                        const uint16_t* __restrict__ DX, float* __restrict__ gw,
-                                                        float* __restrict__ gp, float* __restrict__ part_t,
-                                                        int64_t rows, int S, int64_t vocab, int ntype) {
+__global__ __launch_bounds__(256) void embed_bwd_word_kernel(const int64_t* __restrict__ sid,
+                                                             const int64_t* __restrict__ perm,
+                                                             const uint16_t* __restrict__ DX, float* __restrict__ gw,
+                                                             int64_t rows, int64_t vocab) {
   constexpr int D = VPL * 256, E = VPL * 4;
-  __shared__ float red[4][2 * D];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float t0[E], t1[E];
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows) return;
+  const int64_t id = sid[i];
+  if (i > 0 && sid[i - 1] == id) return;  // not the start of a run
+  float acc[E];
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    t0[i] = 0.f;
-    t1[i] = 0.f;
-  }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  for (int64_t j = i; j < rows && sid[j] == id; ++j) {
     float d[E];
-    load_row<VPL>(DX + row * D, d);
-    int64_t id = ids[row];
-    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-    const int pos = (int)(row % S);
-    const int64_t ty = tt ? tt[row] : 0;
+    load_row<VPL>(DX + perm[j] * D, d);
 #pragma unroll
-    for (int v = 0; v < VPL; ++v)
+    for (int e = 0; e < E; ++e) acc[e] += d[e];
+  }
+  const int64_t row = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * (lane + 64 * v) + q;
-        atomicAdd(gw + id * D + c, d[4 * v + q]);
-        atomicAdd(gp + (int64_t)pos * D + c, d[4 * v + q]);
-        if (ty == 0) t0[4 * v + q] += d[4 * v + q];
-        else t1[4 * v + q] += d[4 * v + q];
-      }
+  for (int v = 0; v < VPL; ++v) {
+    float4* g = reinterpret_cast<float4*>(gw + row * D + 4 * (lane + 64 * v));
+    float4 o = *g;
+    o.x += acc[4 * v];
+    o.y += acc[4 * v + 1];
+    o.z += acc[4 * v + 2];
+    o.w += acc[4 * v + 3];
+    *g = o;
+  }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const int64_t* __restrict__ tt,
+                                                            const uint16_t* __restrict__ DX, float* __restrict__ gp,
+                                                            float* __restrict__ part_t, int64_t rows, int S) {
+  constexpr int D = VPL * 256, E = VPL * 4;
+  const int lane = threadIdx.x & 63;
+  const int pos = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= S) return;
+  float a[E], t0[E], t1[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) a[e] = t0[e] = t1[e] = 0.f;
+  for (int64_t r = pos; r < rows; r += S) {
+    float d[E];
+    load_row<VPL>(DX + r * D, d);
+    const bool one = tt && tt[r] != 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      a[e] += d[e];
+      t0[e] += one ? 0.f : d[e];
+      t1[e] += one ? d[e] : 0.f;
+    }
   }
 #pragma unroll
-  for (int v = 0; v < VPL; ++v)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = 4 * (lane + 64 * v) + q;
-      red[wid][c] = t0[4 * v + q];
-      red[wid][D + c] = t1[4 * v + q];
-    }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += 256)
-    part_t[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  for (int v = 0; v < VPL; ++v) {
+    const int c = 4 * (lane + 64 * v);
+    float4* g = reinterpret_cast<float4*>(gp + (int64_t)pos * D + c);
+    float4 o = *g;
+    o.x += a[4 * v];
+    o.y += a[4 * v + 1];
+    o.z += a[4 * v + 2];
+    o.w += a[4 * v + 3];
+    *g = o;
+    *reinterpret_cast<float4*>(part_t + (int64_t)pos * 2 * D + c) =
+        make_float4(t0[4 * v], t0[4 * v + 1], t0[4 * v + 2], t0[4 * v + 3]);
+    *reinterpret_cast<float4*>(part_t + (int64_t)pos * 2 * D + D + c) =
+        make_float4(t1[4 * v], t1[4 * v + 1], t1[4 * v + 2], t1[4 * v + 3]);
+  }
 }
 
 void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww, const uint16_t* Wp,
@@ -326,21 +359,25 @@ void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww,
   }
 }
 
-void launch_embed_bwd(const int64_t* ids, const int64_t* tt, const uint16_t* DX, float* gw, float* gp, float* gt,
-                      float* part, int64_t rows, int S, int D, int64_t vocab, int ntype, hipStream_t st) {
+void launch_embed_bwd(const int64_t* sid, const int64_t* perm, const int64_t* tt, const uint16_t* DX, float* gw,
+                      float* gp, float* gt, float* part, int64_t rows, int S, int D, int64_t vocab, int ntype,
+                      hipStream_t st) {
   if (rows <= 0) return;
-  const int nb = ln_bwd_partial_blocks(rows);
-  const dim3 grid(nb), block(256);
+  const dim3 gw_grid((unsigned)((rows + 3) / 4)), gp_grid((unsigned)((S + 3) / 4)), block(256);
+#define MLT_EMB_BWD(V)                                                                                          \
+  hipLaunchKernelGGL(embed_bwd_word_kernel<V>, gw_grid, block, 0, st, sid, perm, DX, gw, rows, vocab);         \
+  hipLaunchKernelGGL(embed_bwd_pos_kernel<V>, gp_grid, block, 0, st, tt, DX, gp, part, rows, S);
   switch (D / 256) {
-    case 3: hipLaunchKernelGGL(embed_bwd_kernel<3>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
-    case 4: hipLaunchKernelGGL(embed_bwd_kernel<4>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
-    case 1: hipLaunchKernelGGL(embed_bwd_kernel<1>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
-    case 2: hipLaunchKernelGGL(embed_bwd_kernel<2>, grid, block, 0, st, ids, tt, DX, gw, gp, part, rows, S, vocab, ntype); break;
+    case 1: MLT_EMB_BWD(1) break;
+    case 2: MLT_EMB_BWD(2) break;
+    case 3: MLT_EMB_BWD(3) break;
+    case 4: MLT_EMB_BWD(4) break;
     default: return;
   }
-  // type rows 0 and 1 (ntype <= 2): accumulate the partials into gt[0:D] and gt[D:2D]
+#undef MLT_EMB_BWD
+  // token types 0 and 1 (ntype <= 2): the S partial rows summed in position order into gt
   SegOut o{{gt, gt + D, nullptr}};
-  launch_reduce_rows(part, nb, 2 * D, ntype >= 2 ? 2 * D : D, D, o, ntype >= 2 ? 3 : 1, st);
+  launch_reduce_rows(part, S, 2 * D, ntype >= 2 ? 2 * D : D, D, o, ntype >= 2 ? 3 : 1, st);
 }
 
 }  // namespace mlt

@@ -353,8 +353,11 @@ class _Embeddings(torch.autograd.Function):
             gt = torch.zeros(st, dtype=torch.float32, device=dout.device)
             ret = (gw, gp, gt)
         D = sw[1]
-        part = torch.empty(C.ln_partial_blocks(ids.numel()) * 2 * D, dtype=torch.float32, device=dout.device)
-        C.embed_bwd(ids, ttf if has_tt else None, dout, gw, gp, gt, part, S)
+        # stable sort of the ids: the word-table scatter then has one writer per row, summing its
+        # tokens in order (no atomics, bitwise reproducible)
+        sid, perm = torch.sort(ids.view(-1).clamp(0, sw[0] - 1), stable=True)
+        part = torch.empty(S * 2 * D, dtype=torch.float32, device=dout.device)
+        C.embed_bwd(sid, perm, ttf if has_tt else None, dout, gw, gp, gt, part, S)
         G.done()
         return (None, None) + ret + (None,)
 
