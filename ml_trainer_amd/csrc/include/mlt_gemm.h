@@ -18,11 +18,25 @@ struct GemmEpi {
   const float* inv_scale_b = nullptr;
 };
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf(z) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 output's ulp):
+// one v_rcp, one v_exp, five FMAs instead of the library erff; `ez2` returns e^{-z^2}, which
+// the GELU derivative reuses as its Gaussian density term.
+__device__ __forceinline__ float erf_fast(float z, float& ez2) {
+  const float a = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  ez2 = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
+  return copysignf(fmaf(-poly, ez2, 1.f), z);
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  float e;
+  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f, e));
+}
 __device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;  // e = exp(-x^2 / 2)
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, e));
+  return fmaf(x, 0.3989422804014327f * e, cdf);
 }
 
 // Apply the epilogue to 4 consecutive columns gn..gn+3 of row gm (values already scaled by
