@@ -373,7 +373,9 @@ void fp8_amax(Tensor x, Tensor amax) {
 }
 
 void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::optional<Tensor> amax, int fmt) {
-  TORCH_CHECK(w.dim() == 2 && w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat, "w: fp32 [R,C]");
+  TORCH_CHECK(w.dim() == 2 && w.is_cuda() && w.is_contiguous() &&
+                  (w.scalar_type() == at::kFloat || w.scalar_type() == at::kBFloat16),
+              "w: fp32 or bf16 [R,C]");
   const int64_t R = w.size(0), Cc = w.size(1);
   TORCH_CHECK(R % 4 == 0 && Cc % 4 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w shape/alignment");
   TORCH_CHECK(y.is_cuda() && y.is_contiguous() && is_fp8_storage(y) && y.numel() == R * Cc, "y");
@@ -384,9 +386,15 @@ void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::option
     check_dev(*amax, "amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
     am = amax->data_ptr<float>();
   }
-  launch_cast_transpose_fp8(w.data_ptr<float>(), reinterpret_cast<uint8_t*>(y.data_ptr()),
-                            reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(), am,
-                            fmt, cur_stream());
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fmt: 0 = e4m3, 1 = e5m2");
+  if (w.scalar_type() == at::kFloat)
+    launch_cast_transpose_fp8(w.data_ptr<float>(), reinterpret_cast<uint8_t*>(y.data_ptr()),
+                              reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(), am,
+                              fmt, cur_stream());
+  else
+    launch_cast_transpose_fp8_bf16(bf16_ptr(w), reinterpret_cast<uint8_t*>(y.data_ptr()),
+                                   reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(),
+                                   am, fmt, cur_stream());
 }
 
 // hist [n, H], amax [n, kAmaxSlots], scale / inv_scale / fmax [n]

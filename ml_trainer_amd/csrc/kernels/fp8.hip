@@ -106,8 +106,17 @@ __global__ __launch_bounds__(256) void amax_kernel(const InT* __restrict__ x, in
 }
 
 // fp32 W [R][C] -> fp8 W [R][C] and W^T [C][R]; 64x64 tile per block, R % 4 == 0, C % 4 == 0
-template <int FMT>
-__global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const float* __restrict__ w, uint8_t* __restrict__ y,
+__device__ __forceinline__ float4 load4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 load4f(const uint16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+// InT = float (master weights) or uint16_t (bf16 activations / gradients: the fp8 weight
+// gradient needs X^T and dY^T with the token dimension contiguous)
+template <int FMT, typename InT>
+__global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const InT* __restrict__ w, uint8_t* __restrict__ y,
                                                                  uint8_t* __restrict__ yt, int R, int C,
                                                                  const float* __restrict__ scale,
                                                                  float* __restrict__ amax) {
@@ -123,7 +132,7 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const float* __
     const int gr = r0 + r, gc = c0 + c4;
     uint32_t packed = 0;
     if (gr < R && gc < C) {
-      const float4 v = *reinterpret_cast<const float4*>(w + (int64_t)gr * C + gc);
+      const float4 v = load4f(w + (int64_t)gr * C + gc);
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       packed = pack4_fp8<FMT>(v.x * s, v.y * s, v.z * s, v.w * s);
       *reinterpret_cast<uint32_t*>(y + (int64_t)gr * C + gc) = packed;
@@ -205,8 +214,18 @@ void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, i
                                int fmt, hipStream_t st) {
   if (R <= 0 || C <= 0) return;
   const dim3 g((C + 63) / 64, (R + 63) / 64), b(256);
-  if (fmt == 0) hipLaunchKernelGGL(cast_transpose_fp8_kernel<0>, g, b, 0, st, w, y, yt, R, C, scale, amax);
-  else hipLaunchKernelGGL(cast_transpose_fp8_kernel<1>, g, b, 0, st, w, y, yt, R, C, scale, amax);
+  if (fmt == 0) hipLaunchKernelGGL((cast_transpose_fp8_kernel<0, float>), g, b, 0, st, w, y, yt, R, C, scale, amax);
+  else hipLaunchKernelGGL((cast_transpose_fp8_kernel<1, float>), g, b, 0, st, w, y, yt, R, C, scale, amax);
+}
+
+void launch_cast_transpose_fp8_bf16(const uint16_t* x, uint8_t* y, uint8_t* yt, int R, int C, const float* scale,
+                                    float* amax, int fmt, hipStream_t st) {
+  if (R <= 0 || C <= 0) return;
+  const dim3 g((C + 63) / 64, (R + 63) / 64), b(256);
+  if (fmt == 0)
+    hipLaunchKernelGGL((cast_transpose_fp8_kernel<0, uint16_t>), g, b, 0, st, x, y, yt, R, C, scale, amax);
+  else
+    hipLaunchKernelGGL((cast_transpose_fp8_kernel<1, uint16_t>), g, b, 0, st, x, y, yt, R, C, scale, amax);
 }
 
 void launch_fp8_update_scale(float* hist, int H, int n, float* amax, float* scale, float* inv_scale, const float* fmax,

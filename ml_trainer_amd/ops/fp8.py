@@ -79,6 +79,15 @@ class Fp8Context:
         require_native().fp8_cast(x, y, self.scale[i:i + 1], self.amax[i], fmt)
         return y
 
+    def cast_t(self, x: torch.Tensor, i: int, fmt: int):
+        """fp8 copy of a bf16 [R, C] tensor plus its transpose [C, R] in one pass (same scale)."""
+        if not self._ready[i]:
+            self._init_exact(i, x)
+        y = torch.empty(x.shape, dtype=_DT[fmt], device=x.device)
+        yt = torch.empty(x.shape[1], x.shape[0], dtype=_DT[fmt], device=x.device)
+        require_native().fp8_cast_transpose(x, y, yt, self.scale[i:i + 1], self.amax[i], fmt)
+        return y, yt
+
     def inv(self, i: int) -> torch.Tensor:
         return self.inv_scale[i:i + 1]
 
@@ -94,7 +103,7 @@ def context(device: torch.device) -> Fp8Context:
 
 
 class _WeightState:
-    __slots__ = ("mx", "mw", "mdy", "w8", "w8t", "key")
+    __slots__ = ("mx", "mw", "mdy", "w8", "w8t", "key", "xt", "dy8")
 
     def __init__(self, ctx: Fp8Context):
         self.mx = ctx.new_meta(E4M3)
@@ -103,6 +112,8 @@ class _WeightState:
         self.w8: Optional[torch.Tensor] = None
         self.w8t: Optional[torch.Tensor] = None
         self.key = None
+        self.xt = None   # (x.data_ptr(), X^T in e4m3) of the last forward, for the fp8 weight gradient
+        self.dy8 = None  # (dy.data_ptr(), dY in e5m2) cast by wgrad, reused by the dgrad that follows
 
 
 def _state(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
@@ -135,26 +146,60 @@ def weight_fp8(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
     return st
 
 
+def _fp8_wgrad_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    # the MX-scaled MFMA GEMM needs K (= tokens) % 128 and both output dims >= 64
+    return x.shape[0] % 128 == 0 and x.shape[1] >= 64 and w.shape[0] >= 64 and x.shape[1] % 4 == 0
+
+
 class Fp8Linear:
-    """Linear arithmetic for ops.transformer blocks: fp8 forward / dgrad, bf16 wgrad."""
+    """Linear arithmetic for ops.transformer blocks, all three GEMMs in fp8 (delayed scaling):
+    forward X(e4m3) . W^T(e4m3), dgrad dY(e5m2) . W(e4m3), wgrad dY^T(e5m2) . X^T(e4m3) -- the
+    activations are cast together with their transposes so every operand is k-contiguous."""
 
     @staticmethod
     def fwd(x, w, bias=None, gelu_aux=None, res=None):
         C = require_native()
         ctx = context(x.device)
         st = weight_fp8(w, ctx)
-        x8 = ctx.cast(x, st.mx, E4M3)
+        if torch.is_grad_enabled() and _fp8_wgrad_ok(x, w):
+            x8, x8t = ctx.cast_t(x, st.mx, E4M3)
+            st.xt = (x.data_ptr(), x8t)
+        else:
+            x8 = ctx.cast(x, st.mx, E4M3)
+            st.xt = None
         y = torch.empty(x.shape[0], w.shape[0], dtype=torch.bfloat16, device=x.device)
         C.gemm_f8(x8, st.w8, y, E4M3, E4M3, ctx.inv(st.mx), ctx.inv(st.mw), bias=bias, aux=gelu_aux, res=res,
                   mode=1 if gelu_aux is not None else 0)
         return y
 
     @staticmethod
+    def wgrad(w, dy, x, out: Optional[torch.Tensor]):
+        """dW = dY^T X in fp8 into ``out`` (accumulate) or a new fp32 tensor; None when the forward
+        left no transposed input for this weight (the caller then uses the bf16 GEMM)."""
+        st = getattr(w, "_mlt_f8", None)
+        if st is None or st.xt is None or st.xt[0] != x.data_ptr() or not _fp8_wgrad_ok(x, w):
+            return None
+        C = require_native()
+        ctx = context(dy.device)
+        dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2)
+        st.dy8 = (dy.data_ptr(), dy8)
+        acc = out is not None
+        if out is None:
+            out = torch.empty(w.shape[0], w.shape[1], dtype=torch.float32, device=dy.device)
+        C.gemm_f8(dy8t, st.xt[1], out, E5M2, E4M3, ctx.inv(st.mdy), ctx.inv(st.mx), accumulate=acc)
+        st.xt = None
+        return out
+
+    @staticmethod
     def dgrad(dy, w, out, aux=None, res=None):
         C = require_native()
         ctx = context(dy.device)
         st = weight_fp8(w, ctx)
-        dy8 = ctx.cast(dy, st.mdy, E5M2)
+        if st.dy8 is not None and st.dy8[0] == dy.data_ptr():
+            dy8 = st.dy8[1]
+        else:
+            dy8 = ctx.cast(dy, st.mdy, E5M2)
+        st.dy8 = None
         C.gemm_f8(dy8, st.w8t, out, E5M2, E4M3, ctx.inv(st.mdy), ctx.inv(st.mw), aux=aux,
                   mode=2 if aux is not None else 0, res=res)
         return out

@@ -109,8 +109,12 @@ class _Grads:
             self.ready.append(p)
         return g
 
-    def wgrad(self, p, dy, x):
+    def wgrad(self, p, dy, x, impl=None):
         g = self.sink(p)
+        if impl is not None and hasattr(impl, "wgrad"):  # fp8 weight gradient
+            r = impl.wgrad(p, dy, x, g)
+            if r is not None:
+                return None if g is not None else r
         if g is None:
             return linear_wgrad(dy, x)
         require_native().gemm(dy, x, g, True, True, accumulate=True)
@@ -145,14 +149,14 @@ def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
     C = require_native()
     x, qkv, attn, lse = saved
     wqkv, bqkv, wo, bo = params
-    dwo = G.wgrad(wo, dy, attn)
+    dwo = G.wgrad(wo, dy, attn, impl)
     if isinstance(dbo, str):
         dbo = G.colsum(bo, dy)
     dattn = impl.dgrad(dy, wo, torch.empty_like(attn))
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
     C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
-    dwqkv = G.wgrad(wqkv, dqkv, x)
+    dwqkv = G.wgrad(wqkv, dqkv, x, impl)
     dbqkv = G.colsum(bqkv, dqkv)
     dx = impl.dgrad(dqkv, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
     return dx, dwqkv, dbqkv, dwo, dbo
@@ -168,11 +172,11 @@ def _ffn_fwd(x, w1, b1, w2, b2, impl=BF16):
 def _ffn_bwd(saved, params, dy, G, db2="colsum", impl=BF16):
     x, pre, a = saved
     w1, b1, w2, b2 = params
-    dw2 = G.wgrad(w2, dy, a)
+    dw2 = G.wgrad(w2, dy, a, impl)
     if isinstance(db2, str):
         db2 = G.colsum(b2, dy)
     dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
-    dw1 = G.wgrad(w1, dpre, x)
+    dw1 = G.wgrad(w1, dpre, x, impl)
     db1 = G.colsum(b1, dpre)
     dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)
     return dx, dw1, db1, dw2, db2

@@ -138,3 +138,54 @@ def test_fp8_bert_trains(dev):
     from ml_trainer_amd.ops.fp8 import context
     ctx = context(ids.device)
     assert ctx.n > 0 and torch.isfinite(ctx.scale[:ctx.n]).all() and (ctx.scale[:ctx.n] > 0).all()
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_cast_transpose_bf16_input(dev, fmt):
+    C = require_native()
+    g = torch.Generator().manual_seed(5 + fmt)
+    x = torch.randn(256, 192, generator=g).to(dev).to(torch.bfloat16)
+    dt = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
+    y = torch.empty(256, 192, dtype=dt, device=dev)
+    yt = torch.empty(192, 256, dtype=dt, device=dev)
+    scale = torch.tensor([2.0], device=dev)
+    amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
+    C.fp8_cast_transpose(x, y, yt, scale, amax, fmt)
+    fm = 448.0 if fmt == 0 else 57344.0
+    ref = (x.float() * 2.0).clamp(-fm, fm).to(dt)
+    assert (y.float() != ref.float()).float().mean().item() < 1e-3
+    assert torch.equal(yt.view(torch.uint8), y.view(torch.uint8).t().contiguous())
+    assert float(amax.max()) == float(x.float().abs().max())
+
+
+def test_fp8_weight_gradient_path(dev):
+    """Fp8Linear: forward caches X^T (e4m3), wgrad casts dY with its transpose (e5m2), runs
+    dY^T . X^T in fp8 and hands the e5m2 dY to the dgrad that follows."""
+    from ml_trainer_amd.ops.fp8 import FP8, context
+    g = torch.Generator().manual_seed(9)
+    T, I, O = 512, 256, 384
+    x = (torch.randn(T, I, generator=g) * 0.5).to(dev).to(torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(O, I, generator=g) * 0.05).to(dev))
+    dy = (torch.randn(T, O, generator=g) * 0.1).to(dev).to(torch.bfloat16)
+    ctx = context(x.device)
+    for _ in range(3):  # delayed scaling settles after the first steps
+        FP8.fwd(x, w)
+        st = w._mlt_f8
+        assert st.xt is not None and st.xt[0] == x.data_ptr()
+        dw = FP8.wgrad(w, dy, x, None)
+        assert dw is not None and st.xt is None and st.dy8 is not None
+        out = torch.empty(T, I, dtype=torch.bfloat16, device=dev)
+        FP8.dgrad(dy, w, out)
+        assert st.dy8 is None
+        ctx.update()
+    ref_dw = dy.float().t() @ x.float()
+    rel = (dw - ref_dw).norm() / ref_dw.norm()
+    assert rel < 0.1, float(rel)
+    ref_dx = dy.float() @ w.detach().float()
+    rel = (out.float() - ref_dx).norm() / ref_dx.norm()
+    assert rel < 0.1, float(rel)
+    # accumulate form
+    acc = torch.ones(O, I, device=dev)
+    FP8.fwd(x, w)
+    assert FP8.wgrad(w, dy, x, acc) is acc
+    assert ((acc - 1 - ref_dw).norm() / ref_dw.norm()) < 0.1
