@@ -154,14 +154,20 @@ def _fp8_wgrad_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 class Fp8Linear:
     """Linear arithmetic for ops.transformer blocks, all three GEMMs in fp8 (delayed scaling):
     forward X(e4m3) . W^T(e4m3), dgrad dY(e5m2) . W(e4m3), wgrad dY^T(e5m2) . X^T(e4m3) -- the
-    activations are cast together with their transposes so every operand is k-contiguous."""
+    activations are cast together with their transposes so every operand is k-contiguous.
+
+    ``training``: whether a backward will follow (the block wrappers set it from the caller's
+    grad mode, which autograd switches off inside Function.forward); only then are the
+    transposed activations produced and kept."""
+
+    training = True
 
     @staticmethod
     def fwd(x, w, bias=None, gelu_aux=None, res=None):
         C = require_native()
         ctx = context(x.device)
         st = weight_fp8(w, ctx)
-        if torch.is_grad_enabled() and _fp8_wgrad_ok(x, w):
+        if Fp8Linear.training and _fp8_wgrad_ok(x, w):
             x8, x8t = ctx.cast_t(x, st.mx, E4M3)
             st.xt = (x.data_ptr(), x8t)
         else:

@@ -366,20 +366,31 @@ class _Embeddings(torch.autograd.Function):
         return (None, None) + ret + (None,)
 
 
+def _mark_training(impl) -> None:
+    # autograd runs Function.forward with grad mode off: tell the linear implementation here
+    # whether a backward will follow (fp8 keeps transposed activations only then)
+    if impl is not BF16:
+        type(impl).training = torch.is_grad_enabled()
+
+
 def attention_block(x, wqkv, bqkv, wo, bo, lens: Optional[torch.Tensor], B: int, S: int, H: int, impl=BF16):
+    _mark_training(impl)
     return _AttentionBlock.apply(x, wqkv, bqkv, wo, bo, lens, B, S, H, impl)
 
 
 def ffn_block(x, w1, b1, w2, b2, impl=BF16):
+    _mark_training(impl)
     return _FFNBlock.apply(x, w1, b1, w2, b2, impl)
 
 
 def attention_ln_block(x, wqkv, bqkv, wo, bo, gamma, beta, lens: Optional[torch.Tensor], B: int, S: int, H: int,
                        eps: float, impl=BF16):
+    _mark_training(impl)
     return _AttentionLNBlock.apply(x, wqkv, bqkv, wo, bo, gamma, beta, lens, B, S, H, eps, impl)
 
 
 def ffn_ln_block(x, w1, b1, w2, b2, gamma, beta, eps: float, impl=BF16):
+    _mark_training(impl)
     return _FFNLNBlock.apply(x, w1, b1, w2, b2, gamma, beta, eps, impl)
 
 

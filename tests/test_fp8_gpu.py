@@ -189,3 +189,19 @@ def test_fp8_weight_gradient_path(dev):
     FP8.fwd(x, w)
     assert FP8.wgrad(w, dy, x, acc) is acc
     assert ((acc - 1 - ref_dw).norm() / ref_dw.norm()) < 0.1
+
+
+def test_fp8_bert_uses_fp8_weight_gradients(dev):
+    """Through the autograd blocks (grad mode is off inside Function.forward) the forward still
+    keeps X^T and the backward consumes it: no weight is left with an unused transpose."""
+    import torch.nn.functional as F
+    m8, _ = _tiny_fp8_pair(dev)
+    ids = torch.randint(5, 1000, (2, 128), device=dev)
+    out = m8(ids)
+    lin = [p for n, p in m8.named_parameters() if p.dim() == 2 and hasattr(p, "_mlt_f8")]
+    assert lin and all(p._mlt_f8.xt is not None for p in lin)
+    F.cross_entropy(out, torch.zeros(2, dtype=torch.long, device=dev)).backward()
+    assert all(p._mlt_f8.xt is None for p in lin)
+    with torch.no_grad():
+        m8(ids)
+    assert all(p._mlt_f8.xt is None for p in lin)  # inference keeps no transposes
