@@ -1020,5 +1020,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("LENET_CE") = (int)LENET_CE;
   m.attr("LENET_BWD") = (int)LENET_BWD;
   m.attr("LENET_OPT") = (int)LENET_OPT;
+  m.attr("LENET_TRACE") = (int)LENET_TRACE;
   m.attr("LENET_REDUCE") = (int)LENET_REDUCE;
 }

@@ -44,6 +44,28 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// Segmented reductions over aligned groups of G lanes (G power of two, <= 64) built from DPP
+// operand modifiers (quad_perm, row_shr, row_bcast15/31: plain VALU ops, a few cycles each)
+// instead of ds_swizzle / ds_bpermute round trips through the LDS crossbar (~100+ cycles each
+// on a dependent chain). The result is valid in the LAST lane of each group only.
+template <int CTRL, int ROWS, bool MAX>
+__device__ __forceinline__ float dpp_reduce_step(float v) {
+  const float id = MAX ? -INFINITY : 0.f;  // lanes without a source (or in masked rows) combine with this
+  const float o =
+      __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), CTRL, ROWS, 0xF, false));
+  return MAX ? fmaxf(v, o) : v + o;
+}
+template <int G, bool MAX = false>
+__device__ __forceinline__ float group_reduce_last(float v) {
+  if constexpr (G >= 2) v = dpp_reduce_step<0xB1, 0xF, MAX>(v);   // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v = dpp_reduce_step<0x4E, 0xF, MAX>(v);   // quad_perm [2,3,0,1]: quad result in all 4
+  if constexpr (G >= 8) v = dpp_reduce_step<0x114, 0xF, MAX>(v);  // row_shr:4 -> lanes 7, 15: 8-lane result
+  if constexpr (G >= 16) v = dpp_reduce_step<0x118, 0xF, MAX>(v); // row_shr:8 -> lane 15: row result
+  if constexpr (G >= 32) v = dpp_reduce_step<0x142, 0xA, MAX>(v); // row_bcast:15 into rows 1, 3 -> lanes 31, 63
+  if constexpr (G >= 64) v = dpp_reduce_step<0x143, 0xC, MAX>(v); // row_bcast:31 into rows 2, 3 -> lane 63
+  return v;
+}
+
 // Block-wide sum; `red` must hold >= blockDim.x/64 floats of LDS. Result broadcast to all threads.
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

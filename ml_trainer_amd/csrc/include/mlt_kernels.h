@@ -30,6 +30,7 @@ enum LeNetMode : int {
   LENET_BWD = 4,        // dlogits -> all parameter gradients
   LENET_OPT = 8,        // fused optimizer update inside the weight-gradient kernel (single process only)
   LENET_REDUCE = 16,    // (kept for API compatibility: the conv1 reduction always happens inside K5)
+  LENET_TRACE = 256,    // fused kernel: block 0 stores per-phase clock64() stamps into slab1 (K5 skipped)
 };
 
 struct LeNetPtrs {

@@ -19,11 +19,15 @@
 // zeroes it otherwise), so one uint8 per pooled cell stores the arg-max (0..3) or 4
 // for "dead".  The backward never materialises the 4x larger un-pooled gradient.
 // All batch reductions run in a fixed order: results are bitwise reproducible.
+#include <cstdlib>
+
 #include "mlt_common.h"
 #include "mlt_kernels.h"
 #include "mlt_optim.h"
 
 namespace mlt {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 template <int C1_, int C2_, int F1_, int F2_, int NC_>
 struct LeNetDims {
@@ -211,7 +215,10 @@ __global__ __launch_bounds__(128) void lenet_conv2_fwd(const float* __restrict__
 // ---------------------------------------------------------------------------
 constexpr int pow2_ge(int v) { return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : v <= 16 ? 16 : v <= 32 ? 32 : 64; }
 
-template <int NCOLS, int NROWS, int NT>
+// IR (< IT) keeps only the first IR row-iterations in registers; rows >= IR*RPI are read from an
+// LDS image of W (set `lw`, filled by the caller, e.g. by LDS-DMA) -- for a kernel that cannot
+// spare IT*PL*4 registers for the whole layer.
+template <int NCOLS, int NROWS, int NT, int IR_ = -1>
 struct RegLinear {
   static constexpr int NV = NCOLS / 4;
   static constexpr int G = pow2_ge(NV);
@@ -220,13 +227,22 @@ struct RegLinear {
   static constexpr int NW = NT / 64;
   static constexpr int RPI = NW * R;  // row groups (rows per iteration over the block)
   static constexpr int IT = (NROWS + RPI - 1) / RPI;
+  static constexpr int IR = IR_ < 0 || IR_ > IT ? IT : IR_;  // register-resident iterations
+  static constexpr int LROW0 = IR * RPI;                      // first LDS-resident row
+  static constexpr int LDS_FLOATS = NROWS > LROW0 ? (NROWS - LROW0) * NCOLS : 0;
   static constexpr int SCRATCH = RPI * NCOLS;
-  float4 w[IT][PL];
+  float4 w[IR > 0 ? IR : 1][PL];
   float bias[IT];
+  const float4* lw = nullptr;  // LDS image [NROWS - LROW0][NV] (float4) of the non-resident rows
 
   __device__ __forceinline__ int row(int it) const {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     return it * RPI + wid * R + lane / G;
+  }
+  // weight float4 v of the row this lane handles in iteration `it` (it is a compile-time unrolled index)
+  __device__ __forceinline__ float4 wv(int it, int i, int v) const {
+    if (it < IR) return w[it < IR ? it : 0][i];
+    return lw[(min(row(it), NROWS - 1) - LROW0) * NV + min(v, NV - 1)];  // padding: as load()
   }
   __device__ __forceinline__ void load(const float* __restrict__ W, const float* __restrict__ b) {
     const int gl = (threadIdx.x & 63) % G;
@@ -234,12 +250,17 @@ struct RegLinear {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int r = row(it);
+      if (it < IR) {
 #pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const int v = gl + i * G;
-        w[it][i] = (r < NROWS && v < NV) ? w4[r * NV + v] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < PL; ++i) {
+          const int v = gl + i * G;
+          // clamped, unconditional loads (a guarded load compiles to a branch + vmcnt(0) each): the
+          // weights of padding rows / columns are never used (fwd stores only r < NROWS, v < NV;
+          // bwd scales padding rows by dv = 0 and stores only v < NV)
+          w[it < IR ? it : 0][i] = w4[min(r, NROWS - 1) * NV + min(v, NV - 1)];
+        }
       }
-      bias[it] = r < NROWS ? b[r] : 0.f;
+      bias[it] = b[min(r, NROWS - 1)];
     }
   }
   template <bool RELU>
@@ -253,16 +274,16 @@ struct RegLinear {
       for (int i = 0; i < PL; ++i) {
         const int v = gl + i * G;
         if (v < NV) {
-          const float4 xv = x4[v];
-          acc = fmaf(w[it][i].x, xv.x, acc);
-          acc = fmaf(w[it][i].y, xv.y, acc);
-          acc = fmaf(w[it][i].z, xv.z, acc);
-          acc = fmaf(w[it][i].w, xv.w, acc);
+          const float4 xv = x4[v], wq = wv(it, i, v);
+          acc = fmaf(wq.x, xv.x, acc);
+          acc = fmaf(wq.y, xv.y, acc);
+          acc = fmaf(wq.z, xv.z, acc);
+          acc = fmaf(wq.w, xv.w, acc);
         }
       }
-      acc = group_sum<G>(acc);
+      acc = group_reduce_last<G>(acc);  // DPP tree: valid in the group's last lane
       const int r = row(it);
-      if (gl == 0 && r < NROWS) {
+      if (gl == G - 1 && r < NROWS) {
         float o = acc + bias[it];
         if (RELU) o = fmaxf(o, 0.f);
         out_lds[r] = o;
@@ -286,10 +307,11 @@ struct RegLinear {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        acc.x = fmaf(dv[it], w[it][i].x, acc.x);
-        acc.y = fmaf(dv[it], w[it][i].y, acc.y);
-        acc.z = fmaf(dv[it], w[it][i].z, acc.z);
-        acc.w = fmaf(dv[it], w[it][i].w, acc.w);
+        const float4 wq = wv(it, i, v);
+        acc.x = fmaf(dv[it], wq.x, acc.x);
+        acc.y = fmaf(dv[it], wq.y, acc.y);
+        acc.z = fmaf(dv[it], wq.z, acc.z);
+        acc.w = fmaf(dv[it], wq.w, acc.w);
       }
       if (v < NV) reinterpret_cast<float4*>(scratch)[grp * NV + v] = acc;
     }
@@ -313,36 +335,40 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // ---------------------------------------------------------------------------
 constexpr int kFcThreads = 1024;
 
-template <class D>
-__global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, float inv_B) {
-  constexpr int FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC, NT = kFcThreads;
-  using L1 = RegLinear<FLAT, F1, NT>;
-  using L2 = RegLinear<F1, F2, NT>;
-  using L3 = RegLinear<F2, NC, NT>;
-  constexpr int SCR = cmax(L1::SCRATCH, cmax(L2::SCRATCH, L3::SCRATCH));
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  __shared__ __attribute__((aligned(16))) float f[FLAT];
-  __shared__ __attribute__((aligned(16))) float sh1[F1];
-  __shared__ __attribute__((aligned(16))) float sh2[F2];
-  __shared__ __attribute__((aligned(16))) float sdl[64];
-  __shared__ __attribute__((aligned(16))) float sdh2[F2];
-  __shared__ __attribute__((aligned(16))) float sdh1[F1];
-  __shared__ __attribute__((aligned(16))) float slog[64];
-  __shared__ __attribute__((aligned(16))) float scratch[SCR];
+// LDS of the fc chain (shared by K3 and the fused per-sample kernel)
+template <class D, int NT, int IR1 = -1>
+struct FcLds {
+  using L1 = RegLinear<D::FLAT, D::F1, NT, IR1>;
+  using L2 = RegLinear<D::F1, D::F2, NT>;
+  using L3 = RegLinear<D::F2, D::NC, NT>;
+  static constexpr int SCR = cmax(L1::SCRATCH, cmax(L2::SCRATCH, L3::SCRATCH));
+  alignas(16) float sh1[D::F1];  // RegLinear reads its inputs as float4
+  alignas(16) float sh2[D::F2];
+  alignas(16) float sdl[64];
+  alignas(16) float sdh2[D::F2];
+  alignas(16) float sdh1[D::F1];
+  alignas(16) float slog[64];
+};
 
-  // the label is needed only by the CE phase, but loading it now keeps it off the dependent chain
-  const int64_t tgt_pre = (mode & LENET_CE) ? P.targets[b] : 0;
-  L1 l1;
-  L2 l2;
-  L3 l3;
-  l1.load(P.w3, P.b3);  // all weight loads in flight together
-  l2.load(P.w4, P.b4);
-  l3.load(P.w5, P.b5);
-
+// fc1 -> fc2 -> fc3 (fwd, from `f` in LDS) -> softmax-CE -> dgrad chain for sample b, with
+// the weights held in registers (l1..l3 loaded by the caller). Writes h1/h2/logits/dlogits/
+// dh2/dh1/dflat of sample b to global (K5 reads them); dflat also to `dflat_lds` if given.
+// Every path ends with a barrier.
+template <class D, int NT, int IR1>
+__device__ __forceinline__ void fc_chain(int mode, const LeNetPtrs& P, int b, int64_t tgt_pre, float inv_B,
+                                         const typename FcLds<D, NT, IR1>::L1& l1,
+                                         const typename FcLds<D, NT, IR1>::L2& l2,
+                                         const typename FcLds<D, NT, IR1>::L3& l3, const float* f,
+                                         FcLds<D, NT, IR1>& s, float* scratch, float* dflat_lds) {
+  constexpr int FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  float* sh1 = s.sh1;
+  float* sh2 = s.sh2;
+  float* sdl = s.sdl;
+  float* sdh2 = s.sdh2;
+  float* sdh1 = s.sdh1;
+  float* slog = s.slog;
   if (mode & LENET_FWD) {
-    const float4* src = reinterpret_cast<const float4*>(P.p2 + (int64_t)b * FLAT);
-    if (t < FLAT / 4) reinterpret_cast<float4*>(f)[t] = src[t];
-    __syncthreads();
     l1.template fwd<true>(f, sh1, P.h1 + (int64_t)b * F1);
     __syncthreads();
     l2.template fwd<true>(sh1, sh2, P.h2 + (int64_t)b * F2);
@@ -358,10 +384,11 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
 
   if (mode & LENET_CE) {
     if (wid == 0) {
+      constexpr int GC = pow2_ge(NC);  // logits live in lanes [0, NC): reduce one DPP group, read its last lane
       const float z = lane < NC ? slog[lane] : -INFINITY;
-      const float mx = wave_max(z);
+      const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC, true>(z)), GC - 1));
       const float e = lane < NC ? expf(z - mx) : 0.f;
-      const float s = wave_sum(e);
+      const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC>(e)), GC - 1));
       const float lse = mx + logf(s);
       const int64_t tgt = tgt_pre;
       const bool valid = tgt >= 0 && tgt < NC;
@@ -387,8 +414,33 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
   if (mode & LENET_BWD) {
     l3.bwd(sdl, scratch, sdh2, P.dh2 + (int64_t)b * F2, sh2);
     l2.bwd(sdh2, scratch, sdh1, P.dh1 + (int64_t)b * F1, sh1);
-    l1.bwd(sdh1, scratch, nullptr, P.dflat + (int64_t)b * FLAT, nullptr);
+    l1.bwd(sdh1, scratch, dflat_lds, P.dflat + (int64_t)b * FLAT, nullptr);
   }
+}
+
+template <class D>
+__global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, float inv_B) {
+  constexpr int FLAT = D::FLAT, NT = kFcThreads;
+  using S = FcLds<D, NT>;
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float f[FLAT];
+  __shared__ __attribute__((aligned(16))) S s;
+  __shared__ __attribute__((aligned(16))) float scratch[S::SCR];
+
+  // the label is needed only by the CE phase, but loading it now keeps it off the dependent chain
+  const int64_t tgt_pre = (mode & LENET_CE) ? P.targets[b] : 0;
+  typename S::L1 l1;
+  typename S::L2 l2;
+  typename S::L3 l3;
+  l1.load(P.w3, P.b3);  // all weight loads in flight together
+  l2.load(P.w4, P.b4);
+  l3.load(P.w5, P.b5);
+  if (mode & LENET_FWD) {
+    const float4* src = reinterpret_cast<const float4*>(P.p2 + (int64_t)b * FLAT);
+    if (t < FLAT / 4) reinterpret_cast<float4*>(f)[t] = src[t];
+    __syncthreads();
+  }
+  fc_chain<D, NT, -1>(mode, P, b, tgt_pre, inv_B, l1, l2, l3, f, s, scratch, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -480,6 +532,356 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
     g1[base + 1] = i1[base + 1] < 4 ? s.y : 0.f;
     g1[base + 14] = i1[base + 14] < 4 ? s.z : 0.f;
     g1[base + 15] = i1[base + 15] < 4 ? s.w : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// KF: K1..K4 fused -- the whole per-sample chain in ONE 1024-thread block per sample:
+//   [augment] -> conv1+ReLU+pool -> conv2+ReLU+pool -> fc1/fc2/fc3 -> softmax-CE
+//   -> fc dgrad chain -> unpool2 -> conv2 dgrad -> pool1 liveness mask.
+// Nothing in that chain crosses samples (only the weight-gradient batch sums of K5 do), so the
+// four launches -- each a launch boundary plus a global round trip of its inputs -- become one,
+// and every intermediate stays in LDS. One CU per sample means the phases must run near the
+// CU's VALU rate, so each is register-tiled (a thread owns a row strip: every LDS operand
+// read feeds 4-14 FMAs) over row-padded, 16-byte-aligned LDS images read with ds_read_b128,
+// and split reductions (input- / output-channel groups, row pairs) are combined across the
+// lanes of a quad with DPP (VALU, no LDS round trip) in a fixed order.
+//
+// The phases follow `mode` (FWD: conv1..fc3 [+CE]; BWD: fc dgrad .. conv2 dgrad, reading the
+// forward state from global when FWD is absent), so the autograd path (FWD, then BWD with a
+// given dlogits) runs the same arithmetic as the fused engine step. fc1's weights do not fit
+// the register budget of 1024 threads beside the conv phases: the first kFusedFc1Regs row
+// iterations stay in registers, the rest are LDS-DMA'd (global_load_lds) at entry.
+// Writes exactly the tensors K5 reads (x, p1, i1, p2, i2, h1, h2, logits, dlogits, dh2, dh1,
+// dflat, g1).
+// ---------------------------------------------------------------------------
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedFc1Regs = 4;  // fc1 row-iterations kept in registers; the rest of W3 is DMA'd to LDS
+constexpr int kXs = 36;           // padded row stride (floats) of the input image [3][32][kXs]
+constexpr int kP1s = 16;          // padded row stride of the pooled conv1 map [C1][14][kP1s]
+constexpr int kDcs = 20;          // padded row stride of the zero-padded conv2-output grad [C2][18][kDcs]
+
+// quad lane exchanges (DPP quad_perm: a VALU operand modifier, no LDS crossbar round trip)
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
+// max-pool of a 2x2 window (k = 0..3 in row-major window order, first max wins) + ReLU;
+// the arg-max code is 4 for a dead cell (as K1/K2)
+__device__ __forceinline__ void pool4(float a00, float a01, float a10, float a11, float& pv, uint8_t& iv) {
+  float m = a00;
+  int k = 0;
+  if (a01 > m) { m = a01; k = 1; }
+  if (a10 > m) { m = a10; k = 2; }
+  if (a11 > m) { m = a11; k = 3; }
+  pv = m > 0.f ? m : 0.f;
+  iv = m > 0.f ? (uint8_t)k : (uint8_t)4;
+}
+
+template <class D>
+struct FusedLds {
+  using S = FcLds<D, kFusedThreads, kFusedFc1Regs>;
+  static constexpr int W3L = S::L1::LDS_FLOATS > 0 ? S::L1::LDS_FLOATS : 4;
+  static constexpr int XS = 3 * 32 * kXs;         // padded input image
+  static constexpr int U0 = XS + 192 * 4;          // + the raw uint8 image (phases 0-1)
+  static constexpr int DC = D::C2 * 18 * kDcs;     // phases 5-6
+  static constexpr int U = cmax(U0, cmax(S::SCR, DC));
+  alignas(16) float u[U];  // image -> fc dgrad scratch -> dc (phases never overlap; barriers between)
+  alignas(16) float p1[D::C1 * 14 * kP1s];
+  alignas(16) float f[D::FLAT];
+  alignas(16) float df[D::FLAT];
+  alignas(16) S s;
+  alignas(16) float w3l[W3L];  // fc1 rows >= L1::LROW0, filled by global_load_lds
+  float w1[D::C1 * 75], b1[D::C1], w2[D::C2 * D::C1 * 25], b2[D::C2];
+  uint8_t i1[D::C1 * 196], i2[D::FLAT];
+};
+
+template <class D>
+__global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, LeNetPtrs P, LeNetAug aug,
+                                                                    float inv_B) {
+  constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, NT = kFusedThreads;
+  static_assert(C1 % 2 == 0 && C2 % 4 == 0 && C1 * 98 <= NT && C2 * 20 <= NT && C1 * 56 <= NT,
+                "fused LeNet geometry");
+  using S = typename FusedLds<D>::S;
+  const int b = blockIdx.x, t = threadIdx.x, wid = t >> 6;
+  const bool fwd = (mode & LENET_FWD) != 0, bwd = (mode & LENET_BWD) != 0;
+  __shared__ __attribute__((aligned(16))) FusedLds<D> L;
+  float* xs = L.u;
+  uint4* rawimg = reinterpret_cast<uint4*>(L.u + FusedLds<D>::XS);
+  // LENET_TRACE: per-phase cycle stamps of block 0 (phase profiling; K5 is not launched then)
+  const bool trace = (mode & LENET_TRACE) && b == 0 && t == 0;
+  auto stamp = [&](int k) {  // pinned in place: s_memtime can otherwise float across whole phases
+    if (!(mode & LENET_TRACE)) return;
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long c, w;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c), "=s"(w)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (trace) {
+      reinterpret_cast<unsigned long long*>(P.slab1)[k] = c;
+      if (k == 0 || k == 7) reinterpret_cast<unsigned long long*>(P.slab1)[8 + k / 7] = w;  // 100 MHz
+    }
+  };
+  stamp(0);
+
+  // ---- phase 0: every load in flight together. Independent loads first and branch-free
+  // (clamped indices: a guarded load compiles to a branch + vmcnt(0) per element), then the
+  // sample-index chain (ctrl -> perm -> image, the longest dependent chain of the kernel), then
+  // the LDS-DMA of fc1's LDS-resident rows, which must not sit in front of a chain wait.
+  constexpr int NW2 = (C2 * C1 * 25 + NT - 1) / NT;
+  static_assert(C1 * 75 <= NT && C1 * 196 <= 2 * NT, "one conv1 filter element / two i1 bytes per thread");
+  const float w1r = P.w1[min(t, C1 * 75 - 1)];
+  float w2r[NW2];
+#pragma unroll
+  for (int j = 0; j < NW2; ++j) w2r[j] = P.w2[min(t + j * NT, C2 * C1 * 25 - 1)];
+  const float b1r = P.b1[min(t, C1 - 1)], b2r = P.b2[min(t, C2 - 1)];
+  typename S::L1 l1;
+  typename S::L2 l2;
+  typename S::L3 l3;
+  l2.load(P.w4, P.b4);
+  l3.load(P.w5, P.b5);
+  int64_t idx = 0;
+  bool fl = false;
+  int ci = 0, cj = 0;
+  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+  float4 xin = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint8_t i1r[2] = {0, 0}, i2r = 0;
+  if (fwd) {
+    if (aug.data) {
+      const int64_t step = aug.ctrl[0], sie = aug.ctrl[1];
+      int64_t pos = sie * aug.batch_stride + b;
+      if (pos >= aug.perm_len) pos %= aug.perm_len;
+      idx = aug.perm[pos];
+      idx = idx < 0 ? 0 : (idx >= aug.n ? aug.n - 1 : idx);
+      const uint64_t h = mix64(mix64(aug.seed + (uint64_t)step) ^ (uint64_t)pos);
+      const int span = 2 * aug.pad + 1;
+      ci = aug.pad ? (int)(h % span) : 0;
+      cj = aug.pad ? (int)((h >> 20) % span) : 0;
+      fl = aug.flip && ((h >> 40) & 1);
+      raw = reinterpret_cast<const uint4*>(aug.data + idx * 3072)[min(t, 191)];
+    } else {
+      xin = reinterpret_cast<const float4*>(P.x + (int64_t)b * 3072)[min(t, 767)];
+    }
+  } else if (bwd) {  // backward only: the forward state comes from global
+    i1r[0] = P.i1[(int64_t)b * C1 * 196 + min(t, C1 * 196 - 1)];
+    i1r[1] = P.i1[(int64_t)b * C1 * 196 + min(t + NT, C1 * 196 - 1)];
+    i2r = P.i2[(int64_t)b * FLAT + min(t, FLAT - 1)];
+  }
+  int64_t tgt_pre = 0;
+  if (mode & LENET_CE) tgt_pre = (fwd && aug.data) ? P.dtargets[idx] : P.targets[b];
+  if constexpr (S::L1::LDS_FLOATS > 0) {  // fc1 rows beyond the register budget: LDS-DMA, no VGPRs
+    constexpr int CH = S::L1::LDS_FLOATS / 4;  // 16-byte chunks
+    const float* src = P.w3 + S::L1::LROW0 * FLAT;
+#pragma unroll
+    for (int i = 0; i < (CH + NT - 1) / NT; ++i) {
+      const int e = i * NT + t;
+      if (e < CH)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * e), (lds_void_t*)(L.w3l + 4 * (i * NT + wid * 64)),
+                                         16, 0, 0);
+    }
+  }
+  l1.lw = reinterpret_cast<const float4*>(L.w3l);
+  if (t < C1 * 75) L.w1[t] = w1r;
+#pragma unroll
+  for (int j = 0; j < NW2; ++j)
+    if (t + j * NT < C2 * C1 * 25) L.w2[t + j * NT] = w2r[j];
+  if (t < C1) L.b1[t] = b1r;
+  if (t < C2) L.b2[t] = b2r;
+  if (fwd) {
+    if (aug.data) {
+      if (t < 192) rawimg[t] = raw;
+    } else if (t < 768) {  // [3*32 rows][8 float4] -> padded rows
+      *reinterpret_cast<float4*>(xs + (t >> 3) * kXs + (t & 7) * 4) = xin;
+    }
+  } else if (bwd) {
+    if (t < C1 * 196) L.i1[t] = i1r[0];
+    if (t + NT < C1 * 196) L.i1[t + NT] = i1r[1];
+    if (t < FLAT) L.i2[t] = i2r;
+  }
+  __syncthreads();
+
+  stamp(1);
+  // ---- phase 1: RandomCrop(pad) + HFlip + Normalize from the staged uint8 image
+  if (fwd && aug.data) {
+    const uint8_t* img = reinterpret_cast<const uint8_t*>(rawimg);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = t + i * NT;
+      const int c = e >> 10, y = (e >> 5) & 31, xx = e & 31;
+      const int sx = fl ? 31 - xx : xx;
+      const int r = y + ci - aug.pad, q = sx + cj - aug.pad;
+      const bool in = (unsigned)r < 32u && (unsigned)q < 32u;
+      const float u = in ? (float)img[(r * 32 + q) * 3 + c] : 0.f;
+      const float v = (u / 255.f - aug.mean[c]) / aug.std[c];
+      xs[(c * 32 + y) * kXs + xx] = v;  // the raw image is a disjoint part of L.u
+      P.x[(int64_t)b * 3072 + e] = v;
+    }
+    if (t == 0 && P.targets) P.targets[b] = tgt_pre;
+    __syncthreads();
+  }
+
+  stamp(2);
+  // ---- phase 2: conv1 + bias + ReLU + maxpool2. Thread = (oc, pooled row, 2 pooled columns):
+  // a 2x4 conv-output strip, input rows read as 2 x b128.
+  if (fwd && t < C1 * 98) {
+    const int oc = t / 98, rem = t - oc * 98, py = rem / 7, pxg = rem - py * 7, y0 = 2 * py, x0 = 4 * pxg;
+    const float bias = L.b1[oc];
+    float acc[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[j][c] = bias;
+#pragma unroll
+    for (int ic = 0; ic < 3; ++ic) {
+      const float* wk = L.w1 + oc * 75 + ic * 25;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const float* row = xs + (ic * 32 + y0 + r) * kXs + x0;
+        const float4 lo = *reinterpret_cast<const float4*>(row), hi = *reinterpret_cast<const float4*>(row + 4);
+        const float in[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int kh = r - j;
+          if (kh < 0 || kh > 4) continue;
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const float wv = wk[kh * 5 + kw];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[j][c] = fmaf(wv, in[c + kw], acc[j][c]);
+          }
+        }
+      }
+    }
+    float pv[2];
+    uint8_t iv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) pool4(acc[0][2 * q], acc[0][2 * q + 1], acc[1][2 * q], acc[1][2 * q + 1], pv[q], iv[q]);
+    *reinterpret_cast<float2*>(L.p1 + (oc * 14 + py) * kP1s + 2 * pxg) = make_float2(pv[0], pv[1]);
+    const int o = oc * 196 + py * 14 + 2 * pxg;
+    L.i1[o] = iv[0];
+    L.i1[o + 1] = iv[1];
+    *reinterpret_cast<float2*>(P.p1 + (int64_t)b * C1 * 196 + o) = make_float2(pv[0], pv[1]);
+    P.i1[(int64_t)b * C1 * 196 + o] = iv[0];
+    P.i1[(int64_t)b * C1 * 196 + o + 1] = iv[1];
+  }
+  if (fwd) __syncthreads();
+
+  stamp(3);
+  // ---- phase 3: conv2 + bias + ReLU + maxpool2 -> flatten. Quad = (oc, pooled row), lane bit 0 =
+  // input-channel half, bit 1 = conv row of the pair; a lane computes a 10-wide conv row over
+  // its C1/2 channels; halves summed, then rows pooled, across the quad (DPP).
+  // (fc1's register weights are loaded here, not at entry: held through conv1 they spill)
+  l1.load(P.w3, P.b3);
+  if (fwd && t < C2 * 20) {
+    const int icg = t & 1, ry = (t >> 1) & 1, rest = t >> 2, oc = rest / 5, py = rest - oc * 5;
+    const int y = 2 * py + ry;
+    float acc[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int icc = 0; icc < C1 / 2; ++icc) {
+      const int ic = icg * (C1 / 2) + icc;
+      const float* wk = L.w2 + (oc * C1 + ic) * 25;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh) {
+        const float4* row = reinterpret_cast<const float4*>(L.p1 + (ic * 14 + y + kh) * kP1s);
+        const float4 v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3];
+        const float in[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                              v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float wv = wk[kh * 5 + kw];
+#pragma unroll
+          for (int c = 0; c < 10; ++c) acc[c] = fmaf(wv, in[c + kw], acc[c]);
+        }
+      }
+    }
+    const float bias = L.b2[oc];
+    float s[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {  // (first half + second half) + bias, identical in both lanes
+      const float o = quad_xor1(acc[c]);
+      s[c] = (icg ? o + acc[c] : acc[c] + o) + bias;
+    }
+#pragma unroll
+    for (int pc = 0; pc < 5; ++pc) {
+      const float n0 = quad_xor2(s[2 * pc]), n1 = quad_xor2(s[2 * pc + 1]);  // the other conv row
+      if (t & 3) continue;  // lane (ry 0, icg 0) owns the pooled row
+      float pv;
+      uint8_t iv;
+      pool4(s[2 * pc], s[2 * pc + 1], n0, n1, pv, iv);
+      const int o = oc * 25 + py * 5 + pc;
+      L.f[o] = pv;
+      L.i2[o] = iv;
+      P.p2[(int64_t)b * FLAT + o] = pv;
+      P.i2[(int64_t)b * FLAT + o] = iv;
+    }
+  }
+  __syncthreads();
+
+  stamp(4);
+  // ---- phase 4: fc chain + CE (+ fc dgrad -> dflat); scratch aliases the (dead) image
+  fc_chain<D, NT, kFusedFc1Regs>(mode, P, b, tgt_pre, inv_B, l1, l2, l3, L.f, L.s, L.u, L.df);
+  if (!bwd) return;
+
+  stamp(5);
+  // ---- phase 5: unpool2 -> dense zero-padded conv2-output grad (aliases the dead scratch)
+  float* dc = L.u;
+  for (int e = t; e < C2 * 18 * kDcs; e += NT) {
+    const int o = e / (18 * kDcs), r = e - o * (18 * kDcs), cy = r / kDcs - 4, cx = r % kDcs - 4;
+    float v = 0.f;
+    if ((unsigned)cy < 10u && (unsigned)cx < 10u) {
+      const int pp = o * 25 + (cy >> 1) * 5 + (cx >> 1);
+      v = L.i2[pp] == (uint8_t)(((cy & 1) << 1) | (cx & 1)) ? L.df[pp] : 0.f;
+    }
+    dc[e] = v;
+  }
+  __syncthreads();
+
+  stamp(6);
+  // ---- phase 6: conv2 dgrad -> pool1 liveness mask -> g1. Quad = (input channel, output row),
+  // lane = quarter of the output channels; a lane computes the 14-wide row over its C2/4
+  // channels, the quarters are summed across the quad (DPP, same order in every lane).
+  if (t < C1 * 56) {
+    const int og = t & 3, rest = t >> 2, ic = rest / 14, y = rest - ic * 14;
+    float acc[14];
+#pragma unroll
+    for (int x = 0; x < 14; ++x) acc[x] = 0.f;
+#pragma unroll
+    for (int oo = 0; oo < C2 / 4; ++oo) {
+      const int o = og * (C2 / 4) + oo;
+      const float* wk = L.w2 + (o * C1 + ic) * 25;
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {  // padded input row y + r pairs with kernel row kh = 4 - r
+        const float4* row = reinterpret_cast<const float4*>(dc + (o * 18 + y + r) * kDcs);
+        const float4 v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4];
+        const float in[20] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y,
+                              v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, v4.x, v4.y, v4.z, v4.w};
+        const int kh = 4 - r;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float wv = wk[kh * 5 + kw];
+#pragma unroll
+          for (int x = 0; x < 14; ++x) acc[x] = fmaf(wv, in[x + 4 - kw], acc[x]);
+        }
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < 14; ++x) {
+      const float s1 = acc[x] + quad_xor1(acc[x]);  // commutative steps: every lane gets the same sum
+      acc[x] = s1 + quad_xor2(s1);
+    }
+    float* g = P.g1 + (int64_t)b * C1 * 196 + ic * 196 + y * 14;
+    const uint8_t* m = L.i1 + ic * 196 + y * 14;
+#pragma unroll
+    for (int x = 0; x < 14; ++x)
+      if ((x & 3) == og) g[x] = m[x] < 4 ? acc[x] : 0.f;
+  }
+  if (mode & LENET_TRACE) {
+    __syncthreads();
+    stamp(7);
   }
 }
 
@@ -807,16 +1209,29 @@ template <class D>
 static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
   if (B <= 0) return;
   const float inv_B = 1.f / (float)B;
-  if (mode & LENET_FWD) {
-    hipLaunchKernelGGL(lenet_conv1_fwd<D>, dim3(B, D::C1), dim3(256), 0, st, A, P.w1, P.b1, P.x, P.p1, P.i1,
-                       A.data ? P.targets : nullptr, P.dtargets);
-    hipLaunchKernelGGL(lenet_conv2_fwd<D>, dim3(B, D::C2 / 4), dim3(128), 0, st, P.p1, P.w2, P.b2, P.p2, P.i2);
+  // MLT_LENET_FUSED=1 runs K1..K4 as the fused per-sample kernel KF in every mode (engine steps,
+  // evaluation and the autograd halves alike). Measured (MI355X, batch 32, bench.py): the
+  // four-kernel path is still faster (40.2 vs ~40-44 us per step): one CU per sample leaves
+  // KF's conv phases LDS-latency bound, so it stays opt-in.
+  static const bool fused_ok = [] {
+    const char* v = getenv("MLT_LENET_FUSED");
+    return v != nullptr && atoi(v) != 0;
+  }();
+  const bool fused = fused_ok && (mode & (LENET_FWD | LENET_CE | LENET_BWD));
+  if (fused) {
+    hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode, P, A, inv_B);
+  } else {
+    if (mode & LENET_FWD) {
+      hipLaunchKernelGGL(lenet_conv1_fwd<D>, dim3(B, D::C1), dim3(256), 0, st, A, P.w1, P.b1, P.x, P.p1, P.i1,
+                         A.data ? P.targets : nullptr, P.dtargets);
+      hipLaunchKernelGGL(lenet_conv2_fwd<D>, dim3(B, D::C2 / 4), dim3(128), 0, st, P.p1, P.w2, P.b2, P.p2, P.i2);
+    }
+    if (mode & (LENET_FWD | LENET_CE | LENET_BWD))
+      hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
+    if (mode & LENET_BWD)
+      hipLaunchKernelGGL(lenet_conv2_dgrad<D>, dim3(B, D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2, P.i1, P.g1);
   }
-  if (mode & (LENET_FWD | LENET_CE | LENET_BWD)) {
-    hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
-  }
-  if (mode & LENET_BWD) {
-    hipLaunchKernelGGL(lenet_conv2_dgrad<D>, dim3(B, D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2, P.i1, P.g1);
+  if ((mode & LENET_BWD) && !(fused && (mode & LENET_TRACE))) {
     constexpr int NB3 = (D::F1 * (D::FLAT / 4) + 255) / 256, NB4 = (D::F2 * (D::F1 / 4) + 255) / 256,
                   NB5 = (D::NC * (D::F2 / 4) + 255) / 256;
     const int nblk = (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
