@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--model", default="default",
                     choices=["default", "tiny", "bert-base", "bert-tiny", "bert-large", "large"])
     ap.add_argument("--seq-len", type=int, default=512)
+    ap.add_argument("--zero", type=int, default=0, choices=(0, 1),
+                    help="BERT modes, N>1: 1 = ZeRO-1 sharded optimizer state instead of replicated DDP")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (BERT modes)")
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-graph", action="store_true")
@@ -75,7 +77,12 @@ def bench_bert(args, world, rank, dev):
     cfg = bert_config(args.model)
     model = BertClassifier(cfg).to(dev)
     per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
-    if world > 1:
+    if world > 1 and args.zero:
+        from ml_trainer_amd.parallel.zero import ZeroDataParallel
+        ddp = ZeroDataParallel(model)  # ZeRO-1: reduce-scatter, sharded AdamW, all-gather
+        opt = ddp.make_optimizer(FusedAdamW, lr=1e-4, weight_decay=0.01)
+        fwd = ddp
+    elif world > 1:
         ddp = DistributedDataParallel(model)
         opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, flat=ddp.flat)
         fwd = ddp
@@ -139,7 +146,8 @@ def bench_bert(args, world, rank, dev):
                             f"{model.num_parameters():,} params)",
                    "global_batch": per_gpu * world * accum, "per_gpu_batch": per_gpu, "grad_accum": accum,
                    "seq_len": args.seq_len, "fp8": bool(cfg.fp8),
-                   "parallelism": f"dp{world}", "optimizer": "fused AdamW lr=1e-4 wd=0.01 (fp32 master, bf16 shadow)",
+                   "parallelism": f"dp{world}" + ("-zero1" if (args.zero and world > 1) else ""),
+                   "optimizer": "fused AdamW lr=1e-4 wd=0.01 (fp32 master, bf16 shadow)",
                    "tokens_per_s": round(value * args.seq_len, 1),
                    "model_tflops": round(model.flops_per_token(args.seq_len) * value * args.seq_len / 1e12, 1),
                    "loss_finite": math.isfinite(float(loss_acc.item()))},

@@ -14,7 +14,7 @@ CIFAR-shaped dataset and says so in the log.
 
 Extension flags (not in the reference): ``--model`` (default/tiny/bert-base/
 large), ``--synthetic``, ``--per_device_batch``, ``--no_engine``,
-``--no_parallel``, ``--resume``, ``--amp bf16``, ``--metrics_jsonl``.
+``--no_parallel``, ``--resume``, ``--amp bf16``, ``--metrics_jsonl``, ``--zero_stage``.
 """
 from __future__ import annotations
 
@@ -88,7 +88,8 @@ def main(args):
         "backend": args.backend,
     }
     options = {"per_device_batch": args.per_device_batch, "resume": args.resume,
-               "metrics_jsonl": args.metrics_jsonl, "amp": args.amp, "progress": not args.no_progress}
+               "metrics_jsonl": args.metrics_jsonl, "amp": args.amp, "progress": not args.no_progress,
+               "zero_stage": args.zero_stage}
     if args.no_engine:
         options["use_engine"] = False
     trainer = Trainer(model, datasets=datasets, epochs=args.epochs, batch_size=args.batch_size,
@@ -132,6 +133,8 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--no_engine", action="store_true", help="disable the fused LeNet step engine")
     parser.add_argument("--no_parallel", action="store_true", help="do not initialise torch.distributed")
     parser.add_argument("--resume", action="store_true")
+    parser.add_argument("--zero_stage", type=int, default=0, choices=(0, 1),
+                        help="1: ZeRO-1 sharded optimizer state (reduce-scatter / all-gather) under DDP")
     parser.add_argument("--amp", type=str, default=None, choices=[None, "bf16"])
     parser.add_argument("--metrics_jsonl", type=str, default=None)
     parser.add_argument("--no_progress", action="store_true")

@@ -53,6 +53,7 @@ class TrainerOptions:
     bucket_cap_mb: float = 32.0
     first_bucket_mb: float = 4.0
     ddp_mode: str = "overlap"             # "overlap" | "manual" (reference _average_gradients semantics)
+    zero_stage: int = 0                   # 1: ZeRO-1 (reduce-scatter grads, sharded optimizer state, all-gather)
     global_metrics: bool = False          # all-reduce epoch loss/metric across ranks (reference: rank-local)
     dist_timeout_s: float = 1800.0
     # --- data -------------------------------------------------------------------------

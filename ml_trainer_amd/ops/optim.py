@@ -132,9 +132,15 @@ class FusedOptimizer(torch.optim.Optimizer):
             groups.append({k: v for k, v in g.items() if k != "params"})
         return {"kind": self.kind_name, "param_groups": groups,
                 "flat_state": [{"step": self._steps[i],
-                                "s1": None if self._s1[i] is None else self._s1[i].detach().cpu(),
-                                "s2": None if self._s2[i] is None else self._s2[i].detach().cpu()}
+                                "s1": self._export(i, self._s1[i]), "s2": self._export(i, self._s2[i])}
                                for i in range(len(self._flats))]}
+
+    def _export(self, i: int, buf: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        if buf is None:
+            return None
+        fp = self._flats[i]
+        # a ZeRO shard (parallel/zero.py) gathers its state into the full flat layout (collective)
+        return fp.export_state(buf) if hasattr(fp, "export_state") else buf.detach().cpu()
 
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
         if sd.get("kind") != self.kind_name:
@@ -148,7 +154,10 @@ class FusedOptimizer(torch.optim.Optimizer):
                 if st[name] is not None:
                     if buf[i] is None:
                         buf[i] = torch.zeros_like(self._flats[i].data)
-                    buf[i].copy_(st[name].to(buf[i].device))
+                    if hasattr(self._flats[i], "import_state"):
+                        self._flats[i].import_state(st[name], buf[i])
+                    else:
+                        buf[i].copy_(st[name].to(buf[i].device))
             self._lr_dev_val[i] = None if self._lr_dev[i] is None else -1.0
 
 

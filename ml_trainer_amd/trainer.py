@@ -49,6 +49,7 @@ from ml_trainer_amd.ops._ext import native_available
 from ml_trainer_amd.ops.optim import FusedOptimizer, build_optimizer
 from ml_trainer_amd.parallel import dist as mdist
 from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+from ml_trainer_amd.parallel.zero import ZeroDataParallel
 from ml_trainer_amd.parallel.sampler import ShardSampler
 from ml_trainer_amd.utils import checkpoint as ckpt
 from ml_trainer_amd.utils.flat import FlatParams
@@ -172,10 +173,16 @@ class Trainer:
             logger.warning("Testing only available. No datasets in arguments.")
         self.model = self.model.to(self.device)
         self._core = self.model
+        self._zero = None
         if self.is_parallel and mdist.is_dist():
-            self.model = DistributedDataParallel(self.model, bucket_cap_mb=self.opts.bucket_cap_mb,
-                                                 first_bucket_mb=self.opts.first_bucket_mb, mode=self.opts.ddp_mode)
+            if self.opts.zero_stage not in (0, 1):
+                raise ValueError("zero_stage must be 0 or 1")
+            ddp_cls = ZeroDataParallel if self.opts.zero_stage == 1 else DistributedDataParallel
+            self.model = ddp_cls(self.model, bucket_cap_mb=self.opts.bucket_cap_mb,
+                                 first_bucket_mb=self.opts.first_bucket_mb, mode=self.opts.ddp_mode)
             self.flat: Optional[FlatParams] = self.model.flat
+            if self.opts.zero_stage == 1:
+                self._zero = self.model
         else:
             has_params = any(p.requires_grad for p in self.model.parameters())
             self.flat = FlatParams(self.model.parameters()) if has_params else None
@@ -216,10 +223,11 @@ class Trainer:
         if not any(p.requires_grad for p in params):
             return None
         opt = build_optimizer(self.optimizer_type, params, lr=self.lr, momentum=self.momentum,
-                              weight_decay=self.weight_decay, flat=self.flat)
+                              weight_decay=self.weight_decay,
+                              flat=self._zero.shard if self._zero is not None else self.flat)
         if opt is None:
             raise ValueError(f"unknown optimizer {self.optimizer_type!r} (sgd|adam|adagrad|adamax|adamw)")
-        return opt
+        return self._zero.attach_optimizer(opt) if self._zero is not None else opt
 
     def _get_criterion(self):
         c = self.criterion_type
@@ -347,7 +355,9 @@ class Trainer:
     def _optimizer_step(self):
         if self.optimizer is None:
             return
-        if self.opts.grad_clip is not None and self.flat is not None:
+        if self.opts.grad_clip is not None and self._zero is not None:
+            self._zero.clip_grad_norm_(self.opts.grad_clip)
+        elif self.opts.grad_clip is not None and self.flat is not None:
             from ml_trainer_amd.ops.optim import clip_grad_norm_flat
             clip_grad_norm_flat(self.flat, self.opts.grad_clip)
         self.optimizer.step()
@@ -583,6 +593,8 @@ class Trainer:
         target.load_state_dict(sd)
         if self.flat is not None:
             self.flat.rebind_params()
+        if self._zero is not None:
+            self._zero.shard.load_from_full()
         if self.optimizer is not None and "optimizer" in st:
             self.optimizer.load_state_dict(st["optimizer"])
         if self.scheduler is not None and "scheduler" in st:
@@ -599,10 +611,12 @@ class Trainer:
 
     def _checkpoint(self, epoch: int) -> None:
         if self.is_parallel and mdist.is_dist():
+            # ZeRO: gathering the sharded optimizer state is collective, so every rank builds it
+            st = self._trainer_state(epoch) if (self.opts.save_trainer_state and self._zero is not None) else None
             if mdist.rank() == 0:
                 self.save_model(self.model_dir)
                 if self.opts.save_trainer_state:
-                    ckpt.save_trainer_state(self._trainer_state(epoch), self.model_dir)
+                    ckpt.save_trainer_state(st if st is not None else self._trainer_state(epoch), self.model_dir)
             mdist.barrier()  # reference has no barrier after the rank-0 save
         else:
             self.save_model(self.model_dir)

@@ -1,0 +1,108 @@
+"""ZeRO-1 (parallel/zero.py) over gloo, world_size 2 on CPU: sharded AdamW must track replicated DDP."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import TensorCifar, dist_env, free_port
+
+
+def _model():
+    return torch.nn.Sequential(torch.nn.Linear(8, 33), torch.nn.ReLU(), torch.nn.Linear(33, 17),
+                               torch.nn.ReLU(), torch.nn.Linear(17, 4))
+
+
+def _zero_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    from ml_trainer_amd.parallel.zero import ZeroDataParallel
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(world * 6, 8, generator=g)
+    y = torch.randn(world * 6, 4, generator=g)
+    xs, ys = x[rank * 6:(rank + 1) * 6], y[rank * 6:(rank + 1) * 6]
+    out = {}
+    for kind in ("ddp", "zero"):
+        torch.manual_seed(1234 + rank)  # different per rank: the initial broadcast must fix it
+        m = _model()
+        if kind == "zero":
+            w = ZeroDataParallel(m, bucket_cap_mb=0.002, first_bucket_mb=0.001)
+            assert len(w.shard.chunks) >= 2 and w.shard.numel * world == w.flat.numel
+            opt = w.make_optimizer(FusedAdamW, lr=1e-2, weight_decay=0.01)
+            out["state_bytes"] = w.optimizer_state_bytes(opt)
+        else:
+            w = DistributedDataParallel(m, bucket_cap_mb=0.002, first_bucket_mb=0.001)
+            opt = FusedAdamW(m.parameters(), lr=1e-2, weight_decay=0.01, flat=w.flat)
+            out["ddp_state_bytes"] = sum(b.numel() * b.element_size() for b in opt.state_buffers(0))
+        for it in range(4):
+            opt.zero_grad()
+            if it == 1:  # gradient accumulation: local micro-batch without communication
+                with w.no_sync():
+                    ((w(xs) - ys) ** 2).mean().backward()
+            ((w(xs) - ys) ** 2).mean().backward()
+            opt.step()
+        sd = w.state_dict()
+        out[kind] = {k: v.clone() for k, v in sd.items()}
+        if kind == "zero":
+            osd = opt.state_dict()  # collective gather of the sharded state
+            out["zero_s1"] = osd["flat_state"][0]["s1"]
+            # round trip: reload the gathered state, the shard must be unchanged
+            before = opt.state_buffers(0)[0].clone()
+            opt.load_state_dict(osd)
+            assert torch.equal(before, opt.state_buffers(0)[0])
+            out["zero_full_numel"] = w.flat.numel
+    torch.save(out, os.path.join(out_dir, f"z{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_zero1_matches_ddp():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_zero_worker, args=(world, free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"z{i}.pt"), weights_only=True) for i in range(world)]
+        for k in r[0]["ddp"]:
+            assert k.startswith("module.")
+            assert torch.equal(r[0]["zero"][k], r[1]["zero"][k])  # replicas identical after all-gather
+            torch.testing.assert_close(r[0]["zero"][k], r[0]["ddp"][k], rtol=1e-5, atol=1e-6)
+        # optimizer state is sharded: each rank holds half of the (padded) replicated state
+        assert r[0]["state_bytes"] * world == 2 * 4 * r[0]["zero_full_numel"]
+        assert r[0]["state_bytes"] < r[0]["ddp_state_bytes"]
+        assert torch.equal(r[0]["zero_s1"], r[1]["zero_s1"])
+
+
+def _trainer_worker(rank, world, port, out_dir, zero):
+    dist_env(rank, world, port)
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.trainer import Trainer
+    torch.manual_seed(0)
+    tr, va = TensorCifar(64, 0), TensorCifar(32, 1)
+    sub = os.path.join(out_dir, f"zero{zero}")
+    os.makedirs(sub, exist_ok=True)
+    t = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=2, batch_size=32, is_parallel=True, backend="gloo",
+                model_dir=sub, optimizer="adamw", lr=0.01,
+                options={"progress": False, "zero_stage": zero, "grad_clip": 1.0})
+    t.fit()
+    torch.save({"params": t.flat.data.clone(), "losses": t.train_losses},
+               os.path.join(sub, f"t{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_trainer_zero1_tracks_ddp():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        for zero in (0, 1):
+            mp.spawn(_trainer_worker, args=(world, free_port(), d, zero), nprocs=world, join=True)
+        r0 = torch.load(os.path.join(d, "zero0", "t0.pt"), weights_only=True)
+        z = [torch.load(os.path.join(d, "zero1", f"t{i}.pt"), weights_only=True) for i in range(world)]
+        assert torch.equal(z[0]["params"], z[1]["params"])
+        torch.testing.assert_close(z[0]["losses"], r0["losses"], rtol=1e-4, atol=1e-5)
+        sd0 = torch.load(os.path.join(d, "zero0", "model.pth"), weights_only=True)
+        sd1 = torch.load(os.path.join(d, "zero1", "model.pth"), weights_only=True)
+        assert sd0.keys() == sd1.keys()
+        for k in sd0:
+            torch.testing.assert_close(sd1[k], sd0[k], rtol=1e-4, atol=1e-5)
+        assert os.path.exists(os.path.join(d, "zero1", "trainer_state.pt"))
