@@ -234,6 +234,64 @@ void accuracy(Tensor logits, Tensor tgt, Tensor out) {
   launch_accuracy(logits.data_ptr(), bf, tgt.data_ptr<int64_t>(), B, (int)C, out.data_ptr<float>(), cur_stream());
 }
 
+void pointwise_loss_fwd(Tensor p, Tensor t, int64_t mode, Tensor g, Tensor part, Tensor out) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(mode == 0 || mode == 1, "mode must be 0 (l1) or 1 (mse)");
+  TORCH_CHECK(t.numel() == n && g.numel() == n, "pred/target/grad sizes differ");
+  check_dev(p, "pred", at::kFloat, n, 4);
+  check_dev(t, "target", at::kFloat, n, 4);
+  check_dev(g, "grad", at::kFloat, n, 4);
+  check_dev(part, "partials", at::kFloat, loss_partials_needed(), 4);
+  check_dev(out, "out", at::kFloat, 2, 4);
+  launch_pointwise_loss_fwd(p.data_ptr<float>(), t.data_ptr<float>(), n, (int)mode, g.data_ptr<float>(),
+                            part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+}
+
+void nll_fwd(Tensor logp, Tensor tgt, int64_t ignore_index, Tensor part, Tensor out) {
+  TORCH_CHECK(logp.dim() == 2, "log-probabilities must be [B, C]");
+  const int64_t B = logp.size(0), C = logp.size(1);
+  check_dev(logp, "logp", at::kFloat, B * C, 4);
+  check_dev(tgt, "targets", at::kLong, B, 8);
+  TORCH_CHECK(tgt.numel() == B, "targets must have B entries");
+  check_dev(part, "partials", at::kFloat, loss_partials_needed(), 4);
+  check_dev(out, "out", at::kFloat, 2, 4);
+  launch_nll_fwd(logp.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, (int)C, ignore_index, part.data_ptr<float>(),
+                 out.data_ptr<float>(), cur_stream());
+}
+
+void loss_scale_grad(Tensor g, Tensor gout, Tensor stats, Tensor out) {
+  const int64_t n = g.numel();
+  check_dev(g, "g", at::kFloat, n, 4);
+  check_dev(gout, "grad_out", at::kFloat, 1, 4);
+  check_dev(stats, "stats", at::kFloat, 2, 4);
+  TORCH_CHECK(out.numel() == n, "out size");
+  check_dev(out, "out", at::kFloat, n, 4);
+  launch_loss_scale_grad(g.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), n,
+                         out.data_ptr<float>(), cur_stream());
+}
+
+void nll_bwd(Tensor tgt, int64_t C, int64_t ignore_index, Tensor gout, Tensor stats, Tensor out) {
+  const int64_t B = tgt.numel();
+  check_dev(tgt, "targets", at::kLong, B, 8);
+  check_dev(gout, "grad_out", at::kFloat, 1, 4);
+  check_dev(stats, "stats", at::kFloat, 2, 4);
+  TORCH_CHECK(out.numel() == B * C, "out size");
+  check_dev(out, "out", at::kFloat, B * C, 4);
+  launch_nll_bwd(tgt.data_ptr<int64_t>(), B, (int)C, ignore_index, gout.data_ptr<float>(), stats.data_ptr<float>(),
+                 out.data_ptr<float>(), cur_stream());
+}
+
+void mcrmse(Tensor p, Tensor t, Tensor col, Tensor out) {
+  TORCH_CHECK(p.dim() == 2 && t.sizes() == p.sizes(), "mcrmse expects matching [B, C] tensors");
+  const int64_t B = p.size(0), C = p.size(1);
+  check_dev(p, "pred", at::kFloat, B * C, 4);
+  check_dev(t, "target", at::kFloat, B * C, 4);
+  check_dev(col, "col", at::kFloat, C, 4);
+  check_dev(out, "out", at::kFloat, 1, 4);
+  launch_mcrmse(p.data_ptr<float>(), t.data_ptr<float>(), B, (int)C, col.data_ptr<float>(), out.data_ptr<float>(),
+                cur_stream());
+}
+
 // ----------------------------------------------------------------------------
 // bf16 GEMM
 // ----------------------------------------------------------------------------
@@ -941,6 +999,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("accuracy", &accuracy);
+  m.def("pointwise_loss_fwd", &pointwise_loss_fwd);
+  m.def("nll_fwd", &nll_fwd);
+  m.def("loss_scale_grad", &loss_scale_grad);
+  m.def("nll_bwd", &nll_bwd);
+  m.def("mcrmse", &mcrmse);
+  m.def("loss_partials_needed", &loss_partials_needed);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("a_mn"), py::arg("b_mn"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
         py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false, py::arg("cfg") = -1,

@@ -86,6 +86,18 @@ void launch_ce_bwd(const float* dl, const float* gout, const float* acc, int64_t
                    hipStream_t st);
 void launch_accuracy(const void* logits, bool bf16, const int64_t* tgt, int64_t B, int C, float* out,
                      hipStream_t st);
+// Regression / NLL criteria and mcrmse (fp32). `part` holds loss_partials_needed() floats;
+// out/stats[2] = {mean loss, denominator}; g is the unscaled elementwise gradient.
+int loss_partials_needed();
+void launch_pointwise_loss_fwd(const float* p, const float* t, int64_t n, int mode, float* g, float* part,
+                               float* out, hipStream_t st);
+void launch_nll_fwd(const float* logp, const int64_t* tgt, int64_t B, int C, int64_t ignore_index, float* part,
+                    float* out, hipStream_t st);
+void launch_loss_scale_grad(const float* g, const float* gout, const float* stats, int64_t n, float* out,
+                            hipStream_t st);
+void launch_nll_bwd(const int64_t* tgt, int64_t B, int C, int64_t ignore_index, const float* gout,
+                    const float* stats, float* out, hipStream_t st);
+void launch_mcrmse(const float* p, const float* t, int64_t B, int C, float* col, float* out, hipStream_t st);
 
 // ----------------------------------------------------------------------------
 // bf16 MFMA GEMM (gemm.hip): C[M,N] = alpha * op(A) . op(B) (+bias) (+epilogue)

@@ -234,11 +234,11 @@ class Trainer:
         if c == "cross_entropy":
             return L.CrossEntropyLoss()
         if c == "neg-loss":
-            return nn.NLLLoss()
+            return L.NLLLoss()
         if c == "l1":
-            return nn.L1Loss()
+            return L.L1Loss()
         if c == "l2":
-            return nn.MSELoss()
+            return L.MSELoss()
         if c == "custom":
             return _CustomLoss(custom_loss_function)
         if callable(c):
@@ -263,8 +263,7 @@ class Trainer:
     def _evaluate(self, outputs, targets):
         """Per-batch metric as a device tensor (reference returns a host float: B12 fix)."""
         if self.metric == "mcrmse":
-            colwise_mse = torch.mean(torch.square(targets - outputs), dim=0)
-            return torch.mean(torch.sqrt(colwise_mse), dim=0)
+            return L.mcrmse(outputs, targets)
         if self.metric == "accuracy":
             return L.accuracy(outputs, targets)
         return None

@@ -187,3 +187,17 @@ def test_cosine_per_batch(tmp_path):
     import math
     exp = 1e-7 + (1e-3 - 1e-7) * (1 + math.cos(math.pi * 0.5 / 5)) / 2
     assert t.optimizer.param_groups[0]["lr"] == pytest.approx(exp, rel=1e-6)
+
+
+def test_native_loss_modules_cpu_fallback():
+    """The native criteria keep torch semantics on CPU tensors (fallback path)."""
+    import torch.nn.functional as F
+    from ml_trainer_amd.ops.losses import L1Loss, MSELoss, NLLLoss, mcrmse
+    torch.manual_seed(0)
+    p, t = torch.randn(16, 4), torch.randn(16, 4)
+    assert torch.allclose(L1Loss()(p, t), F.l1_loss(p, t))
+    assert torch.allclose(MSELoss()(p, t), F.mse_loss(p, t))
+    lp, y = F.log_softmax(p, -1), torch.randint(0, 4, (16,))
+    assert torch.allclose(NLLLoss()(lp, y), F.nll_loss(lp, y))
+    ref = torch.mean(torch.sqrt(torch.mean(torch.square(t - p), dim=0)))
+    assert torch.allclose(mcrmse(p, t), ref)
