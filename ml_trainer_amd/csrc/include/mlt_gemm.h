@@ -2,6 +2,8 @@
 // gemm_tile.hip: 256-wide global_load_lds kernels with split-K): epilogue parameters and
 // the fused 4-column epilogue store.
 #pragma once
+#include <type_traits>
+
 #include "mlt_common.h"
 
 namespace mlt {
@@ -120,6 +122,107 @@ __device__ __forceinline__ void epilogue_store4(OutT* __restrict__ C, int64_t ld
         if (gn + q < N) hp[q] = f32_to_bf16(vv[q]);
     }
   }
+}
+
+
+// ---- prefetched epilogue side operands --------------------------------------------------------
+// A tile's epilogue stores IT float4 groups per lane per pass. When the runtime epilogue mode needs
+// a side operand (the dGELU pre-activation, a residual, or the fp32 accumulate target), loading it
+// next to each store costs one dependent HBM round trip per group (hipcc waits vmcnt(0) at every use
+// inside the mode branches). Instead the whole pass's side operands are loaded up front -- before
+// the pass's accumulator -> LDS round trip, so that latency is hidden behind it -- and consumed from
+// registers. kind: 0 = no side operand (plain epilogue_store4), 1 = one bf16 operand (aux in mode 2
+// XOR res), 2 = fp32 accumulate target; -1 = combination / alignment without a fast path.
+struct EpiSide {
+  const uint16_t* x = nullptr;
+  int64_t ldx = 0;
+  int kind = 0;
+};
+
+template <typename OutT>
+__device__ __forceinline__ EpiSide epi_side(const GemmEpi& epi, const OutT* C, int64_t ldc, int N, bool ext) {
+  EpiSide s;
+  if (ext) return s;
+  const bool dg = epi.mode == 2, rs = epi.res != nullptr;
+  if (dg && rs) {
+    s.kind = -1;
+  } else if (dg || rs) {
+    s.x = dg ? epi.aux : epi.res;
+    s.ldx = dg ? epi.ldaux : epi.ldres;
+    s.kind = 1;
+  }
+  if (sizeof(OutT) == 4 && epi.accumulate) s.kind = s.kind == 0 ? 2 : -1;
+  if (s.kind > 0) {
+    const bool ok = N % 4 == 0 && ldc % 4 == 0 && (((uintptr_t)C) & 15) == 0 &&
+                    (s.kind != 1 || (s.ldx % 4 == 0 && (((uintptr_t)s.x) & 7) == 0));
+    if (!ok) s.kind = -1;
+  }
+  return s;
+}
+
+// One epilogue pass of EIT float4 groups per lane with a side operand, for a tile that lies wholly
+// inside C (no range checks, no divergent branches: hipcc then counts the waits instead of
+// draining vmcnt at every group). The first H groups' operands are loaded before `stage()` (the
+// accumulator -> LDS round trip, barriers included); each later load re-fills the slot just
+// consumed. H = EIT for the 2-VGPR bf16 operands; HF for the 4-VGPR fp32 accumulate target, which
+// would otherwise spill kernels already at 256 VGPRs. `rc(it, gm, gn, off)` gives group it's
+// output coordinates and its float offset in the staged LDS image.
+enum { EPI_RES = 1, EPI_DGELU = 2, EPI_ACC = 3 };
+
+template <int KIND, typename OutT, int EIT, int HF, class RC, class STAGE>
+__device__ __forceinline__ void epi_pass_side(OutT* __restrict__ C, int64_t ldc, const EpiSide& s, const float* cs,
+                                              RC rc, STAGE stage) {
+  constexpr int H = KIND == EPI_ACC ? HF : (EIT >= 8 ? EIT / 2 : EIT);
+  using X = std::conditional_t<KIND == EPI_ACC, float4, ushort4>;
+  X x[H];
+  auto load = [&](int k, int it) __attribute__((always_inline)) {
+    int gm, gn, off;
+    rc(it, gm, gn, off);
+    if constexpr (KIND == EPI_ACC)
+      x[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + (int64_t)gm * ldc + gn);
+    else
+      x[k] = *reinterpret_cast<const ushort4*>(s.x + (int64_t)gm * s.ldx + gn);
+  };
+#pragma unroll
+  for (int it = 0; it < H; ++it) load(it, it);
+  stage();
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    int gm, gn, off;
+    rc(it, gm, gn, off);
+    const int k = it % H;
+    const float4 v = *reinterpret_cast<const float4*>(cs + off);
+    float vv[4] = {v.x, v.y, v.z, v.w};
+    OutT* cp = C + (int64_t)gm * ldc + gn;
+    if constexpr (KIND == EPI_ACC) {
+      const float4 o = x[k];
+      *reinterpret_cast<float4*>(cp) = make_float4(vv[0] + o.x, vv[1] + o.y, vv[2] + o.z, vv[3] + o.w);
+    } else {
+      const ushort4 a = x[k];
+      const float xv[4] = {bf16_to_f32(a.x), bf16_to_f32(a.y), bf16_to_f32(a.z), bf16_to_f32(a.w)};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = KIND == EPI_DGELU ? vv[q] * gelu_grad(xv[q]) : vv[q] + xv[q];
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<float4*>(cp) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      } else {
+        ushort4 o;
+        o.x = f32_to_bf16(vv[0]);
+        o.y = f32_to_bf16(vv[1]);
+        o.z = f32_to_bf16(vv[2]);
+        o.w = f32_to_bf16(vv[3]);
+        *reinterpret_cast<ushort4*>(cp) = o;
+      }
+    }
+    if (it + H < EIT) load(k, it + H);
+  }
+}
+
+// which side-operand pass a tile takes (0 = the general epilogue)
+template <typename OutT>
+__device__ __forceinline__ int epi_side_kind(const EpiSide& s, const GemmEpi& epi, bool interior) {
+  if (s.kind <= 0 || !interior) return 0;
+  if (s.kind == 1) return epi.mode == 2 ? EPI_DGELU : EPI_RES;
+  return sizeof(OutT) == 4 ? EPI_ACC : 0;
 }
 
 }  // namespace mlt

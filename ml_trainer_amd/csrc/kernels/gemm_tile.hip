@@ -287,8 +287,9 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
     const int gn = n0 + wn + 16 * j + cl;
     bv[j] = (epi.bias && gn < N && !ext) ? epi.bias[gn] : 0.f;
   }
-#pragma unroll
-  for (int h = 0; h < TI / RI; ++h) {
+  constexpr int EIT = EPR * WTN / 4 / 64;  // float4 groups per lane per pass
+  const EpiSide side = epi_side<OutT>(epi, C, ldc, N, ext);
+  auto stage_pass = [&](int h) __attribute__((always_inline)) {
     __syncthreads();  // LDS free (main loop / previous pass)
 #pragma unroll
     for (int ii = 0; ii < RI; ++ii)
@@ -298,8 +299,36 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
         for (int r = 0; r < 4; ++r)
           cs[(16 * ii + 4 * g + r) * EPS + 16 * j + cl] = acc[RI * h + ii][j][r] * alpha + bv[j];
     __syncthreads();
+  };
+  // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
+  const int sk = epi_side_kind<OutT>(side, epi, m0 + BM <= M && n0 + BN <= N);
+  constexpr int HF = WTN % 3 == 0 ? EIT / 3 : EIT / 2;
+#pragma unroll
+  for (int h = 0; h < TI / RI; ++h) {
+    auto rc = [&](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
+      const int e = it * 64 + lane, row = e / (WTN / 4), c4 = (e % (WTN / 4)) * 4;
+      gm = m0 + wm + EPR * h + row;
+      gn = n0 + wn + c4;
+      off = row * EPS + c4;
+    };
+    auto stg = [&]() __attribute__((always_inline)) { stage_pass(h); };
+    if (sk == EPI_RES) {
+      epi_pass_side<EPI_RES, OutT, EIT, HF>(C, ldc, side, cs, rc, stg);
+      continue;
+    }
+    if (sk == EPI_DGELU) {
+      epi_pass_side<EPI_DGELU, OutT, EIT, HF>(C, ldc, side, cs, rc, stg);
+      continue;
+    }
+    if constexpr (sizeof(OutT) == 4) {
+      if (sk == EPI_ACC) {
+        epi_pass_side<EPI_ACC, OutT, EIT, HF>(C, ldc, side, cs, rc, stg);
+        continue;
+      }
+    }
+    stage_pass(h);
 #pragma unroll 4
-    for (int it = 0; it < EPR * WTN / 4 / 64; ++it) {
+    for (int it = 0; it < EIT; ++it) {
       const int e = it * 64 + lane, row = e / (WTN / 4), c4 = (e % (WTN / 4)) * 4;
       const int gm = m0 + wm + EPR * h + row, gn = n0 + wn + c4;
       if (gm >= M || gn >= N) continue;
@@ -604,14 +633,15 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   float* const wsz = ws + (int64_t)blockIdx.y * M * N;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (64 * EPS);
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) {
-    const int qm = qd >> 1, qn = qd & 1;
-    const int gm0 = m0 + qm * 128 + wr * 64, gn0 = n0 + qn * 128 + wc * 32;
+  const EpiSide side = epi_side<OutT>(epi, C, ldc, N, ext);
+  // quadrant qd of the wave's output: rows gm0(qd) + 0..63, columns gn0(qd) + 0..31
+  auto q_gm0 = [&](int qd) __attribute__((always_inline)) { return m0 + (qd >> 1) * 128 + wr * 64; };
+  auto q_gn0 = [&](int qd) __attribute__((always_inline)) { return n0 + (qd & 1) * 128 + wc * 32; };
+  auto stage_q = [&](int qd) __attribute__((always_inline)) {
     float bv[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int gn = gn0 + 16 * j + cl;
+      const int gn = q_gn0(qd) + 16 * j + cl;
       bv[j] = (epi.bias && gn < N && !ext) ? epi.bias[gn] : 0.f;
     }
     __syncthreads();
@@ -620,8 +650,37 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cs[(16 * i + 4 * g + r) * EPS + 16 * j + cl] = acc[qd * 8 + i * 2 + j][r] * alpha + bv[j];
+        for (int r = 0; r < 4; ++r)
+          cs[(16 * i + 4 * g + r) * EPS + 16 * j + cl] = acc[qd * 8 + i * 2 + j][r] * alpha + bv[j];
     __syncthreads();
+  };
+  // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
+  const int sk = epi_side_kind<OutT>(side, epi, m0 + 256 <= M && n0 + 256 <= N);
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+    auto rc = [&](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
+      const int e = it * 64 + lane, row = e >> 3, c4 = (e & 7) * 4;
+      gm = q_gm0(qd) + row;
+      gn = q_gn0(qd) + c4;
+      off = row * EPS + c4;
+    };
+    auto stg = [&]() __attribute__((always_inline)) { stage_q(qd); };
+    if (sk == EPI_RES) {
+      epi_pass_side<EPI_RES, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
+      continue;
+    }
+    if (sk == EPI_DGELU) {
+      epi_pass_side<EPI_DGELU, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
+      continue;
+    }
+    if constexpr (sizeof(OutT) == 4) {
+      if (sk == EPI_ACC) {
+        epi_pass_side<EPI_ACC, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
+        continue;
+      }
+    }
+    stage_q(qd);
+    const int gm0 = q_gm0(qd), gn0 = q_gn0(qd);
 #pragma unroll 4
     for (int it = 0; it < 8; ++it) {
       const int e = it * 64 + lane, row = e >> 3, c4 = (e & 7) * 4;

@@ -112,6 +112,12 @@ def test_tile_kernels(dev, cfg, splits, a_mn, b_mn):
     acc = torch.ones(M, N, device=dev)
     C.gemm(A, B, acc, bool(a_mn), bool(b_mn), accumulate=True, cfg=cfg, splits=splits)
     torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-2)
+    # dGELU epilogue (interior tile takes the prefetched side-operand path, tails the general one)
+    pre = _mk((M, N), dev, g)
+    C.gemm(A, B, out, bool(a_mn), bool(b_mn), aux=pre, mode=2, cfg=cfg, splits=splits)
+    x = pre.float()
+    dg = 0.5 * (1 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+    torch.testing.assert_close(out.float(), ref * dg, rtol=2e-2, atol=0.15)
 
 
 def test_tile_split_k_deterministic(dev):
