@@ -709,16 +709,20 @@ namespace {
 constexpr int kCUs = 256;
 struct CfgDesc {
   int bm, bn;
-  double rate;  // sustained FLOP/s per CU (relative model, measured ordering)
-  int per_cu;   // resident blocks per CU
+  double rate;   // sustained FLOP/s per CU (relative model, measured ordering)
+  int per_cu;    // resident blocks per CU
+  double fixed;  // per-block fixed cost (prologue fill + epilogue), s
 };
 constexpr int kNumCfg = 6;
-const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2},
-                               {256, 256, 1.15e15 / kCUs, 1},
-                               {256, 128, 0.92e15 / kCUs, 1},
-                               {128, 256, 0.92e15 / kCUs, 1},
-                               {256, 192, 1.05e15 / kCUs, 1},
-                               {256, 256, 1.15e15 / kCUs, 1}};  // 5: ping-pong (rate calibrated below)
+// cfg 5 (ping-pong) fitted to the 64K-token BERT shapes (profiles/gemm_bf16_64k_tokens.jsonl):
+// 5 % slower than cfg 1 at K = 768 (12 K-steps: its deeper pipeline fill does not amortise),
+// 8-10 % faster at K = 2304-3072 -> a faster steady state with a larger fixed cost.
+const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2, 1.0e-6},
+                               {256, 256, 1.15e15 / kCUs, 1, 1.0e-6},
+                               {256, 128, 0.92e15 / kCUs, 1, 1.0e-6},
+                               {128, 256, 0.92e15 / kCUs, 1, 1.0e-6},
+                               {256, 192, 1.05e15 / kCUs, 1, 1.0e-6},
+                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6}};  // 5: ping-pong
 
 // split-K combine override: -1 planner, 0 in-kernel, 1 external (env MLT_GEMM_SPLIT_EXT, or
 // set_gemm_split_mode() from tests / benchmarks)
@@ -754,13 +758,14 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
   const int64_t slots = (int64_t)kCUs * c.per_cu;
   const int64_t rounds = (blocks + slots - 1) / slots;
   const int nk = (K + kstep - 1) / kstep, ks = (nk + splits - 1) / splits;
-  const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + 1.0e-6;
+  const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + c.fixed;
   double t = rounds * t_block;
   if (splits > 1) t += split_cost(cfg, splits, M, N, nullptr);
   return t;
 }
 
-GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy) {
+GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
+                    bool allow_pp = true) {
   GemmPlan p{0, 1, 0, 0, 0};
   const bool big_ok = K % kstep == 0 && K >= kstep && M >= 64 && N >= 64;
   const double speed = kstep == 128 ? 1.8 : 1.0;
@@ -773,6 +778,7 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
     const int nk = K / kstep;
     for (int cfg = 1; cfg < kNumCfg; ++cfg)
       for (int s = 1; s <= 16; ++s) {
+        if (cfg == 5 && !allow_pp) break;
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
         if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
@@ -910,9 +916,10 @@ void launch_split_reduce(const GemmPlan& p, const float* ws, OutT* C, int M, int
 void set_gemm_split_mode(int mode) { g_split_mode = mode; }
 
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
-  (void)a_mn;
   (void)b_mn;
-  return plan_tiles(M, N, K, force_cfg, force_splits, 64, true);
+  // the ping-pong kernel's fit covers the k-contiguous-A (forward / dgrad) shapes; weight
+  // gradients (A = dY^T, mn-contiguous) stay on the 256-wide tiles with split-K
+  return plan_tiles(M, N, K, force_cfg, force_splits, 64, true, a_mn == 0);
 }
 
 GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {
