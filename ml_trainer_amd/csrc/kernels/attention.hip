@@ -915,6 +915,144 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Forward, ring-staged (opt-in, MLT_ATTN_FWD_RING=3|4): kRing-1 K/V blocks in flight through
+// LDS-DMA (glds) into a ring of stages (counted vmcnt + raw barrier, one __shared__ array, V^T
+// through the asm transpose read), like the backward ring kernels, instead of the register-staged
+// forward's one block ahead. Same arithmetic and order as attn_fwd_kernel: bit-identical outputs.
+// Measured slower than the register-staged forward on BERT shapes (see launch_attn_fwd), so
+// not the default.
+// ---------------------------------------------------------------------------
+template <int NQ, int kRing>
+__global__ __launch_bounds__(256) void attn_fwd_ring_kernel(const uint16_t* __restrict__ qkv,
+                                                            uint16_t* __restrict__ out, float* __restrict__ lse,
+                                                            const int* __restrict__ lens, int S, int H,
+                                                            float scale) {
+  constexpr int STAGE = 2 * kTile;  // K tile, V tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
+  int qb, h, b;
+  block_coords(S, 64 * NQ, H, qb, h, b);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int D = H * AH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t base = (int64_t)b * S;
+  const int len = lens ? lens[b] : S;
+  int q[NQ];
+  bf16x8 qf[NQ][2];
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+      qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
+                           : bf16x8{};
+  }
+  const int nkb = (len + AB - 1) / AB;
+  // stage = 4 glds per thread: 2 (K) + 2 (V); rows past the valid keys re-read the last valid
+  // row (finite values whose probabilities are exactly 0 after the key mask)
+  auto issue = [&](int slot, int kb) {
+    uint8_t* st = smem + slot * STAGE;
+    const int k0 = kb * AB, nv = min(AB, S - k0);
+    glds_tile(st, qkv, ld, base + k0, nv, D + h * AH);
+    glds_tile(st + kTile, qkv, ld, base + k0, nv, 2 * D + h * AH);
+  };
+#pragma unroll
+  for (int s0 = 0; s0 < kRing - 1; ++s0)
+    if (s0 < nkb) issue(s0, s0);
+  f32x4 o[NQ][4];
+  float m[NQ], l[NQ];
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    m[n] = -INFINITY;
+    l[n] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float sl2 = scale * 1.4426950408889634f;
+  for (int kb = 0; kb < nkb; ++kb) {
+    ring_wait4(min(kRing - 2, nkb - 1 - kb));
+    raw_barrier();  // stage kb visible to all waves; everyone is done with slot (kb - 1) % kRing
+    if (kb + kRing - 1 < nkb) issue((kb + kRing - 1) % kRing, kb + kRing - 1);
+    const uint8_t* Ks = smem + (kb % kRing) * STAGE;
+    const uint8_t* Vs = Ks + kTile;
+    f32x4 s[NQ][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) s[n][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const bf16x8 kfr = frag_row(Ks, kt * 16, kh);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) s[n][kt] = mfma(kfr, qf[n][kh], s[n][kt]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+      float bm = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * AB + kt * 16 + 4 * g + r;
+          const float v = key < len ? s[n][kt][r] * sl2 : -INFINITY;
+          s[n][kt][r] = v;
+          bm = fmaxf(bm, v);
+        }
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m[n], bm);
+      const float alpha = fast_exp2(m[n] - mn);
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(s[n][kt][r] - mn);
+          s[n][kt][r] = pv;
+          ps += pv;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l[n] = l[n] * alpha + ps;
+      m[n] = mn;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[n][d] *= alpha;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pb[NQ];
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) pb[n] = pack_acc(s[n][2 * ks], s[n][2 * ks + 1]);
+      bf16x8 va[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) va[d] = frag_tr_asm(Vs, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+      frag_tr_wait(va);
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) o[n][d] = mfma(va[d], pb[n], o[n][d]);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    if (q[n] < S) {
+      const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
+      uint16_t* op = out + (base + q[n]) * (int64_t)D + h * AH;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        ushort4 u;
+        u.x = f32_to_bf16(o[n][d][0] * inv);
+        u.y = f32_to_bf16(o[n][d][1] * inv);
+        u.z = f32_to_bf16(o[n][d][2] * inv);
+        u.w = f32_to_bf16(o[n][d][3] * inv);
+        *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
+      }
+      if (g == 0) lse[((int64_t)b * H + h) * S + q[n]] = m[n] + __log2f(l[n]);
+    }
+  }
+}
+
 // 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
 // MLT_ATTN_FWD_GROUPS / MLT_ATTN_DKDV_GROUPS / MLT_ATTN_DQ_GROUPS = 1|2 override the choice
 // Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dK/dV 1 group (2 groups need
@@ -929,7 +1067,27 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* 
                      float scale, hipStream_t st) {
   if (B <= 0 || S <= 0) return;
   const unsigned g2 = (unsigned)((S + 127) / 128 * H * B), g1 = (unsigned)((S + 63) / 64 * H * B);
-  if (attn_groups("MLT_ATTN_FWD_GROUPS", S, 1) == 2)
+  // MLT_ATTN_FWD_RING: 0 = register-staged kernel (default), 3 / 4 = ring depth. Measured
+  // (B32 / B128, S512, H12): ring 3 is 4-5 % slower, ring 4 12-18 % slower -- the forward is not
+  // bound by its one-block-ahead K/V loads but by occupancy (48 / 64 KB of LDS per block vs 32).
+  const char* rv = getenv("MLT_ATTN_FWD_RING");
+  const int ring = rv ? atoi(rv) : 0;
+  const bool two = attn_groups("MLT_ATTN_FWD_GROUPS", S, 1) == 2;
+  if (ring == 3 || ring == 4) {
+    if (ring == 3) {
+      if (two)
+        hipLaunchKernelGGL((attn_fwd_ring_kernel<2, 3>), dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+      else
+        hipLaunchKernelGGL((attn_fwd_ring_kernel<1, 3>), dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+    } else {
+      if (two)
+        hipLaunchKernelGGL((attn_fwd_ring_kernel<2, 4>), dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+      else
+        hipLaunchKernelGGL((attn_fwd_ring_kernel<1, 4>), dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+    }
+    return;
+  }
+  if (two)
     hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);

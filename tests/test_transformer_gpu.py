@@ -350,3 +350,27 @@ def test_attention_bwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
             res[ring, grp] = dqkv
     for grp in ("1", "2"):
         assert torch.equal(res["0", grp], res["3", grp]) and torch.equal(res["0", grp], res["4", grp])
+
+
+@pytest.mark.parametrize("B,S,H,use_lens", [(2, 512, 3, False), (3, 200, 2, True), (2, 64, 1, False)])
+def test_attention_fwd_ring_matches_register_staged(dev, B, S, H, use_lens, monkeypatch):
+    """The glds ring-staged forward (MLT_ATTN_FWD_RING) keeps the register-staged forward's
+    arithmetic and order: bit-identical O and LSE, including tails and key masks."""
+    C = require_native()
+    g = torch.Generator().manual_seed(7 * S + H)
+    D = H * 64
+    qkv = _bf((B * S, 3 * D), g, 1.0)
+    lens = None
+    if use_lens:
+        lens = torch.randint(1, S + 1, (B,), generator=g).to(torch.int32).to(dev)
+    res = {}
+    for ring in ("0", "3", "4"):
+        monkeypatch.setenv("MLT_ATTN_FWD_RING", ring)
+        for grp in ("1", "2"):
+            monkeypatch.setenv("MLT_ATTN_FWD_GROUPS", grp)
+            out = torch.full((B * S, D), float("nan"), dtype=torch.bfloat16, device=dev)
+            lse = torch.full((B * H * S,), float("nan"), device=dev)
+            C.attn_fwd(qkv, out, lse, lens, B, S, H, 0.125)
+            res[ring, grp] = (out, lse)
+    for key, (o, l) in res.items():
+        assert torch.equal(o, res["0", key[1]][0]) and torch.equal(l, res["0", key[1]][1]), key
