@@ -793,7 +793,7 @@ class LeNetEngine {
     P_.dh1 = fp("dh1", B * F1);
     P_.dflat = fp("dflat", B * FLAT);
     P_.g1 = fp("g1", B * C1 * 196);
-    P_.slab1 = fp("slab1", B * C1 * 128);
+    P_.slab1 = fp("slab1", B * C1 * 640);  // kSlabStride floats per (sample, channel)
     P_.i1 = get("i1", at::kByte, B * C1 * 196).data_ptr<uint8_t>();
     P_.i2 = get("i2", at::kByte, B * FLAT).data_ptr<uint8_t>();
     P_.targets = get("targets", at::kLong, B).data_ptr<int64_t>();

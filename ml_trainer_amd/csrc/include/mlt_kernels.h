@@ -31,6 +31,8 @@ enum LeNetMode : int {
   LENET_OPT = 8,        // fused optimizer update inside the weight-gradient kernel (single process only)
   LENET_REDUCE = 16,    // (kept for API compatibility: the conv1 reduction always happens inside K5)
   LENET_TRACE = 256,    // fused kernel: block 0 stores per-phase clock64() stamps into slab1 (K5 skipped)
+  LENET_SKIP_CONV1 = 512, LENET_SKIP_CONV2 = 1024, LENET_SKIP_FC = 2048,  // K5 roles skipped (profiling)
+  LENET_K4WG = 4096,    // internal: K4 wrote the conv wgrad slabs, K5 only reduces them
 };
 
 struct LeNetPtrs {

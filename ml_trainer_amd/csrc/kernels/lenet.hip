@@ -10,9 +10,12 @@
 //   K1 conv1_fwd   grid (B, C1)     [augment (RandomCrop+HFlip+Normalize) fused] conv5x5+bias+ReLU+maxpool2
 //   K2 conv2_fwd   grid (B, C2/4)   conv5x5+bias+ReLU+maxpool2 -> flatten (c*25+h*5+w, src/model.py:20)
 //   K3 fc          grid (B)         fc1/fc2/fc3 (+ReLU) -> softmax-CE + accuracy -> fc dgrad chain
-//   K4 conv2_dgrad grid (B, C1)     unpool2 -> conv2 dgrad -> ReLU/unpool1 mask
-//   K5 wgrad       role-split grid  conv1/conv2/fc1..fc3 wgrad+bias + fused optimizer update + step counters
-//                  (conv1 partials reduced in-launch by the last-arriving block of each channel)
+//   K4 conv2_dgrad grid (B, 2*C1)   unpool2 -> conv2 dgrad -> ReLU/unpool1 mask -> the sample's conv1
+//                                   wgrad slab (blocks y < C1); the sample's conv2 wgrad slab (y >= C1)
+//   K5 wgrad       role-split grid  batch sums of the conv wgrad slabs (sample order), fc1..fc3 wgrad
+//                  +bias, fused optimizer update, step counters
+//                  (the fused KF path keeps the K5 conv roles: conv1 partials reduced in-launch
+//                  by the last-arriving block of each channel)
 //
 // ReLU+maxpool are fused: pool(relu(c)) = relu(max(c)); the gradient reaches the
 // first arg-max of the window only when that max is > 0 (torch's threshold_backward
@@ -38,7 +41,10 @@ using LeNetDefault = LeNetDims<6, 16, 120, 84, 10>;
 using LeNetTiny = LeNetDims<4, 8, 64, 32, 10>;
 
 constexpr int kTaps1 = 76;        // conv1 wgrad partial: 75 taps + bias
-constexpr int kSlabStride = 128;  // floats per (sample group, oc) slab: 512 B, so no two writers share a cache line
+// floats per (sample, channel) slab: [0, 76) conv1 wgrad partial, [128, 128 + C2*25 + C2) conv2
+// wgrad partial (K4 path); 2.5 KB, so no two writers share a cache line
+constexpr int kSlabStride = 640;
+constexpr int kSlab2Off = 128;
 constexpr int kSpb1 = 1;          // samples per conv1-wgrad block (slabs per oc = ceil(B / kSpb1)); 4 measured slower
 
 // ---------------------------------------------------------------------------
@@ -448,15 +454,47 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
 // Block (256 = 4 waves) per (sample, input channel); lane = 2x2 output patch of the
 // 14x14 map, wave = quarter of the conv2 output channels (reduced through LDS in order).
 // ---------------------------------------------------------------------------
-template <class D>
+//
+// WG (the engine / autograd path): the conv weight gradients move here from K5. Everything they
+// need per sample is at hand -- the masked conv1-output grad this kernel produces, the dense
+// conv2-output grad image `dc` every block rebuilds from dflat, x[b] and p1[b, ic] -- so the grid
+// gets a second half: blocks (b, ic) also reduce their sample's conv1 wgrad (oc = ic) after the
+// dgrad, blocks (b, C1 + ic) compute the sample's conv2 wgrad for input channel ic instead of a
+// dgrad. Both store per-(sample, channel) slabs; K5 only sums B slabs per weight in sample order.
+// (The conv wgrads were K5's two longest roles: 11.5 / 9.2 us of a 12.8 us kernel.)
+// ---------------------------------------------------------------------------
+template <class D, bool WG>
 __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict__ dflat,
                                                          const uint8_t* __restrict__ i2,
                                                          const float* __restrict__ w2,
-                                                         const uint8_t* __restrict__ i1, float* __restrict__ g1) {
+                                                         const uint8_t* __restrict__ i1, float* __restrict__ g1,
+                                                         const float* __restrict__ x, const float* __restrict__ p1,
+                                                         float* __restrict__ slab) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, NZ4 = C2 * 81, NS = (FLAT + 255) / 256;
-  const int b = blockIdx.x, ic = blockIdx.y, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  constexpr int W2N = C2 * 25 + C2;  // conv2 wgrad outputs of one input channel (+ the biases)
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool w2role = WG && (int)blockIdx.y >= C1;
+  const int ic = w2role ? (int)blockIdx.y - C1 : (int)blockIdx.y;
   __shared__ __attribute__((aligned(16))) float dc[C2 * 324];  // zero-padded dense conv2-output grad [C2][18][18]
   __shared__ __attribute__((aligned(16))) float4 red[4][64];
+  // WG staging: x[b] [3][32][32] | p1[b, ic] rows padded to 16 (aliased: one role each), the
+  // conv1-grad cells with their input offsets, the conv2 partials of 3 row groups
+  __shared__ __attribute__((aligned(16))) float wx[WG ? 3 * 32 * 37 : 4];
+  __shared__ float wg1[WG ? 196 : 1];
+  __shared__ int wpos[WG ? 196 : 1];
+  __shared__ float wred[WG ? 3 * W2N : 1];
+  float4 xv[3];
+  float pv[4];
+  if constexpr (WG) {  // issued first: in flight across the dgrad / dc build below
+    if (!w2role) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xv[i] = reinterpret_cast<const float4*>(x + (int64_t)b * 3072)[t + 256 * i];
+    } else if (t < 49) {
+      const float* src = p1 + ((int64_t)b * C1 + ic) * 196 + 4 * t;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pv[q] = src[q];
+    }
+  }
   int kk[NS];
   float gg[NS];
 #pragma unroll
@@ -476,6 +514,49 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
       const int o = e / 25, p = e - o * 25;
       const int cy = 2 * (p / 5) + (k >> 1), cx = 2 * (p % 5) + (k & 1);
       dc[o * 324 + (cy + 4) * 18 + cx + 4] = gg[i];
+    }
+  }
+  if constexpr (WG) {
+    if (w2role) {
+      // conv2 wgrad of sample b, input channel ic: thread (oc, kh, row group) slides a 5-wide p1
+      // window along x; kh == 0 threads also sum dc (the conv2 bias gradient, stored by ic == 0)
+      float* wp = wx;  // [14][16]
+      if (t < 49) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = 4 * t + q, r = e / 14;
+          wp[r * 16 + e - r * 14] = pv[q];
+        }
+      }
+      __syncthreads();
+      float a2[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, ab = 0.f;
+      const int o2 = t % (C2 * 5), yg = t / (C2 * 5), oc = o2 / 5, kh = o2 - oc * 5;
+      if (yg < 3) {
+        const int y0 = yg == 0 ? 0 : 1 + 3 * yg, y1 = 4 + 3 * yg;  // rows 0-3, 4-6, 7-9
+#pragma unroll 1
+        for (int y = y0; y < y1; ++y) {
+          const float* dr = dc + oc * 324 + (y + 4) * 18 + 4;
+          const float* pr = wp + (y + kh) * 16;
+          float win[14];
+#pragma unroll
+          for (int q = 0; q < 14; ++q) win[q] = pr[q];
+#pragma unroll
+          for (int xx = 0; xx < 10; ++xx) {
+            const float dv = dr[xx];
+            ab += dv;
+#pragma unroll
+            for (int kw = 0; kw < 5; ++kw) a2[kw] = fmaf(dv, win[xx + kw], a2[kw]);
+          }
+        }
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) wred[yg * W2N + oc * 25 + kh * 5 + kw] = a2[kw];
+        if (kh == 0) wred[yg * W2N + C2 * 25 + oc] = ab;
+      }
+      __syncthreads();
+      float* slb = slab + ((int64_t)b * C1 + ic) * kSlabStride + kSlab2Off;
+      for (int e = t; e < C2 * 25 + (ic == 0 ? C2 : 0); e += 256)
+        slb[e] = (wred[e] + wred[W2N + e]) + wred[2 * W2N + e];
+      return;
     }
   }
   __syncthreads();
@@ -528,10 +609,58 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
     }
     const int by = t / 7, bx = t - by * 7, y0 = 2 * by, x0 = 2 * bx;
     const int64_t base = ((int64_t)(b * C1 + ic) * 14 + y0) * 14 + x0;
-    g1[base] = i1[base] < 4 ? s.x : 0.f;
-    g1[base + 1] = i1[base + 1] < 4 ? s.y : 0.f;
-    g1[base + 14] = i1[base + 14] < 4 ? s.z : 0.f;
-    g1[base + 15] = i1[base + 15] < 4 ? s.w : 0.f;
+    const int k00 = i1[base], k01 = i1[base + 1], k10 = i1[base + 14], k11 = i1[base + 15];
+    const float v00 = k00 < 4 ? s.x : 0.f, v01 = k01 < 4 ? s.y : 0.f, v10 = k10 < 4 ? s.z : 0.f,
+                v11 = k11 < 4 ? s.w : 0.f;
+    g1[base] = v00;
+    g1[base + 1] = v01;
+    g1[base + 14] = v10;
+    g1[base + 15] = v11;
+    if constexpr (WG) {  // conv1-output grad cell c -> (value, offset of its arg-max in a 32x32 plane)
+      const int cells[4] = {y0 * 14 + x0, y0 * 14 + x0 + 1, (y0 + 1) * 14 + x0, (y0 + 1) * 14 + x0 + 1};
+      const int ks[4] = {k00, k01, k10, k11};
+      const float vs[4] = {v00, v01, v10, v11};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = cells[q], k = ks[q] < 4 ? ks[q] : 0, py = c / 14, px = c - py * 14;
+        wg1[c] = vs[q];
+        wpos[c] = (2 * py + (k >> 1)) * 37 + 2 * px + (k & 1);  // row stride of the staged x (XR below)
+      }
+    }
+  }
+  if constexpr (WG) {
+    // conv1 wgrad of sample b, output channel ic: dW1[ic, c, kh, kw] (+ bias) over the 196 pooled
+    // cells in 3 slices (lane = tap: the cell's grad / offset are LDS broadcasts). x[b] is staged
+    // with a 37-float row stride so the 5 kh rows of a tap window fall in disjoint bank ranges
+    // (with 32 they alias every 2 rows: 9-way conflicts).
+    constexpr int XR = 37, XC = 32 * XR;  // (wpos above is built with the same 37)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = 4 * (t + 256 * i), c = e >> 10, r = (e >> 5) & 31, col = e & 31;
+      float* d = wx + c * XC + r * XR + col;
+      d[0] = xv[i].x;
+      d[1] = xv[i].y;
+      d[2] = xv[i].z;
+      d[3] = xv[i].w;
+    }
+    __syncthreads();
+    float acc = 0.f;
+    const int tap = t % kTaps1, sl = t / kTaps1;
+    if (sl < 3) {
+      if (tap < 75) {
+        const int c = tap / 25, kh = (tap % 25) / 5, kw = tap % 5;
+        const float* xc = wx + c * XC + kh * XR + kw;
+#pragma unroll 7
+        for (int e = sl; e < 196; e += 3) acc = fmaf(wg1[e], xc[wpos[e]], acc);
+      } else {
+#pragma unroll 7
+        for (int e = sl; e < 196; e += 3) acc += wg1[e];
+      }
+    }
+    float* r1 = reinterpret_cast<float*>(red);
+    if (sl < 3) r1[sl * kTaps1 + tap] = acc;
+    __syncthreads();
+    if (t < kTaps1) slab[((int64_t)b * C1 + ic) * kSlabStride + t] = r1[t] + r1[kTaps1 + t] + r1[2 * kTaps1 + t];
   }
 }
 
@@ -999,7 +1128,7 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
   __shared__ __attribute__((aligned(16))) float lds[kSpb1 * (3072 + 2 * 196) + 3 * kTaps1 + 4 > 8192
                                                         ? kSpb1 * (3072 + 2 * 196) + 3 * kTaps1 + 4
                                                         : 8192];
-  const int nA = (B + kSpb1 - 1) / kSpb1 * C1, nblk = nA + C2 * C1 + NB3 + NB4 + NB5;
+  const int nA = (B + kSpb1 - 1) / kSpb1 * C1;
   int blk = blockIdx.x;
   const int t = threadIdx.x;
   // The step counters are read by every block here and advanced by the last block of the launch.
@@ -1012,7 +1141,49 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     oc.t = (float)(step + 1);
     if (O.lr_ptr) oc.lr = O.lr_ptr[O.lr_table ? sie : 0];
   }
-  if (blk < nA) {
+  // K4WG: K4 left per-(sample, channel) conv wgrad slabs; the conv roles only reduce them over
+  // the batch in sample order (one output per thread) -- the fc roles keep their block ids
+  constexpr int NR1 = (C1 * kTaps1 + 255) / 256, NR2 = (C2 * C1 * 25 + C2 + 255) / 256;
+  if (mode & LENET_K4WG) {
+    if (blk < NR1 + NR2) {
+      const bool c1r = blk < NR1;
+      const int o = (c1r ? blk : blk - NR1) * 256 + t;
+      const int nout = c1r ? C1 * kTaps1 : C2 * C1 * 25 + C2;
+      if (o < nout) {
+        int64_t src, dst;
+        if (c1r) {
+          const int ocn = o / kTaps1, tap = o - ocn * kTaps1;
+          src = (int64_t)ocn * kSlabStride + tap;
+          dst = tap < 75 ? O.off[0] + ocn * 75 + tap : O.off[1] + ocn;
+        } else if (o < C2 * C1 * 25) {
+          const int ocn = o / (C1 * 25), icn = (o / 25) % C1, tap = o % 25;
+          src = (int64_t)icn * kSlabStride + kSlab2Off + ocn * 25 + tap;
+          dst = O.off[2] + o;
+        } else {
+          src = kSlab2Off + C2 * 25 + (o - C2 * C1 * 25);  // ic == 0 slabs hold the bias sums
+          dst = O.off[3] + (o - C2 * C1 * 25);
+        }
+        const Opt1 pst = opt_prefetch1(O, oc, dst);
+        const int64_t sstride = (int64_t)C1 * kSlabStride;
+        float g = 0.f;
+        for (int b0 = 0; b0 < B; b0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = b0 + u < B ? P.slab1[(b0 + u) * sstride + src] : 0.f;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) g += v[u];
+        }
+        apply_pre1(O, oc, dst, g, pst);
+      }
+      blk = -1;  // done: skip the role dispatch below
+    } else {
+      blk = blk - NR1 - NR2 + nA + C2 * C1;  // fc roles
+    }
+  }
+  // LENET_SKIP_* (profiling only, MLT_LENET_WGRAD_SKIP): drop a role to time the others
+  const int role = blk < nA ? 0 : (blk < nA + C2 * C1 ? 1 : 2);
+  if (blk < 0 || ((mode >> (9 + role)) & 1)) {
+  } else if (blk < nA) {
     // conv1: dW1[oc, ic, kh, kw] partial over kSpb1 samples x 196 pooled cells.
     const int bg = blk / C1, ocn = blk - bg * C1, nbg = (B + kSpb1 - 1) / kSpb1;
     const Opt1 pst = t < kTaps1 ? opt_prefetch1(O, oc, t < 75 ? O.off[0] + ocn * 75 + t : O.off[1] + ocn) : Opt1{};
@@ -1195,7 +1366,7 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
     if (t == 0) {
       const unsigned prev =
           __hip_atomic_fetch_add(&P.counters[C1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (unsigned)(nblk - 1)) {
+      if (prev == gridDim.x - 1) {
         ctrl[0] += 1;
         ctrl[1] += 1;
         __hip_atomic_store(&P.counters[C1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1229,13 +1400,23 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     if (mode & (LENET_FWD | LENET_CE | LENET_BWD))
       hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
     if (mode & LENET_BWD)
-      hipLaunchKernelGGL(lenet_conv2_dgrad<D>, dim3(B, D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2, P.i1, P.g1);
+      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, 2 * D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2,
+                         P.i1, P.g1, P.x, P.p1, P.slab1);
   }
   if ((mode & LENET_BWD) && !(fused && (mode & LENET_TRACE))) {
     constexpr int NB3 = (D::F1 * (D::FLAT / 4) + 255) / 256, NB4 = (D::F2 * (D::F1 / 4) + 255) / 256,
                   NB5 = (D::NC * (D::F2 / 4) + 255) / 256;
-    const int nblk = (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
-    hipLaunchKernelGGL(lenet_wgrad<D>, dim3(nblk), dim3(256), 0, st, mode, P, O, B, A.ctrl);
+    // non-fused path: K4 already produced the conv wgrad slabs (K4WG); the fused KF does not
+    const int k4wg = fused ? 0 : LENET_K4WG;
+    constexpr int NR1 = (D::C1 * kTaps1 + 255) / 256, NR2 = (D::C2 * D::C1 * 25 + D::C2 + 255) / 256;
+    const int nblk = k4wg ? NR1 + NR2 + NB3 + NB4 + NB5
+                          : (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
+    // MLT_LENET_WGRAD_SKIP=<mask> (profiling only): 1 conv1 / 2 conv2 / 4 fc roles return at once
+    static const int skip = [] {
+      const char* v = getenv("MLT_LENET_WGRAD_SKIP");
+      return v ? (atoi(v) & 7) : 0;
+    }();
+    hipLaunchKernelGGL(lenet_wgrad<D>, dim3(nblk), dim3(256), 0, st, mode | (skip << 9) | k4wg, P, O, B, A.ctrl);
   }
 }
 

@@ -97,7 +97,7 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         "dh1": torch.empty(B * f1, **f32),
         "dflat": torch.empty(B * flat, **f32),
         "g1": torch.empty(B * c1 * 196, **f32),
-        "slab1": torch.empty(B * c1 * 128, **f32),  # 512 B per (sample, channel): line-disjoint
+        "slab1": torch.empty(B * c1 * 640, **f32),  # conv wgrad slabs, 2.5 KB per (sample, channel)
         "i1": torch.empty(_align4(B * c1 * 196), dtype=torch.uint8, device=device),
         "i2": torch.empty(_align4(B * flat), dtype=torch.uint8, device=device),
         "targets": torch.zeros(B, dtype=torch.int64, device=device),
