@@ -33,6 +33,7 @@ enum LeNetMode : int {
   LENET_TRACE = 256,    // fused kernel: block 0 stores per-phase clock64() stamps into slab1 (K5 skipped)
   LENET_SKIP_CONV1 = 512, LENET_SKIP_CONV2 = 1024, LENET_SKIP_FC = 2048,  // K5 roles skipped (profiling)
   LENET_K4WG = 4096,    // internal: K4 wrote the conv wgrad slabs, K5 only reduces them
+  LENET_FROM_P1 = 8192, // internal: the per-sample kernel starts from p1 (conv2 -> fc chain) and stops there
 };
 
 struct LeNetPtrs {

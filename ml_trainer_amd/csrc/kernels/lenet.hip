@@ -737,6 +737,11 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
   using S = typename FusedLds<D>::S;
   const int b = blockIdx.x, t = threadIdx.x, wid = t >> 6;
   const bool fwd = (mode & LENET_FWD) != 0, bwd = (mode & LENET_BWD) != 0;
+  // LENET_FROM_P1 (the default engine path): K1 already ran augment + conv1 for the whole batch;
+  // this kernel starts from p1 in global (conv2 -> fc chain -> CE -> fc dgrad) and stops there
+  // (K4 does unpool2 / conv2 dgrad / the conv wgrads): K2 + K3 as one launch, with fc1's weights
+  // streaming into registers while conv2 computes.
+  const bool from_p1 = (mode & LENET_FROM_P1) != 0;
   __shared__ __attribute__((aligned(16))) FusedLds<D> L;
   float* xs = L.u;
   uint4* rawimg = reinterpret_cast<uint4*>(L.u + FusedLds<D>::XS);
@@ -777,7 +782,11 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
   uint4 raw = make_uint4(0u, 0u, 0u, 0u);
   float4 xin = make_float4(0.f, 0.f, 0.f, 0.f);
   uint8_t i1r[2] = {0, 0}, i2r = 0;
-  if (fwd) {
+  float p1r[2] = {0.f, 0.f};
+  if (fwd && from_p1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) p1r[j] = P.p1[(int64_t)b * C1 * 196 + min(t + j * NT, C1 * 196 - 1)];
+  } else if (fwd) {
     if (aug.data) {
       const int64_t step = aug.ctrl[0], sie = aug.ctrl[1];
       int64_t pos = sie * aug.batch_stride + b;
@@ -799,7 +808,7 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
     i2r = P.i2[(int64_t)b * FLAT + min(t, FLAT - 1)];
   }
   int64_t tgt_pre = 0;
-  if (mode & LENET_CE) tgt_pre = (fwd && aug.data) ? P.dtargets[idx] : P.targets[b];
+  if (mode & LENET_CE) tgt_pre = (fwd && aug.data && !from_p1) ? P.dtargets[idx] : P.targets[b];
   if constexpr (S::L1::LDS_FLOATS > 0) {  // fc1 rows beyond the register budget: LDS-DMA, no VGPRs
     constexpr int CH = S::L1::LDS_FLOATS / 4;  // 16-byte chunks
     const float* src = P.w3 + S::L1::LROW0 * FLAT;
@@ -818,7 +827,16 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
     if (t + j * NT < C2 * C1 * 25) L.w2[t + j * NT] = w2r[j];
   if (t < C1) L.b1[t] = b1r;
   if (t < C2) L.b2[t] = b2r;
-  if (fwd) {
+  if (fwd && from_p1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = t + j * NT;
+      if (e < C1 * 196) {
+        const int ic = e / 196, r = e - ic * 196, y = r / 14;
+        L.p1[(ic * 14 + y) * kP1s + r - y * 14] = p1r[j];
+      }
+    }
+  } else if (fwd) {
     if (aug.data) {
       if (t < 192) rawimg[t] = raw;
     } else if (t < 768) {  // [3*32 rows][8 float4] -> padded rows
@@ -833,7 +851,7 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
 
   stamp(1);
   // ---- phase 1: RandomCrop(pad) + HFlip + Normalize from the staged uint8 image
-  if (fwd && aug.data) {
+  if (fwd && aug.data && !from_p1) {
     const uint8_t* img = reinterpret_cast<const uint8_t*>(rawimg);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -854,7 +872,7 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
   stamp(2);
   // ---- phase 2: conv1 + bias + ReLU + maxpool2. Thread = (oc, pooled row, 2 pooled columns):
   // a 2x4 conv-output strip, input rows read as 2 x b128.
-  if (fwd && t < C1 * 98) {
+  if (fwd && !from_p1 && t < C1 * 98) {
     const int oc = t / 98, rem = t - oc * 98, py = rem / 7, pxg = rem - py * 7, y0 = 2 * py, x0 = 4 * pxg;
     const float bias = L.b1[oc];
     float acc[2][4];
@@ -895,7 +913,7 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
     P.i1[(int64_t)b * C1 * 196 + o] = iv[0];
     P.i1[(int64_t)b * C1 * 196 + o + 1] = iv[1];
   }
-  if (fwd) __syncthreads();
+  if (fwd && !from_p1) __syncthreads();
 
   stamp(3);
   // ---- phase 3: conv2 + bias + ReLU + maxpool2 -> flatten. Quad = (oc, pooled row), lane bit 0 =
@@ -953,7 +971,7 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
   stamp(4);
   // ---- phase 4: fc chain + CE (+ fc dgrad -> dflat); scratch aliases the (dead) image
   fc_chain<D, NT, kFusedFc1Regs>(mode, P, b, tgt_pre, inv_B, l1, l2, l3, L.f, L.s, L.u, L.df);
-  if (!bwd) return;
+  if (!bwd || from_p1) return;
 
   stamp(5);
   // ---- phase 5: unpool2 -> dense zero-padded conv2-output grad (aliases the dead scratch)
@@ -1392,13 +1410,25 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
   if (fused) {
     hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode, P, A, inv_B);
   } else {
+    // MLT_LENET_C2FC=0: conv2 (K2) and the fc chain (K3) as two launches instead of the fused
+    // per-sample conv2 -> fc kernel (KF from p1)
+    static const bool c2fc = [] {
+      const char* v = getenv("MLT_LENET_C2FC");
+      return v == nullptr || atoi(v) != 0;
+    }();
     if (mode & LENET_FWD) {
       hipLaunchKernelGGL(lenet_conv1_fwd<D>, dim3(B, D::C1), dim3(256), 0, st, A, P.w1, P.b1, P.x, P.p1, P.i1,
                          A.data ? P.targets : nullptr, P.dtargets);
-      hipLaunchKernelGGL(lenet_conv2_fwd<D>, dim3(B, D::C2 / 4), dim3(128), 0, st, P.p1, P.w2, P.b2, P.p2, P.i2);
-    }
-    if (mode & (LENET_FWD | LENET_CE | LENET_BWD))
+      if (c2fc) {
+        hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode | LENET_FROM_P1, P, A,
+                           inv_B);
+      } else {
+        hipLaunchKernelGGL(lenet_conv2_fwd<D>, dim3(B, D::C2 / 4), dim3(128), 0, st, P.p1, P.w2, P.b2, P.p2, P.i2);
+        hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
+      }
+    } else if (mode & (LENET_CE | LENET_BWD)) {
       hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
+    }
     if (mode & LENET_BWD)
       hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, 2 * D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2,
                          P.i1, P.g1, P.x, P.p1, P.slab1);
