@@ -450,6 +450,130 @@ __global__ __launch_bounds__(kFcThreads) void lenet_fc(int mode, LeNetPtrs P, fl
 }
 
 // ---------------------------------------------------------------------------
+// weight-gradient helpers shared by K4 (fc roles) and K5
+// ---------------------------------------------------------------------------
+struct OptCtx {
+  bool on;
+  float lr, t;
+};
+
+// optimizer state of one float4 / scalar, loaded before the gradient is ready so the loads
+// overlap the gradient computation instead of adding a dependent round trip after it
+struct Opt4 {
+  float4 p, a, c;
+};
+struct Opt1 {
+  float p, a, c;
+};
+__device__ __forceinline__ Opt4 opt_prefetch4(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
+  Opt4 r{};
+  if (!oc.on) return r;
+  r.p = *reinterpret_cast<const float4*>(O.p + i);
+  r.a = O.s1 ? *reinterpret_cast<const float4*>(O.s1 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  r.c = O.s2 ? *reinterpret_cast<const float4*>(O.s2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  return r;
+}
+__device__ __forceinline__ Opt1 opt_prefetch1(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
+  Opt1 r{};
+  if (!oc.on) return r;
+  r.p = O.p[i];
+  r.a = O.s1 ? O.s1[i] : 0.f;
+  r.c = O.s2 ? O.s2[i] : 0.f;
+  return r;
+}
+__device__ __forceinline__ void apply_pre4(const LeNetOpt& O, const OptCtx& oc, int64_t i, float4 g, Opt4 st) {
+  *reinterpret_cast<float4*>(O.g + i) = g;  // keep the gradient visible (inspection / checkpoints)
+  if (!oc.on) return;
+  opt_update(O.h, oc.lr, oc.t, st.p.x, g.x, st.a.x, st.c.x);
+  opt_update(O.h, oc.lr, oc.t, st.p.y, g.y, st.a.y, st.c.y);
+  opt_update(O.h, oc.lr, oc.t, st.p.z, g.z, st.a.z, st.c.z);
+  opt_update(O.h, oc.lr, oc.t, st.p.w, g.w, st.a.w, st.c.w);
+  *reinterpret_cast<float4*>(O.p + i) = st.p;
+  if (O.s1) *reinterpret_cast<float4*>(O.s1 + i) = st.a;
+  if (O.s2) *reinterpret_cast<float4*>(O.s2 + i) = st.c;
+}
+__device__ __forceinline__ void apply_pre1(const LeNetOpt& O, const OptCtx& oc, int64_t i, float g, Opt1 st) {
+  O.g[i] = g;
+  if (!oc.on) return;
+  opt_update(O.h, oc.lr, oc.t, st.p, g, st.a, st.c);
+  O.p[i] = st.p;
+  if (O.s1) O.s1[i] = st.a;
+  if (O.s2) O.s2[i] = st.c;
+}
+
+template <int NCOLS>
+__device__ __forceinline__ void fc_wgrad_block(int blk, int nrows, int B, const float* __restrict__ dY,
+                                               const float* __restrict__ X, const LeNetOpt& O, int64_t offW,
+                                               int64_t offb, const OptCtx& oc) {
+  constexpr int NV = NCOLS / 4;
+  const int item = blk * 256 + threadIdx.x;
+  if (item >= nrows * NV) return;
+  const int j = item / NV, v = item - j * NV;
+  const Opt4 pw = opt_prefetch4(O, oc, offW + 4 * (int64_t)item);
+  const Opt1 pb = v == 0 ? opt_prefetch1(O, oc, offb + j) : Opt1{};
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float bacc = 0.f;
+  const float4* x4 = reinterpret_cast<const float4*>(X);
+#pragma unroll 4
+  for (int b0 = 0; b0 < B; b0 += 8) {
+    float d[8];
+    float4 xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // 16 independent loads in flight
+      const int bb = b0 + u;
+      const bool ok = bb < B;
+      d[u] = ok ? dY[(int64_t)bb * nrows + j] : 0.f;
+      xv[u] = ok ? x4[(int64_t)bb * NV + v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc.x = fmaf(d[u], xv[u].x, acc.x);
+      acc.y = fmaf(d[u], xv[u].y, acc.y);
+      acc.z = fmaf(d[u], xv[u].z, acc.z);
+      acc.w = fmaf(d[u], xv[u].w, acc.w);
+      bacc += d[u];
+    }
+  }
+  apply_pre4(O, oc, offW + 4 * (int64_t)item, acc, pw);
+  if (v == 0) apply_pre1(O, oc, offb + j, bacc, pb);
+}
+
+// optimizer context of a weight-gradient launch: step counters / lr read from device memory
+// (the last K5 block advances the counters, so every reader in a step sees the same values)
+__device__ __forceinline__ OptCtx make_optctx(int mode, const LeNetOpt& O, const int64_t* ctrl) {
+  OptCtx oc;
+  oc.on = (mode & LENET_OPT) != 0;
+  oc.lr = O.h.lr;
+  oc.t = 1.f;
+  if (oc.on) {
+    const int64_t step = ctrl ? ctrl[0] : 0, sie = ctrl ? ctrl[1] : 0;
+    oc.t = (float)(step + 1);
+    if (O.lr_ptr) oc.lr = O.lr_ptr[O.lr_table ? sie : 0];
+  }
+  return oc;
+}
+
+// the fc weight-gradient roles (+ fused update): block `bf` of NB3 + NB4 + NB5
+template <class D>
+__device__ __forceinline__ void fc_wgrad_roles(int bf, int B, const LeNetPtrs& P, const LeNetOpt& O,
+                                               const OptCtx& oc) {
+  constexpr int F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
+  constexpr int NB3 = (F1 * (FLAT / 4) + 255) / 256, NB4 = (F2 * (F1 / 4) + 255) / 256,
+                NB5 = (NC * (F2 / 4) + 255) / 256;
+  if (bf < NB3) {
+    fc_wgrad_block<FLAT>(bf, F1, B, P.dh1, P.p2, O, O.off[4], O.off[5], oc);
+  } else if ((bf -= NB3) < NB4) {
+    fc_wgrad_block<F1>(bf, F2, B, P.dh2, P.h1, O, O.off[6], O.off[7], oc);
+  } else if ((bf -= NB4) < NB5) {
+    fc_wgrad_block<F2>(bf, NC, B, P.dlogits, P.h2, O, O.off[8], O.off[9], oc);
+  }
+}
+template <class D>
+constexpr int fc_wgrad_blocks() {
+  return (D::F1 * (D::FLAT / 4) + 255) / 256 + (D::F2 * (D::F1 / 4) + 255) / 256 + (D::NC * (D::F2 / 4) + 255) / 256;
+}
+
+// ---------------------------------------------------------------------------
 // K4: unpool2 (via arg-max) -> conv2 dgrad -> mask by pool1 arg-max liveness.
 // Block (256 = 4 waves) per (sample, input channel); lane = 2x2 output patch of the
 // 14x14 map, wave = quarter of the conv2 output channels (reduced through LDS in order).
@@ -469,10 +593,16 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
                                                          const float* __restrict__ w2,
                                                          const uint8_t* __restrict__ i1, float* __restrict__ g1,
                                                          const float* __restrict__ x, const float* __restrict__ p1,
-                                                         float* __restrict__ slab) {
+                                                         float* __restrict__ slab, int mode, LeNetPtrs P, LeNetOpt O,
+                                                         const int64_t* __restrict__ ctrl) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, NZ4 = C2 * 81, NS = (FLAT + 255) / 256;
   constexpr int W2N = C2 * 25 + C2;  // conv2 wgrad outputs of one input channel (+ the biases)
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (WG && (int)blockIdx.y >= 2 * C1) {  // fc wgrad (+ update) blocks: independent of the dgrad
+    const int bf = ((int)blockIdx.y - 2 * C1) * (int)gridDim.x + b;
+    if (bf < fc_wgrad_blocks<D>()) fc_wgrad_roles<D>(bf, (int)gridDim.x, P, O, make_optctx(mode, O, ctrl));
+    return;
+  }
   const bool w2role = WG && (int)blockIdx.y >= C1;
   const int ic = w2role ? (int)blockIdx.y - C1 : (int)blockIdx.y;
   __shared__ __attribute__((aligned(16))) float dc[C2 * 324];  // zero-padded dense conv2-output grad [C2][18][18]
@@ -1051,91 +1181,6 @@ __global__ __launch_bounds__(kFusedThreads) void lenet_sample_fused(int mode, Le
 // ---------------------------------------------------------------------------
 constexpr int kWgChunk = 32;  // samples staged per LDS pass in the conv2 wgrad role
 
-struct OptCtx {
-  bool on;
-  float lr, t;
-};
-
-// optimizer state of one float4 / scalar, loaded before the gradient is ready so the loads
-// overlap the gradient computation instead of adding a dependent round trip after it
-struct Opt4 {
-  float4 p, a, c;
-};
-struct Opt1 {
-  float p, a, c;
-};
-__device__ __forceinline__ Opt4 opt_prefetch4(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
-  Opt4 r{};
-  if (!oc.on) return r;
-  r.p = *reinterpret_cast<const float4*>(O.p + i);
-  r.a = O.s1 ? *reinterpret_cast<const float4*>(O.s1 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-  r.c = O.s2 ? *reinterpret_cast<const float4*>(O.s2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-  return r;
-}
-__device__ __forceinline__ Opt1 opt_prefetch1(const LeNetOpt& O, const OptCtx& oc, int64_t i) {
-  Opt1 r{};
-  if (!oc.on) return r;
-  r.p = O.p[i];
-  r.a = O.s1 ? O.s1[i] : 0.f;
-  r.c = O.s2 ? O.s2[i] : 0.f;
-  return r;
-}
-__device__ __forceinline__ void apply_pre4(const LeNetOpt& O, const OptCtx& oc, int64_t i, float4 g, Opt4 st) {
-  *reinterpret_cast<float4*>(O.g + i) = g;  // keep the gradient visible (inspection / checkpoints)
-  if (!oc.on) return;
-  opt_update(O.h, oc.lr, oc.t, st.p.x, g.x, st.a.x, st.c.x);
-  opt_update(O.h, oc.lr, oc.t, st.p.y, g.y, st.a.y, st.c.y);
-  opt_update(O.h, oc.lr, oc.t, st.p.z, g.z, st.a.z, st.c.z);
-  opt_update(O.h, oc.lr, oc.t, st.p.w, g.w, st.a.w, st.c.w);
-  *reinterpret_cast<float4*>(O.p + i) = st.p;
-  if (O.s1) *reinterpret_cast<float4*>(O.s1 + i) = st.a;
-  if (O.s2) *reinterpret_cast<float4*>(O.s2 + i) = st.c;
-}
-__device__ __forceinline__ void apply_pre1(const LeNetOpt& O, const OptCtx& oc, int64_t i, float g, Opt1 st) {
-  O.g[i] = g;
-  if (!oc.on) return;
-  opt_update(O.h, oc.lr, oc.t, st.p, g, st.a, st.c);
-  O.p[i] = st.p;
-  if (O.s1) O.s1[i] = st.a;
-  if (O.s2) O.s2[i] = st.c;
-}
-
-template <int NCOLS>
-__device__ __forceinline__ void fc_wgrad_block(int blk, int nrows, int B, const float* __restrict__ dY,
-                                               const float* __restrict__ X, const LeNetOpt& O, int64_t offW,
-                                               int64_t offb, const OptCtx& oc) {
-  constexpr int NV = NCOLS / 4;
-  const int item = blk * 256 + threadIdx.x;
-  if (item >= nrows * NV) return;
-  const int j = item / NV, v = item - j * NV;
-  const Opt4 pw = opt_prefetch4(O, oc, offW + 4 * (int64_t)item);
-  const Opt1 pb = v == 0 ? opt_prefetch1(O, oc, offb + j) : Opt1{};
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  float bacc = 0.f;
-  const float4* x4 = reinterpret_cast<const float4*>(X);
-#pragma unroll 4
-  for (int b0 = 0; b0 < B; b0 += 8) {
-    float d[8];
-    float4 xv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {  // 16 independent loads in flight
-      const int bb = b0 + u;
-      const bool ok = bb < B;
-      d[u] = ok ? dY[(int64_t)bb * nrows + j] : 0.f;
-      xv[u] = ok ? x4[(int64_t)bb * NV + v] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      acc.x = fmaf(d[u], xv[u].x, acc.x);
-      acc.y = fmaf(d[u], xv[u].y, acc.y);
-      acc.z = fmaf(d[u], xv[u].z, acc.z);
-      acc.w = fmaf(d[u], xv[u].w, acc.w);
-      bacc += d[u];
-    }
-  }
-  apply_pre4(O, oc, offW + 4 * (int64_t)item, acc, pw);
-  if (v == 0) apply_pre1(O, oc, offb + j, bacc, pb);
-}
 
 template <class D>
 __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetOpt O, int B,
@@ -1150,15 +1195,7 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
   int blk = blockIdx.x;
   const int t = threadIdx.x;
   // The step counters are read by every block here and advanced by the last block of the launch.
-  OptCtx oc;
-  oc.on = (mode & LENET_OPT) != 0;
-  oc.lr = O.h.lr;
-  oc.t = 1.f;
-  if (oc.on) {
-    const int64_t step = ctrl ? ctrl[0] : 0, sie = ctrl ? ctrl[1] : 0;
-    oc.t = (float)(step + 1);
-    if (O.lr_ptr) oc.lr = O.lr_ptr[O.lr_table ? sie : 0];
-  }
+  const OptCtx oc = make_optctx(mode, O, ctrl);
   // K4WG: K4 left per-(sample, channel) conv wgrad slabs; the conv roles only reduce them over
   // the batch in sample order (one output per thread) -- the fc roles keep their block ids
   constexpr int NR1 = (C1 * kTaps1 + 255) / 256, NR2 = (C2 * C1 * 25 + C2 + 255) / 256;
@@ -1429,9 +1466,13 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     } else if (mode & (LENET_CE | LENET_BWD)) {
       hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
     }
-    if (mode & LENET_BWD)
-      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, 2 * D::C1), dim3(256), 0, st, P.dflat, P.i2, P.w2,
-                         P.i1, P.g1, P.x, P.p1, P.slab1);
+    if (mode & LENET_BWD) {
+      // K4: dgrad + conv1 wgrad slabs (y < C1), conv2 wgrad slabs (C1 <= y < 2 C1), fc wgrads
+      // with their update (y >= 2 C1: fc weights are not read after K3/KF)
+      const unsigned k4y = 2 * D::C1 + (fc_wgrad_blocks<D>() + B - 1) / B;
+      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, k4y), dim3(256), 0, st,
+                         P.dflat, P.i2, P.w2, P.i1, P.g1, P.x, P.p1, P.slab1, mode, P, O, A.ctrl);
+    }
   }
   if ((mode & LENET_BWD) && !(fused && (mode & LENET_TRACE))) {
     constexpr int NB3 = (D::F1 * (D::FLAT / 4) + 255) / 256, NB4 = (D::F2 * (D::F1 / 4) + 255) / 256,
@@ -1439,7 +1480,7 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     // non-fused path: K4 already produced the conv wgrad slabs (K4WG); the fused KF does not
     const int k4wg = fused ? 0 : LENET_K4WG;
     constexpr int NR1 = (D::C1 * kTaps1 + 255) / 256, NR2 = (D::C2 * D::C1 * 25 + D::C2 + 255) / 256;
-    const int nblk = k4wg ? NR1 + NR2 + NB3 + NB4 + NB5
+    const int nblk = k4wg ? NR1 + NR2  // K4 ran the fc roles too
                           : (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
     // MLT_LENET_WGRAD_SKIP=<mask> (profiling only): 1 conv1 / 2 conv2 / 4 fc roles return at once
     static const int skip = [] {
