@@ -1220,13 +1220,13 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
         }
         const Opt1 pst = opt_prefetch1(O, oc, dst);
         const int64_t sstride = (int64_t)C1 * kSlabStride;
-        float g = 0.f;
-        for (int b0 = 0; b0 < B; b0 += 8) {
-          float v[8];
+        float g = 0.f;  // all 32 loads of a batch chunk in flight (clamped, branch-free), summed in order
+        for (int b0 = 0; b0 < B; b0 += 32) {
+          float v[32];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = b0 + u < B ? P.slab1[(b0 + u) * sstride + src] : 0.f;
+          for (int u = 0; u < 32; ++u) v[u] = P.slab1[min(b0 + u, B - 1) * sstride + src];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) g += v[u];
+          for (int u = 0; u < 32; ++u) g += b0 + u < B ? v[u] : 0.f;
         }
         apply_pre1(O, oc, dst, g, pst);
       }
