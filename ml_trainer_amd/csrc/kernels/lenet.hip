@@ -57,7 +57,11 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
                                                        int64_t* __restrict__ targets,
                                                        const int64_t* __restrict__ dtargets) {
   const int b = blockIdx.x, oc = blockIdx.y, t = threadIdx.x;
-  __shared__ __attribute__((aligned(16))) float xs[3 * 1024];
+  // input image rows at a 46-float stride: the 14 lanes of a pooled row read 2 px apart, so with
+  // a 32-float stride the (up to 5) pooled rows of a wave land on the same banks; 2 * 46 = 28 (mod
+  // 64) staggers them (even, so the 8-byte window reads stay aligned)
+  constexpr int XR = 46, XC = 32 * XR;
+  __shared__ __attribute__((aligned(16))) float xs[3 * XC];
   __shared__ __attribute__((aligned(16))) uint4 rawimg[192];
   // filter + bias first: block-uniform scalar loads that overlap the ctrl -> perm -> image chain
   float wr[75];
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
       const bool in = (unsigned)r < 32u && (unsigned)q < 32u;
       const float u = in ? (float)img[(r * 32 + q) * 3 + c] : 0.f;
       const float v = (u / 255.f - aug.mean[c]) / aug.std[c];
-      xs[e] = v;
+      xs[c * XC + y * XR + xx] = v;
       if (oc == 0) x[(int64_t)b * 3072 + e] = v;
     }
     if (oc == 0 && t == 0 && targets) targets[b] = dtargets[idx];
@@ -99,7 +103,12 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
 #pragma unroll
     for (int i = 0; i < 3; ++i) v[i] = src[t + i * 256];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(xs)[t + i * 256] = v[i];
+    for (int i = 0; i < 3; ++i) {
+      const int e = 4 * (t + i * 256), c = e >> 10, y = (e >> 5) & 31, xx = e & 31;
+      float2* d = reinterpret_cast<float2*>(xs + c * XC + y * XR + xx);
+      d[0] = make_float2(v[i].x, v[i].y);
+      d[1] = make_float2(v[i].z, v[i].w);
+    }
   }
   __syncthreads();
   if (t >= 196) return;
@@ -111,7 +120,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
     for (int r = 0; r < 6; ++r) {
       float in[6];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) in[q] = xs[ic * 1024 + (y0 + r) * 32 + x0 + q];
+      for (int q = 0; q < 6; ++q) in[q] = xs[ic * XC + (y0 + r) * XR + x0 + q];
       if (r < 5) {
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
