@@ -93,11 +93,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     g[4 * v + 2] = gv.z;
     g[4 * v + 3] = gv.w;
   }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+  // software-pipelined over the wave's rows: the next row's x / dy / statistics are in flight
+  // while this row computes (each wave walks ~rows / 2048 rows; one row of latency per step otherwise)
+  const int64_t rstep = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + wid;
+  ushort4 nx[VPL], ndy[VPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    const int64_t rr = r < rows ? r : rows - 1;  // clamped, branch-free
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      nx[v] = reinterpret_cast<const ushort4*>(X + rr * D)[lane + 64 * v];
+      ndy[v] = reinterpret_cast<const ushort4*>(DY + rr * D)[lane + 64 * v];
+    }
+    nmu = mean[rr];
+    nrs = rstd[rr];
+  };
+  if (row < rows) fetch(row);
+  for (; row < rows; row += rstep) {
     float x[E], dy[E];
-    load_row<VPL>(X + row * D, x);
-    load_row<VPL>(DY + row * D, dy);
-    const float mu = mean[row], rs = rstd[row];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      x[4 * v + 0] = bf16_to_f32(nx[v].x);
+      x[4 * v + 1] = bf16_to_f32(nx[v].y);
+      x[4 * v + 2] = bf16_to_f32(nx[v].z);
+      x[4 * v + 3] = bf16_to_f32(nx[v].w);
+      dy[4 * v + 0] = bf16_to_f32(ndy[v].x);
+      dy[4 * v + 1] = bf16_to_f32(ndy[v].y);
+      dy[4 * v + 2] = bf16_to_f32(ndy[v].z);
+      dy[4 * v + 3] = bf16_to_f32(ndy[v].w);
+    }
+    const float mu = nmu, rs = nrs;
+    fetch(row + rstep);  // unconditional: past the end it re-reads the last row (unused)
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
