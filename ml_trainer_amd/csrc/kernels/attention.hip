@@ -1055,8 +1055,10 @@ __global__ __launch_bounds__(256) void attn_fwd_ring_kernel(const uint16_t* __re
 
 // 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
 // MLT_ATTN_FWD_GROUPS / MLT_ATTN_DKDV_GROUPS / MLT_ATTN_DQ_GROUPS = 1|2 override the choice
-// Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dK/dV 1 group (2 groups need
-// > 256 VGPRs and halve the occupancy), dQ 2 groups.
+// Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dQ 2 groups. dK/dV: with the
+// register-staged kernel 1 group (2 need > 256 VGPRs and halve the occupancy); with the ring
+// kernels (the default) 2 groups, 10-14 % faster backward at B16..B128 (B32 198 -> 176 us,
+// B128 727 -> 629 us: each Q / dO ring stage feeds twice the MFMAs).
 static int attn_groups(const char* env, int S, int dflt = 2) {
   const char* v = getenv(env);
   if (v && (v[0] == '1' || v[0] == '2')) return S >= 128 ? v[0] - '0' : 1;
@@ -1104,7 +1106,7 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   const char* rv = getenv("MLT_ATTN_RING");
   const int ring = rv ? atoi(rv) : 4;
   if (ring == 3 || ring == 4) {
-    const bool k2 = attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2, q2 = attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2;
+    const bool k2 = attn_groups("MLT_ATTN_DKDV_GROUPS", S, 2) == 2, q2 = attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2;
 #define MLT_RING_LAUNCH(RD)                                                                                         \
   {                                                                                                                 \
     if (k2)                                                                                                         \
