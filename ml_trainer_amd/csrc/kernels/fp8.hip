@@ -159,6 +159,73 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_kernel(const InT* __re
   }
 }
 
+// Activation / gradient variant (bf16 [R, C], R % 128 == 0, C % 128 == 0 -- checked by the
+// launcher): 128 x 128 tiles, 8 x 16-byte loads in flight per thread, 8-byte y stores, and the
+// transposed side read back from LDS as dwords (8 rows x 4 columns per thread, transposed in
+// registers) so each wave's yt stores form 128-byte row segments instead of 64-byte ones.
+// 33-dword LDS row stride: the 16 row groups of a wave's dword reads land on 2-way banks.
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_fp8_wide_kernel(const uint16_t* __restrict__ x,
+                                                                      uint8_t* __restrict__ y,
+                                                                      uint8_t* __restrict__ yt, int R, int C,
+                                                                      const float* __restrict__ scale,
+                                                                      float* __restrict__ amax) {
+  constexpr int S = 132;  // LDS row stride in bytes
+  __shared__ uint32_t tile32[128 * S / 4];
+  __shared__ float red[4];
+  const float s = *scale;
+  const int r0 = blockIdx.y * 128, c0 = blockIdx.x * 128;
+  const int tid = threadIdx.x;
+  float mx = 0.f;
+  uint4 raw[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {  // item: row (it * 16 + tid / 16), 8 columns at (tid % 16) * 8
+    const int r = it * 16 + (tid >> 4), c8 = (tid & 15) * 8;
+    raw[it] = *reinterpret_cast<const uint4*>(x + (int64_t)(r0 + r) * C + c0 + c8);
+  }
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int r = it * 16 + (tid >> 4), c8 = (tid & 15) * 8;
+    const uint32_t w[4] = {raw[it].x, raw[it].y, raw[it].z, raw[it].w};
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+    const uint32_t lo = pack4_fp8<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    const uint32_t hi = pack4_fp8<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    *reinterpret_cast<uint2*>(y + (int64_t)(r0 + r) * C + c0 + c8) = make_uint2(lo, hi);
+    tile32[(r * S + c8) / 4] = lo;
+    tile32[(r * S + c8) / 4 + 1] = hi;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {  // item: 4 columns at c4 = (e / 16) * 4, 8 rows at r8 = (e % 16) * 8
+    const int e = it * 256 + tid, c4 = (e >> 4) * 4, r8 = (e & 15) * 8;
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = tile32[((r8 + k) * S + c4) / 4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sh = 8 * j;
+      const uint32_t lo = ((d[0] >> sh) & 0xffu) | (((d[1] >> sh) & 0xffu) << 8) | (((d[2] >> sh) & 0xffu) << 16) |
+                          (((d[3] >> sh) & 0xffu) << 24);
+      const uint32_t hi = ((d[4] >> sh) & 0xffu) | (((d[5] >> sh) & 0xffu) << 8) | (((d[6] >> sh) & 0xffu) << 16) |
+                          (((d[7] >> sh) & 0xffu) << 24);
+      *reinterpret_cast<uint2*>(yt + (int64_t)(c0 + c4 + j) * R + r0 + r8) = make_uint2(lo, hi);
+    }
+  }
+  if (amax) {
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
 // Batched delayed scaling over n tensors: a = max over the amax slots of tensor i;
 // hist[i][step % H] = a; scale[i] = fmax[i] / (max_h hist[i][h] * 2^margin);
 // inv_scale[i] = 1 / scale[i]; slots reset to 0.
@@ -221,6 +288,20 @@ void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, i
 void launch_cast_transpose_fp8_bf16(const uint16_t* x, uint8_t* y, uint8_t* yt, int R, int C, const float* scale,
                                     float* amax, int fmt, hipStream_t st) {
   if (R <= 0 || C <= 0) return;
+  // MLT_FP8_CT_WIDE=0 keeps the 64x64 kernel (A/B knob)
+  static const bool wide_ok = [] {
+    const char* e = getenv("MLT_FP8_CT_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (wide_ok && R % 128 == 0 && C % 128 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(yt) & 7) == 0) {
+    const dim3 g(C / 128, R / 128), b(256);
+    if (fmt == 0)
+      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<0>), g, b, 0, st, x, y, yt, R, C, scale, amax);
+    else
+      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<1>), g, b, 0, st, x, y, yt, R, C, scale, amax);
+    return;
+  }
   const dim3 g((C + 63) / 64, (R + 63) / 64), b(256);
   if (fmt == 0)
     hipLaunchKernelGGL((cast_transpose_fp8_kernel<0, uint16_t>), g, b, 0, st, x, y, yt, R, C, scale, amax);

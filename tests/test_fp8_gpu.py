@@ -141,13 +141,15 @@ def test_fp8_bert_trains(dev):
 
 
 @pytest.mark.parametrize("fmt", [0, 1])
-def test_cast_transpose_bf16_input(dev, fmt):
+@pytest.mark.parametrize("shape", [(256, 192), (384, 512), (1024, 3072)])  # 64x64 kernel / 128x128 wide kernel
+def test_cast_transpose_bf16_input(dev, fmt, shape):
     C = require_native()
+    R, Cc = shape
     g = torch.Generator().manual_seed(5 + fmt)
-    x = torch.randn(256, 192, generator=g).to(dev).to(torch.bfloat16)
+    x = torch.randn(R, Cc, generator=g).to(dev).to(torch.bfloat16)
     dt = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
-    y = torch.empty(256, 192, dtype=dt, device=dev)
-    yt = torch.empty(192, 256, dtype=dt, device=dev)
+    y = torch.empty(R, Cc, dtype=dt, device=dev)
+    yt = torch.empty(Cc, R, dtype=dt, device=dev)
     scale = torch.tensor([2.0], device=dev)
     amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
     C.fp8_cast_transpose(x, y, yt, scale, amax, fmt)
