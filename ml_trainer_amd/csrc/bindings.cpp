@@ -430,7 +430,8 @@ void fp8_amax(Tensor x, Tensor amax) {
   launch_amax(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), amax.data_ptr<float>(), cur_stream());
 }
 
-void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::optional<Tensor> amax, int fmt) {
+void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::optional<Tensor> amax, int fmt,
+                        c10::optional<Tensor> colsum_out, bool colsum_accumulate) {
   TORCH_CHECK(w.dim() == 2 && w.is_cuda() && w.is_contiguous() &&
                   (w.scalar_type() == at::kFloat || w.scalar_type() == at::kBFloat16),
               "w: fp32 or bf16 [R,C]");
@@ -445,14 +446,35 @@ void fp8_cast_transpose(Tensor w, Tensor y, Tensor yt, Tensor scale, c10::option
     am = amax->data_ptr<float>();
   }
   TORCH_CHECK(fmt == 0 || fmt == 1, "fmt: 0 = e4m3, 1 = e5m2");
+  TORCH_CHECK(!colsum_out.has_value() || w.scalar_type() == at::kBFloat16, "colsum_out needs a bf16 input");
   if (w.scalar_type() == at::kFloat)
     launch_cast_transpose_fp8(w.data_ptr<float>(), reinterpret_cast<uint8_t*>(y.data_ptr()),
                               reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(), am,
                               fmt, cur_stream());
-  else
+  else if (!colsum_out.has_value())
     launch_cast_transpose_fp8_bf16(bf16_ptr(w), reinterpret_cast<uint8_t*>(y.data_ptr()),
                                    reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc, scale.data_ptr<float>(),
                                    am, fmt, cur_stream());
+  else {
+    // column sums of w (the bias gradient when w is a GEMM's dY) from the same read of w
+    check_dev(*colsum_out, "colsum_out", at::kFloat, Cc, 16);
+    float* cs = colsum_out->data_ptr<float>();
+    const int acc = colsum_accumulate ? 1 : 0;
+    if (cast_transpose_fp8_wide_ok(w.data_ptr(), y.data_ptr(), yt.data_ptr(), (int)R, (int)Cc)) {
+      Tensor ws = at::empty({R / 128 * Cc}, w.options().dtype(at::kFloat));
+      launch_cast_transpose_fp8_bf16(bf16_ptr(w), reinterpret_cast<uint8_t*>(y.data_ptr()),
+                                     reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc,
+                                     scale.data_ptr<float>(), am, fmt, cur_stream(), ws.data_ptr<float>());
+      SegOut o{{cs, nullptr, nullptr}};
+      launch_reduce_rows(ws.data_ptr<float>(), (int)(R / 128), Cc, (int)Cc, (int)Cc, o, acc, cur_stream());
+    } else {
+      launch_cast_transpose_fp8_bf16(bf16_ptr(w), reinterpret_cast<uint8_t*>(y.data_ptr()),
+                                     reinterpret_cast<uint8_t*>(yt.data_ptr()), (int)R, (int)Cc,
+                                     scale.data_ptr<float>(), am, fmt, cur_stream());
+      Tensor ws = at::empty({std::max<int64_t>(colsum_ws_floats((int)R, (int)Cc), 4)}, w.options().dtype(at::kFloat));
+      launch_colsum_bf16(bf16_ptr(w), (int)R, (int)Cc, Cc, cs, acc, ws.data_ptr<float>(), cur_stream());
+    }
+  }
 }
 
 // hist [n, H], amax [n, kAmaxSlots], scale / inv_scale / fmax [n]
@@ -1022,7 +1044,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("fmt") = 0);
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_cast_transpose", &fp8_cast_transpose, py::arg("w"), py::arg("y"), py::arg("yt"), py::arg("scale"),
-        py::arg("amax") = py::none(), py::arg("fmt") = 0);
+        py::arg("amax") = py::none(), py::arg("fmt") = 0, py::arg("colsum_out") = py::none(),
+        py::arg("colsum_accumulate") = false);
   m.attr("FP8_AMAX_SLOTS") = kAmaxSlots * kAmaxStride;  // floats of amax state per tensor
   m.def("fp8_update_scale", &fp8_update_scale, py::arg("hist"), py::arg("amax"), py::arg("scale"),
         py::arg("inv_scale"), py::arg("fmax"), py::arg("step"), py::arg("margin") = 0);

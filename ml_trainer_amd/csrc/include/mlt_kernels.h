@@ -141,8 +141,9 @@ void launch_cast_fp8(const void* x, bool x_f32, uint8_t* y, int64_t n, const flo
 void launch_amax(const void* x, bool x_f32, int64_t n, float* amax, hipStream_t st);
 void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, int C, const float* scale, float* amax,
                                int fmt, hipStream_t st);
+bool cast_transpose_fp8_wide_ok(const void* x, const void* y, const void* yt, int R, int C);
 void launch_cast_transpose_fp8_bf16(const uint16_t* x, uint8_t* y, uint8_t* yt, int R, int C, const float* scale,
-                                    float* amax, int fmt, hipStream_t st);
+                                    float* amax, int fmt, hipStream_t st, float* colpart = nullptr);
 void launch_fp8_update_scale(float* hist, int H, int n, float* amax, float* scale, float* inv_scale, const float* fmax,
                              int margin, int64_t step, hipStream_t st);
 

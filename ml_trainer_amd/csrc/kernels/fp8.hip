@@ -169,7 +169,8 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_wide_kernel(const uint
                                                                       uint8_t* __restrict__ y,
                                                                       uint8_t* __restrict__ yt, int R, int C,
                                                                       const float* __restrict__ scale,
-                                                                      float* __restrict__ amax) {
+                                                                      float* __restrict__ amax,
+                                                                      float* __restrict__ colpart) {
   constexpr int S = 132;  // LDS row stride in bytes
   __shared__ uint32_t tile32[128 * S / 4];
   __shared__ float red[4];
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_wide_kernel(const uint
   const int r0 = blockIdx.y * 128, c0 = blockIdx.x * 128;
   const int tid = threadIdx.x;
   float mx = 0.f;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of x over this thread's 8 rows
   uint4 raw[8];
 #pragma unroll
   for (int it = 0; it < 8; ++it) {  // item: row (it * 16 + tid / 16), 8 columns at (tid % 16) * 8
@@ -194,7 +196,10 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_wide_kernel(const uint
       v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+    for (int j = 0; j < 8; ++j) {
+      mx = fmaxf(mx, fabsf(v[j]));
+      cs[j] += v[j];
+    }
     const uint32_t lo = pack4_fp8<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
     const uint32_t hi = pack4_fp8<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
     *reinterpret_cast<uint2*>(y + (int64_t)(r0 + r) * C + c0 + c8) = make_uint2(lo, hi);
@@ -216,6 +221,20 @@ __global__ __launch_bounds__(256) void cast_transpose_fp8_wide_kernel(const uint
       const uint32_t hi = ((d[4] >> sh) & 0xffu) | (((d[5] >> sh) & 0xffu) << 8) | (((d[6] >> sh) & 0xffu) << 16) |
                           (((d[7] >> sh) & 0xffu) << 24);
       *reinterpret_cast<uint2*>(yt + (int64_t)(c0 + c4 + j) * R + r0 + r8) = make_uint2(lo, hi);
+    }
+  }
+  if (colpart) {  // bias gradient of the GEMM whose dY this is: per-tile column sums, fixed order
+    __syncthreads();  // the transposed reads of the tile are done; reuse it as [16][128] floats
+    float* cp = reinterpret_cast<float*>(tile32);
+    const int grp = tid >> 4, c8 = (tid & 15) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cp[grp * 128 + c8 + j] = cs[j];
+    __syncthreads();
+    if (tid < 128) {
+      float a = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < 16; ++g2) a += cp[g2 * 128 + tid];
+      colpart[(int64_t)blockIdx.y * C + c0 + tid] = a;
     }
   }
   if (amax) {
@@ -285,23 +304,30 @@ void launch_cast_transpose_fp8(const float* w, uint8_t* y, uint8_t* yt, int R, i
   else hipLaunchKernelGGL((cast_transpose_fp8_kernel<1, float>), g, b, 0, st, w, y, yt, R, C, scale, amax);
 }
 
-void launch_cast_transpose_fp8_bf16(const uint16_t* x, uint8_t* y, uint8_t* yt, int R, int C, const float* scale,
-                                    float* amax, int fmt, hipStream_t st) {
-  if (R <= 0 || C <= 0) return;
+bool cast_transpose_fp8_wide_ok(const void* x, const void* y, const void* yt, int R, int C) {
   // MLT_FP8_CT_WIDE=0 keeps the 64x64 kernel (A/B knob)
-  static const bool wide_ok = [] {
+  static const bool enabled = [] {
     const char* e = getenv("MLT_FP8_CT_WIDE");
     return !(e && e[0] == '0');
   }();
-  if (wide_ok && R % 128 == 0 && C % 128 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-      (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(yt) & 7) == 0) {
+  return enabled && R > 0 && C > 0 && R % 128 == 0 && C % 128 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(yt) & 7) == 0;
+}
+
+// colpart: optional [R / 128, C] fp32 column partial sums of x -- only with the wide kernel
+// (the caller checks cast_transpose_fp8_wide_ok first)
+void launch_cast_transpose_fp8_bf16(const uint16_t* x, uint8_t* y, uint8_t* yt, int R, int C, const float* scale,
+                                    float* amax, int fmt, hipStream_t st, float* colpart) {
+  if (R <= 0 || C <= 0) return;
+  if (cast_transpose_fp8_wide_ok(x, y, yt, R, C)) {
     const dim3 g(C / 128, R / 128), b(256);
     if (fmt == 0)
-      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<0>), g, b, 0, st, x, y, yt, R, C, scale, amax);
+      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<0>), g, b, 0, st, x, y, yt, R, C, scale, amax, colpart);
     else
-      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<1>), g, b, 0, st, x, y, yt, R, C, scale, amax);
+      hipLaunchKernelGGL((cast_transpose_fp8_wide_kernel<1>), g, b, 0, st, x, y, yt, R, C, scale, amax, colpart);
     return;
   }
+  if (colpart) return;  // contract violation: the caller must have used the wide path
   const dim3 g((C + 63) / 64, (R + 63) / 64), b(256);
   if (fmt == 0)
     hipLaunchKernelGGL((cast_transpose_fp8_kernel<0, uint16_t>), g, b, 0, st, x, y, yt, R, C, scale, amax);

@@ -79,13 +79,17 @@ class Fp8Context:
         require_native().fp8_cast(x, y, self.scale[i:i + 1], self.amax[i], fmt)
         return y
 
-    def cast_t(self, x: torch.Tensor, i: int, fmt: int):
-        """fp8 copy of a bf16 [R, C] tensor plus its transpose [C, R] in one pass (same scale)."""
+    def cast_t(self, x: torch.Tensor, i: int, fmt: int, colsum_out: Optional[torch.Tensor] = None,
+               colsum_accumulate: bool = False):
+        """fp8 copy of a bf16 [R, C] tensor plus its transpose [C, R] in one pass (same scale);
+        ``colsum_out`` (fp32 [C]) also receives the column sums of x from the same read (set or
+        accumulated): the bias gradient when x is a linear's dY."""
         if not self._ready[i]:
             self._init_exact(i, x)
         y = torch.empty(x.shape, dtype=_DT[fmt], device=x.device)
         yt = torch.empty(x.shape[1], x.shape[0], dtype=_DT[fmt], device=x.device)
-        require_native().fp8_cast_transpose(x, y, yt, self.scale[i:i + 1], self.amax[i], fmt)
+        require_native().fp8_cast_transpose(x, y, yt, self.scale[i:i + 1], self.amax[i], fmt,
+                                            colsum_out=colsum_out, colsum_accumulate=colsum_accumulate)
         return y, yt
 
     def inv(self, i: int) -> torch.Tensor:
@@ -161,6 +165,7 @@ class Fp8Linear:
     transposed activations produced and kept."""
 
     training = True
+    wgrad_fuses_bias = True  # wgrad(..., db_out=) reduces the bias gradient inside the dY cast
 
     @staticmethod
     def fwd(x, w, bias=None, gelu_aux=None, res=None):
@@ -179,15 +184,16 @@ class Fp8Linear:
         return y
 
     @staticmethod
-    def wgrad(w, dy, x, out: Optional[torch.Tensor]):
+    def wgrad(w, dy, x, out: Optional[torch.Tensor], db_out: Optional[torch.Tensor] = None, db_acc: bool = False):
         """dW = dY^T X in fp8 into ``out`` (accumulate) or a new fp32 tensor; None when the forward
-        left no transposed input for this weight (the caller then uses the bf16 GEMM)."""
+        left no transposed input for this weight (the caller then uses the bf16 GEMM, and
+        ``db_out`` is untouched). ``db_out``: bias gradient column sums of dY, from the cast."""
         st = getattr(w, "_mlt_f8", None)
         if st is None or st.xt is None or st.xt[0] != x.data_ptr() or not _fp8_wgrad_ok(x, w):
             return None
         C = require_native()
         ctx = context(dy.device)
-        dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2)
+        dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2, colsum_out=db_out, colsum_accumulate=db_acc)
         st.dy8 = (dy.data_ptr(), dy8)
         acc = out is not None
         if out is None:

@@ -120,6 +120,29 @@ class _Grads:
         require_native().gemm(dy, x, g, True, True, accumulate=True)
         return None
 
+    def wgrad_bias(self, pw, pb, dy, x, impl=None):
+        """(dW, db) of one linear. With an fp8 ``impl`` the bias gradient is reduced inside the
+        dY cast the fp8 weight gradient needs anyway (one read of dY instead of two)."""
+        if pb is None or impl is None or not getattr(impl, "wgrad_fuses_bias", False):
+            return self.wgrad(pw, dy, x, impl), self.colsum(pb, dy)
+        C = require_native()
+        g, gb = self.sink(pw), self.sink(pb)
+        db = gb if gb is not None else torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device)
+        r = impl.wgrad(pw, dy, x, g, db_out=db, db_acc=gb is not None)
+        if r is not None:
+            return (None if g is not None else r), (None if gb is not None else db)
+        # fp8 weight gradient not applicable here: separate kernels into the same sinks
+        if g is None:
+            dw = linear_wgrad(dy, x)
+        else:
+            C.gemm(dy, x, g, True, True, accumulate=True)
+            dw = None
+        if gb is None:
+            C.colsum(dy, db, False)
+            return dw, db
+        C.colsum(dy, gb, accumulate=True)
+        return dw, None
+
     def colsum(self, p, dy):
         g = self.sink(p)
         if g is None:
@@ -156,8 +179,7 @@ def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
     C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
-    dwqkv = G.wgrad(wqkv, dqkv, x, impl)
-    dbqkv = G.colsum(bqkv, dqkv)
+    dwqkv, dbqkv = G.wgrad_bias(wqkv, bqkv, dqkv, x, impl)
     dx = impl.dgrad(dqkv, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
     return dx, dwqkv, dbqkv, dwo, dbo
 
@@ -176,8 +198,7 @@ def _ffn_bwd(saved, params, dy, G, db2="colsum", impl=BF16):
     if isinstance(db2, str):
         db2 = G.colsum(b2, dy)
     dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
-    dw1 = G.wgrad(w1, dpre, x, impl)
-    db1 = G.colsum(b1, dpre)
+    dw1, db1 = G.wgrad_bias(w1, b1, dpre, x, impl)
     dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)
     return dx, dw1, db1, dw2, db2
 

@@ -160,6 +160,32 @@ def test_cast_transpose_bf16_input(dev, fmt, shape):
     assert float(amax.max()) == float(x.float().abs().max())
 
 
+@pytest.mark.parametrize("shape", [(256, 192), (384, 512), (1024, 3072)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_cast_transpose_fused_colsum(dev, shape, acc):
+    """Bias-gradient column sums from the dY cast (wide kernel partials + fixed-order reduce, or
+    the separate colsum on the 64x64 path) vs an fp32 torch reduction; casts are unchanged."""
+    C = require_native()
+    R, Cc = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(R, Cc, generator=g).to(dev).to(torch.bfloat16)
+    y = torch.empty(R, Cc, dtype=torch.float8_e5m2, device=dev)
+    yt = torch.empty(Cc, R, dtype=torch.float8_e5m2, device=dev)
+    y2, yt2 = torch.empty_like(y), torch.empty_like(yt)
+    scale = torch.tensor([4.0], device=dev)
+    amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
+    base = torch.randn(Cc, generator=g).to(dev)
+    out = base.clone() if acc else torch.full((Cc,), float("nan"), device=dev)
+    C.fp8_cast_transpose(x, y, yt, scale, amax, 1, colsum_out=out, colsum_accumulate=acc)
+    C.fp8_cast_transpose(x, y2, yt2, scale, None, 1)
+    assert torch.equal(y.view(torch.uint8), y2.view(torch.uint8)) and torch.equal(yt.view(torch.uint8), yt2.view(torch.uint8))
+    ref = x.float().sum(0) + (base if acc else 0.0)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-3)
+    out2 = base.clone() if acc else torch.empty(Cc, device=dev)
+    C.fp8_cast_transpose(x, y2, yt2, scale, None, 1, colsum_out=out2, colsum_accumulate=acc)
+    assert torch.equal(out, out2)  # deterministic
+
+
 def test_fp8_weight_gradient_path(dev):
     """Fp8Linear: forward caches X^T (e4m3), wgrad casts dY with its transpose (e5m2), runs
     dY^T . X^T in fp8 and hands the e5m2 dY to the dgrad that follows."""
