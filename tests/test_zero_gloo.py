@@ -59,19 +59,20 @@ def _zero_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_zero1_matches_ddp():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_zero1_matches_ddp(world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_zero_worker, args=(world, free_port(), d), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"z{i}.pt"), weights_only=True) for i in range(world)]
         for k in r[0]["ddp"]:
             assert k.startswith("module.")
-            assert torch.equal(r[0]["zero"][k], r[1]["zero"][k])  # replicas identical after all-gather
+            for q in range(1, world):  # replicas identical after all-gather
+                assert torch.equal(r[0]["zero"][k], r[q]["zero"][k])
             torch.testing.assert_close(r[0]["zero"][k], r[0]["ddp"][k], rtol=1e-5, atol=1e-6)
-        # optimizer state is sharded: each rank holds half of the (padded) replicated state
+        # optimizer state is sharded: each rank holds 1/world of the (padded) replicated state
         assert r[0]["state_bytes"] * world == 2 * 4 * r[0]["zero_full_numel"]
         assert r[0]["state_bytes"] < r[0]["ddp_state_bytes"]
-        assert torch.equal(r[0]["zero_s1"], r[1]["zero_s1"])
+        assert all(torch.equal(r[0]["zero_s1"], r[q]["zero_s1"]) for q in range(1, world))
 
 
 def _trainer_worker(rank, world, port, out_dir, zero):
