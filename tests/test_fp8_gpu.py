@@ -233,3 +233,26 @@ def test_fp8_bert_uses_fp8_weight_gradients(dev):
     with torch.no_grad():
         m8(ids)
     assert all(p._mlt_f8.xt is None for p in lin)  # inference keeps no transposes
+
+
+def test_fp8_wgrad_bias_fused_and_fallback(dev):
+    """_Grads.wgrad_bias with the fp8 impl: the bias gradient comes out of the dY cast when the
+    forward kept X^T, and from the separate colsum when it did not -- same values either way."""
+    from ml_trainer_amd.ops.fp8 import FP8
+    from ml_trainer_amd.ops.transformer import _Grads
+    g = torch.Generator().manual_seed(13)
+    T, I, O = 512, 256, 384
+    x = (torch.randn(T, I, generator=g) * 0.5).to(dev).to(torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(O, I, generator=g) * 0.05).to(dev))
+    b = torch.nn.Parameter(torch.zeros(O, device=dev))
+    dy = (torch.randn(T, O, generator=g) * 0.1).to(dev).to(torch.bfloat16)
+    ref_db = dy.float().sum(0)
+    FP8.fwd(x, w, b)
+    G = _Grads()
+    dw, db = G.wgrad_bias(w, b, dy, x, FP8)  # fused: X^T cached by the forward
+    assert dw is not None and w._mlt_f8.xt is None
+    torch.testing.assert_close(db, ref_db, rtol=1e-5, atol=1e-3)
+    dw2, db2 = G.wgrad_bias(w, b, dy, x, FP8)  # no cached X^T: bf16 wgrad + separate colsum
+    torch.testing.assert_close(db2, ref_db, rtol=1e-5, atol=1e-3)
+    ref_dw = dy.float().t() @ x.float()
+    assert ((dw2 - ref_dw).norm() / ref_dw.norm()) < 0.02 and ((dw - ref_dw).norm() / ref_dw.norm()) < 0.1
