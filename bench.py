@@ -18,7 +18,12 @@ Scaling modes:
   reference       global batch 32 split across ranks (src/trainer.py:62-64)
 
 Usage:  python bench.py --gpus N --steps K --warmup W
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  N > 1 under a launcher (torch.distributed.run / torchrun): one rank per GPU over RCCL.
+  N > 1 without one: bench.py starts torch.distributed.run --nproc-per-node N itself.
+
+Timing: every hipGraph the K timed steps replay is captured and uploaded before the timed
+region (a capture counter is checked after it); wall time between barrier+synchronize pairs is
+reported, plus hipEvent device time per step in config.device_ms_per_step.
 
 BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgrad GEMMs with
 delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
@@ -56,7 +61,10 @@ def parse():
     ap.add_argument("--zero", type=int, default=0, choices=(0, 1),
                     help="BERT modes, N>1: 1 = ZeRO-1 sharded optimizer state instead of replicated DDP")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (BERT modes)")
-    ap.add_argument("--steps-per-graph", type=int, default=16)
+    ap.add_argument("--steps-per-graph", type=int, default=0,
+                    help="LeNet steps per captured hipGraph (0 = auto: min(steps, 64))")
+    ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
+                    help="cpu: BASELINE config 1 plumbing (stock torch ops, gloo); also used without a GPU")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dataset-size", type=int, default=50000)
     ap.add_argument("--optimizer", default="sgd")
@@ -156,8 +164,122 @@ def bench_bert(args, world, rank, dev):
     }
 
 
+def lenet_plan(nsteps: int, st: dict, n_data: int, world: int, rank: int, per_gpu: int, spg: int, shard_fn):
+    """The LeNet engine calls of the next ``nsteps`` steps, crossing epochs as needed, advancing
+    the epoch state ``st`` (keys epoch/shard_len/step_in_epoch/steps_per_epoch): yields
+    ("epoch", indices) and ("steps", batch, k, steps_per_graph). Every epoch ends with its
+    partial batch (DistributedSampler shard length not divisible by the batch) as a 1-step call."""
+    while nsteps > 0:
+        if st["step_in_epoch"] >= st["steps_per_epoch"]:
+            idx = shard_fn(n_data, world, rank, shuffle=True, seed=0, epoch=st["epoch"])
+            st["epoch"] += 1
+            st["shard_len"] = len(idx)
+            st["steps_per_epoch"] = math.ceil(len(idx) / per_gpu)
+            st["step_in_epoch"] = 0
+            yield ("epoch", idx)
+        left = st["steps_per_epoch"] - st["step_in_epoch"]
+        full_left = left - (1 if st["shard_len"] % per_gpu else 0)
+        if full_left > 0:
+            k = min(nsteps, full_left)
+            yield ("steps", per_gpu, k, spg)
+        else:
+            k = 1
+            yield ("steps", st["shard_len"] - (st["steps_per_epoch"] - 1) * per_gpu, 1, 1)
+        st["step_in_epoch"] += k
+        nsteps -= k
+
+
+def precapture(engine, events, use_graph: bool) -> None:
+    """Capture (and upload) every hipGraph the planned steps will replay, without running one."""
+    for ev in events:
+        if ev[0] == "steps":
+            engine.prepare(ev[1], ev[2], use_graph=use_graph, steps_per_graph=ev[3])
+
+
+def _self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start N fresh rank processes through torch.distributed.run
+    (rendezvous on 127.0.0.1, a free port) and return its exit code. The parent never touches the
+    GPU (no HIP init, no exec); rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _emit(out, rank, args):
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+
+
+def bench_cpu(args, world, rank):
+    """BASELINE config 1 (tiny/default LeNet on CPU, gloo): plumbing path with stock torch ops,
+    the native DDP bucket engine over gloo and the flat optimizer's CPU implementation."""
+    import torch
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(args.seed)
+    model = MLModel(args.model)
+    fwd = DistributedDataParallel(model) if world > 1 else model
+    opt = build_optimizer(args.optimizer, model.parameters(), lr=1e-3, momentum=0.9, weight_decay=0.0,
+                          flat=fwd.flat if world > 1 else None)
+    per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
+    g = torch.Generator().manual_seed(1234 + rank)
+    xs = torch.randn(4, per_gpu, 3, 32, 32, generator=g)
+    ys = torch.randint(0, 10, (4, per_gpu), generator=g)
+    loss_acc = torch.zeros(())
+
+    def run(n, start):
+        for i in range(n):
+            opt.zero_grad(set_to_none=False)
+            loss = F.cross_entropy(fwd(xs[(start + i) % 4]), ys[(start + i) % 4])
+            loss.backward()
+            opt.step()
+            loss_acc.add_(loss.detach())
+
+    run(args.warmup, 0)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = per_gpu * world * args.steps / elapsed
+    return {
+        "metric": "samples/sec/node", "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak" if args.scaling == "weak" else "strong",
+        "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2), "dtype": "fp32",
+        "data": "synthetic CIFAR-shaped float tensors, random-init weights",
+        "config": {"model": f"src/model.py MLModel ({args.model})", "device": "cpu",
+                   "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
+                   "parallelism": f"dp{world}", "backend": dist.get_backend() if world > 1 else "none",
+                   "loss_finite": math.isfinite(float(loss_acc))},
+    }
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args))
     import torch
     import torch.distributed as dist
 
@@ -165,17 +287,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    # rehearsal knobs for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
-    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring WORLD_SIZE ranks",
+              file=sys.stderr)
     backend = os.environ.get("MLT_BENCH_BACKEND", "nccl")
-    dev = torch.device("cuda", 0 if same_dev else local_rank)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
     if args.batch is None:
         # LeNet: the reference batch (src/trainer.py / main.py: 32). Transformer configs: micro-batches
         # sized for 288 GB of HBM per GPU (per-GPU throughput keeps rising with the micro-batch:
@@ -183,16 +297,32 @@ def main():
         # config 5 "sized to fill HBM", 551 / 768 / 809 / 840 at 16 / 64 / 128 / 256 using 126 GiB)
         args.batch = {"bert-base": 128, "bert-large": 128, "large": 256, "bert-tiny": 32}.get(args.model, 32)
 
+    if args.device == "cpu" or not torch.cuda.is_available():
+        if world > 1:
+            dist.init_process_group("gloo")
+        if args.steps == 3000 and args.warmup == 300:
+            args.steps, args.warmup = 50, 5
+        _emit(bench_cpu(args, world, rank), rank, args)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # rehearsal knob for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
+    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
+    dev = torch.device("cuda", 0 if same_dev else local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        world = dist.get_world_size()
+
     if args.model in ("bert-base", "bert-tiny", "bert-large", "large"):
         if args.steps == 3000 and args.warmup == 300:  # LeNet-sized defaults -> BERT-sized
             args.steps, args.warmup = 20, 5
-        out = bench_bert(args, world, rank, dev)
-        if rank == 0:
-            line = json.dumps(out)
-            print(line, flush=True)
-            if args.json_out:
-                with open(args.json_out, "w") as f:
-                    f.write(line + "\n")
+        _emit(bench_bert(args, world, rank, dev), rank, args)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
@@ -212,6 +342,10 @@ def main():
     opt = build_optimizer(args.optimizer, model.parameters(), lr=1e-3, momentum=0.9, weight_decay=0.0, flat=flat)
     per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
     engine = LeNetStepEngine(model, flat, max_batch=per_gpu, optimizer=opt, world_size=world, seed=args.seed)
+    if os.environ.get("MLT_BENCH_FORCE_RCCL") == "1" and world == 1:
+        # W=1 rehearsal of the data-parallel step: real ncclAllReduce inside the captured graph
+        C = engine.C
+        engine.use_transport(comm=C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index))
 
     # Synthetic CIFAR-10-shaped dataset (uint8 HWC) resident in HBM; random labels.
     N = args.dataset_size
@@ -219,59 +353,57 @@ def main():
     data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
     targets = torch.randint(0, 10, (N,), dtype=torch.int64, device=dev, generator=g)
     engine.set_dataset(data, targets, batch_size=per_gpu, augment=True)
+    # graphs of up to 64 steps: one replay covers a short timed run, long runs amortise launches
+    spg = args.steps_per_graph or max(1, min(64, args.steps))
+    use_graph = not args.no_graph
 
-    state = {"epoch": 0, "steps_left": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}
-
-    def new_epoch():
-        idx = shard_indices(N, world, rank, shuffle=True, seed=0, epoch=state["epoch"])
-        state["epoch"] += 1
-        state["shard_len"] = len(idx)
-        state["steps_per_epoch"] = math.ceil(len(idx) / per_gpu)
-        state["step_in_epoch"] = 0
-        engine.start_epoch(torch.as_tensor(idx, dtype=torch.int32))
+    state = {"epoch": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}
 
     def run(nsteps: int) -> int:
-        """Run nsteps training steps (crossing epochs as needed); return samples processed on this rank."""
+        """Run nsteps training steps; return samples processed on this rank."""
         samples = 0
-        while nsteps > 0:
-            if state["step_in_epoch"] >= state["steps_per_epoch"]:
-                new_epoch()
-            left = state["steps_per_epoch"] - state["step_in_epoch"]
-            full_left = left - (1 if state["shard_len"] % per_gpu else 0)
-            if full_left > 0:
-                k = min(nsteps, full_left)
-                engine.train_steps(per_gpu, k, use_graph=not args.no_graph, steps_per_graph=args.steps_per_graph)
-                samples += k * per_gpu
+        for ev in lenet_plan(nsteps, state, N, world, rank, per_gpu, spg, shard_indices):
+            if ev[0] == "epoch":
+                engine.start_epoch(torch.as_tensor(ev[1], dtype=torch.int32))
             else:
-                k = 1
-                last = state["shard_len"] - (state["steps_per_epoch"] - 1) * per_gpu
-                engine.train_steps(last, 1, use_graph=not args.no_graph, steps_per_graph=1)
-                samples += last
-            state["step_in_epoch"] += k
-            nsteps -= k
+                _, b, k, per_graph = ev
+                engine.train_steps(b, k, use_graph=use_graph, steps_per_graph=per_graph)
+                samples += b * k
         return samples
 
     run(args.warmup)
+    # capture + upload every hipGraph the timed steps replay (no step runs here), so the timed
+    # region holds exactly K steps of replays and nothing else
+    precapture(engine, lenet_plan(args.steps, dict(state), N, world, rank, per_gpu, spg, shard_indices), use_graph)
+    captures_before = engine.captures
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     samples = run(args.steps)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if engine.captures != captures_before:
+        raise RuntimeError("a hipGraph was captured inside the timed region")
+    device_s = ev0.elapsed_time(ev1) / 1e3
 
-    tot = torch.tensor([elapsed, float(samples)], dtype=torch.float64,
+    tot = torch.tensor([elapsed, float(samples), device_s], dtype=torch.float64,
                        device=dev if backend == "nccl" else torch.device("cpu"))
     if world > 1:
         t_max = tot[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         s_sum = tot[1:2].clone()
         dist.all_reduce(s_sum, op=dist.ReduceOp.SUM)
-        elapsed, total_samples = float(t_max.item()), float(s_sum.item())
+        d_max = tot[2:3].clone()
+        dist.all_reduce(d_max, op=dist.ReduceOp.MAX)
+        elapsed, total_samples, device_s = float(t_max.item()), float(s_sum.item()), float(d_max.item())
     else:
         total_samples = float(samples)
     # sanity: training actually ran (finite loss accumulated on device); transport healthy
@@ -296,17 +428,14 @@ def main():
                    else f"src/model.py MLModel ({args.model})",
                    "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
-                   "hipgraph_steps": 0 if args.no_graph else args.steps_per_graph,
+                   "hipgraph_steps": 0 if args.no_graph else spg,
+                   "device_ms_per_step": round(device_s / args.steps * 1e3, 5),
                    "dp_transport": engine.dp_transport,
+                   "comm_ranks": engine.comm.size if engine.comm is not None else None,
                    "transport_ms": getattr(engine, "transport_times_ms", None),
                    "loss_finite": math.isfinite(loss_sum)},
     }
-    if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+    _emit(out, rank, args)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -63,7 +63,8 @@ class TrainerOptions:
     # --- fault tolerance / checkpoints ---------------------------------------------------
     resume: bool = False                  # reload model.pth + trainer_state.pt from model_dir
     save_trainer_state: bool = True       # write trainer_state.pt (optimizer/scheduler/epoch/RNG) per epoch
-    watchdog_s: float = 0.0               # >0: abort if a step makes no progress for this long
+    watchdog_s: Optional[float] = None    # >0: abort if no step progress this long / a collective fails
+                                          # (None: 600 s for multi-rank jobs, off otherwise; 0: off)
     fault_inject_step: int = -1           # testing: raise at this global step on rank fault_inject_rank
     fault_inject_rank: int = 0
     # --- observability -------------------------------------------------------------------

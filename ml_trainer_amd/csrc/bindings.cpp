@@ -727,6 +727,8 @@ class PyXgmi {
     x_.launch(t.data_ptr<float>(), t.numel(), average ? 1.f / x_.world() : 1.f, cur_stream());
   }
   unsigned error() const { return x_.error(); }
+  void set_timeout_ms(long long ms) { x_.set_timeout_ms(ms); }
+  long long timeout_ms() const { return x_.timeout_ms(); }
   XgmiAllReduce& raw() { return x_; }
 
  private:
@@ -942,7 +944,7 @@ class LeNetEngine {
         xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s, &post);
         return;
       }
-      if (comm && comm->size() > 1)
+      if (comm)  // (size 1 too: the W=1 RCCL rehearsal captures a real ncclAllReduce)
         comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
       // ctrl[0] = steps taken (already advanced by the backward kernel) -> Adam t; ctrl[1] -> lr table index
       launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
@@ -1080,7 +1082,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("handle", &PyXgmi::handle)
       .def("open", &PyXgmi::open)
       .def("all_reduce", &PyXgmi::all_reduce, py::arg("tensor"), py::arg("average") = true)
-      .def("error", &PyXgmi::error);
+      .def("error", &PyXgmi::error)
+      .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms);
   py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)

@@ -26,8 +26,12 @@ XgmiAllReduce::XgmiAllReduce(int64_t cap_floats, int world, int rank, int device
   hcheck(hipSetDevice(device), "hipSetDevice");
   hcheck(hipExtMallocWithFlags(&region_, bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
   hcheck(hipMemset(region_, 0, bytes_), "hipMemset(region)");
-  hcheck(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(unsigned)), "hipMalloc(err)");
-  hcheck(hipMemset(err_, 0, sizeof(unsigned)), "hipMemset(err)");
+  // error word in coherent pinned host memory: the kernel ORs into it at system scope and the
+  // host reads it with a plain load after every replay (no device synchronisation)
+  hcheck(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(unsigned),
+                       hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc(err)");
+  *err_host_ = 0u;
+  hcheck(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_), err_host_, 0), "hipHostGetDevicePointer(err)");
   hcheck(hipMalloc(reinterpret_cast<void**>(&seqs_), sizeof(uint64_t) * blocks), "hipMalloc(seqs)");
   hcheck(hipMemset(seqs_, 0, sizeof(uint64_t) * blocks), "hipMemset(seqs)");
   hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -39,7 +43,7 @@ XgmiAllReduce::~XgmiAllReduce() {
   for (int q = 0; q < world_; ++q)
     if (q != rank_ && peer_base_[q]) (void)hipIpcCloseMemHandle(peer_base_[q]);
   if (region_) (void)hipFree(region_);
-  if (err_) (void)hipFree(err_);
+  if (err_host_) (void)hipHostFree(err_host_);
   if (seqs_) (void)hipFree(seqs_);
   delete static_cast<XgmiPeers*>(peers_host_);
 }
@@ -77,13 +81,16 @@ void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st, 
   if (!opened_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (n > cap_) throw std::runtime_error("xgmi: vector larger than the region capacity");
   launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale, err_,
-                        post, st);
+                        timeout_ms_ * 100000LL, post, st);  // 100 MHz constant clock: 1e5 ticks per ms
 }
 
 unsigned XgmiAllReduce::error() const {
-  unsigned e = 0;
-  hcheck(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "hipMemcpy(err)");
-  return e;
+  return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
+}
+
+void XgmiAllReduce::set_timeout_ms(long long ms) {
+  if (ms < 1 || ms > 3600LL * 1000) throw std::runtime_error("xgmi: timeout must be in [1 ms, 1 h]");
+  timeout_ms_ = ms;
 }
 
 }  // namespace mlt

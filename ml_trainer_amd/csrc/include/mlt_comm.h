@@ -59,7 +59,11 @@ class XgmiAllReduce {
   // in-place average (scale = 1/W) or sum of grad[0:n) across the ranks (every rank must make
   // the same sequence of calls)
   void launch(float* grad, int64_t n, float scale, hipStream_t st, const struct XgmiPostOpt* post = nullptr);
-  unsigned error() const;  // nonzero after a peer wait timed out
+  // nonzero once a peer wait timed out (sticky; a plain host read of mapped memory, no sync)
+  unsigned error() const;
+  // peer-wait timeout; graphs captured earlier keep the value they were captured with
+  void set_timeout_ms(long long ms);
+  long long timeout_ms() const { return timeout_ms_; }
   int world() const { return world_; }
   int64_t capacity() const { return cap_; }
 
@@ -69,7 +73,9 @@ class XgmiAllReduce {
   void* region_ = nullptr;
   size_t bytes_ = 0;
   void* peer_base_[8] = {nullptr};
-  unsigned* err_ = nullptr;
+  unsigned* err_ = nullptr;       // device alias of err_host_
+  unsigned* err_host_ = nullptr;  // coherent pinned host word
+  long long timeout_ms_ = 2000;
   uint64_t* seqs_ = nullptr;
   bool opened_ = false;
   void* peers_host_ = nullptr;  // XgmiPeers

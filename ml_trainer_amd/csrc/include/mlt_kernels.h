@@ -163,7 +163,8 @@ struct XgmiPostOpt {
   const int64_t* step_ptr;
 };
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
-                           uint64_t* seqs, float scale, unsigned* err, const XgmiPostOpt* post, hipStream_t st);
+                           uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
+                           const XgmiPostOpt* post, hipStream_t st);
 
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,

@@ -8,13 +8,19 @@
 //   1. copy its slice of the local gradient into data[p] of its own region, fence (system);
 //   2. store seq into flags[p][b][me] of EVERY peer's region (remote release stores);
 //   3. spin on its own flags[p][b][*] until all W peers published seq (system acquire loads,
-//      bounded by a 2 s wall-clock timeout that raises an error word instead of hanging);
+//      bounded by a wall-clock timeout);
 //   4. sum slice b over the W regions in rank order (same order on every rank -> bit-identical
 //      results everywhere), scale (1/W for AVG), write the local gradient.
 // No second barrier: a rank can only reach step s+2 (and overwrite parity p) after it saw all
 // peers publish step s+1, and a peer publishes s+1 only after its step-s kernel -- including
 // its reads of parity p -- completed (stream order). seq is a per-block device launch counter
 // (monotonic, never reset), so the kernel is replay-safe inside multi-step hipGraphs.
+// Failure: a wait that exceeds the timeout sets the sticky error word (host-mapped, so the
+// host polls it after every graph replay without a device sync) and the block returns WITHOUT
+// reducing or updating -- no step ever runs on partial peer data. Every later launch on this
+// rank sees the word and returns at once (it stops publishing), so every peer times out too and
+// the whole job fails loudly instead of training divergent replicas; the parity argument
+// above no longer matters because no launch after the error touches gradients or weights.
 // With POST the averaged gradient slice is consumed right away by the flat optimizer update
 // (the data-parallel step then needs no separate optimizer launch).
 #include "mlt_common.h"
@@ -27,8 +33,13 @@ template <bool POST>
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__ grad, int64_t n, XgmiPeers P,
                                                              int rank, int W, int64_t cap,
                                                              uint64_t* __restrict__ seqs, float scale,
-                                                             unsigned* __restrict__ err, XgmiPostOpt O) {
+                                                             unsigned* __restrict__ err, long long timeout,
+                                                             XgmiPostOpt O) {
   const int G = gridDim.x, b = blockIdx.x;
+  __shared__ int failed;
+  if (threadIdx.x == 0) failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  __syncthreads();
+  if (failed) return;  // an earlier launch timed out: this rank no longer takes steps
   const uint64_t seq = seqs[b] + 1;  // per-block launch counter: identical on every block and rank
   const int p = (int)(seq & 1);
   const int64_t chunk = ((n + G - 1) / G + 3) & ~(int64_t)3;  // float4 granules
@@ -54,14 +65,16 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
     uint64_t* f = P.flags[rank] + ((int64_t)p * G + b) * W + threadIdx.x;
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-      if (wall_clock64() - t0 > 200000000LL) {  // 2 s at the 100 MHz constant clock
-        atomicOr(err, 1u);
+      if (wall_clock64() - t0 > timeout) {  // wall_clock64 ticks at the 100 MHz constant clock
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        failed = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
+  if (failed) return;  // partial peer data: leave gradient, weights and the launch counter alone
   // 4. reduce in rank order (+ optimizer update)
   float lr = 0.f, tstep = 0.f;
   bool has_s1 = false, has_s2 = false;
@@ -120,14 +133,15 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
 }
 
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
-                           uint64_t* seqs, float scale, unsigned* err, const XgmiPostOpt* post, hipStream_t st) {
+                           uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
+                           const XgmiPostOpt* post, hipStream_t st) {
   if (n <= 0) return;
   if (post)
     hipLaunchKernelGGL(xgmi_allreduce_kernel<true>, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs,
-                       scale, err, *post);
+                       scale, err, timeout_ticks, *post);
   else
     hipLaunchKernelGGL(xgmi_allreduce_kernel<false>, dim3(blocks), dim3(256), 0, st, grad, n, P, rank, W, cap, seqs,
-                       scale, err, XgmiPostOpt{});
+                       scale, err, timeout_ticks, XgmiPostOpt{});
 }
 
 }  // namespace mlt

@@ -29,6 +29,9 @@ void HipGraph::capture(const std::function<void(hipStream_t)>& body) {
   hip_check(hipGetLastError(), "launch during capture");
   hip_check(hipGraphGetNodes(graph_, nullptr, &nodes_), "hipGraphGetNodes");
   hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+  // upload now so the first replay costs what every later one does
+  hip_check(hipGraphUpload(exec_, cap_stream_), "hipGraphUpload");
+  hip_check(hipStreamSynchronize(cap_stream_), "hipStreamSynchronize(upload)");
 }
 
 void HipGraph::launch(hipStream_t stream) {

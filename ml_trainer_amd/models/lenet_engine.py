@@ -37,6 +37,10 @@ CIFAR_MEAN = (0.4914, 0.4822, 0.4465)
 CIFAR_STD = (0.2023, 0.1994, 0.2010)
 
 
+class TransportError(RuntimeError):
+    """The data-parallel gradient collective failed (peer timeout / RCCL async error)."""
+
+
 class LeNetStepEngine:
     def __init__(self, model: MLModel, flat: FlatParams, max_batch: int, optimizer=None, process_group=None,
                  world_size: int = 1, seed: int = 0):
@@ -66,6 +70,7 @@ class LeNetStepEngine:
         self.offsets = [flat.segment(p)[0] for p in params]
         self.comm = None
         self.xgmi = None
+        self.captures = 0  # hipGraphs captured so far (bench asserts none inside its timed region)
         self.dp_transport = "none" if self.world_size == 1 else "torch.distributed"
         if self.world_size > 1:
             self._setup_transport(process_group)
@@ -122,11 +127,26 @@ class LeNetStepEngine:
             self.eng.set_comm(self.comm)
             self.dp_transport = "rccl"
 
+    def _poll_transport(self) -> None:
+        """Non-blocking health check of the in-graph collective, run after every graph replay:
+        the xGMI kernel's sticky error word lives in mapped host memory and RCCL reports through
+        ncclCommGetAsyncError, so neither read synchronises the device. A failure aborts the
+        communicator (unblocking any stuck collective) and raises TransportError."""
+        if self.dp_transport == "xgmi-oneshot" and self.xgmi is not None:
+            if self.xgmi.error():
+                raise TransportError("xGMI all-reduce: a peer did not arrive within "
+                                     f"{self.xgmi.timeout_ms} ms; the step was not applied")
+        elif self.dp_transport == "rccl" and self.comm is not None:
+            err = self.comm.async_error()
+            if err:
+                self.comm.abort()
+                raise TransportError(f"RCCL communicator failed: {err}")
+
     def check_transport(self) -> None:
-        """Raise if the one-shot all-reduce ever timed out waiting for a peer (its kernel never
-        hangs: after 2 s it flags the error and continues with incomplete data)."""
-        if self.dp_transport == "xgmi-oneshot" and self.xgmi is not None and self.xgmi.error():
-            raise RuntimeError("xGMI all-reduce: a peer did not arrive within the timeout; gradients are invalid")
+        """Blocking health check: wait for the queued steps, then poll (see _poll_transport)."""
+        if self.in_graph_collective:
+            torch.cuda.current_stream(self.device).synchronize()
+            self._poll_transport()
 
     def set_optimizer(self, optimizer, lr_table_len: int = 0) -> None:
         self.optimizer = optimizer
@@ -183,7 +203,24 @@ class LeNetStepEngine:
     # ------------------------------------------------------------------ steps
     @property
     def fused(self) -> bool:
-        return self.world_size == 1
+        """Single-rank step with the optimizer fused into the backward kernels."""
+        return self.world_size == 1 and self.dp_transport == "none"
+
+    def use_transport(self, comm=None, xgmi=None) -> None:
+        """Route the step's gradient through ``comm`` (a ``_C.Communicator``) or ``xgmi`` inside
+        the captured graph -- also at world size 1, which rehearses the data-parallel step (RCCL
+        all-reduce + flat optimizer launch) on a single GPU."""
+        if (comm is None) == (xgmi is None):
+            raise ValueError("pass exactly one of comm / xgmi")
+        self.comm, self.xgmi = comm, xgmi
+        if comm is not None:
+            self.eng.set_xgmi(None)
+            self.eng.set_comm(comm)
+            self.dp_transport = "rccl"
+        else:
+            self.eng.set_comm(None)
+            self.eng.set_xgmi(xgmi)
+            self.dp_transport = "xgmi-oneshot"
 
     @property
     def in_graph_collective(self) -> bool:
@@ -196,6 +233,33 @@ class LeNetStepEngine:
             return base | C.LENET_OPT
         return base | (C.LENET_REDUCE if self.in_graph_collective else 0)
 
+    def graph_shapes(self, B: int, n: int, use_graph: bool = True, steps_per_graph: int = 8):
+        """The (mode, B, nsteps) hipGraphs ``train_steps(B, n, ...)`` replays, in order (empty
+        without graphs). Lets a caller capture them all before a timed region."""
+        if not use_graph or n <= 0:
+            return []
+        mode = self._train_mode()
+        if not (self.fused or self.in_graph_collective):
+            return [(mode, B, 1)]
+        k = max(1, min(steps_per_graph, n))
+        full, rem = divmod(n, k)
+        return ([(mode, B, k)] if full else []) + ([(mode, B, rem)] if rem else [])
+
+    def prepare(self, B: int, n: int, use_graph: bool = True, steps_per_graph: int = 8) -> int:
+        """Capture (and upload) every graph ``train_steps(B, n, ...)`` needs without running a
+        step. Returns the number of graphs newly captured."""
+        new = 0
+        for shape in self.graph_shapes(B, n, use_graph, steps_per_graph):
+            new += self._ensure_graph(*shape)
+        return new
+
+    def _ensure_graph(self, mode: int, B: int, k: int) -> int:
+        if self.eng.has_graph(mode, B, k):
+            return 0
+        self.eng.capture(mode, B, k)
+        self.captures += 1
+        return 1
+
     def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8) -> None:
         """Run ``n`` full training steps of batch ``B`` from the device dataset."""
         mode = self._train_mode()
@@ -206,14 +270,15 @@ class LeNetStepEngine:
                 return
             k = max(1, min(steps_per_graph, n))
             full, rem = divmod(n, k)
-            if full and not self.eng.has_graph(mode, B, k):
-                self.eng.capture(mode, B, k)
+            if full:
+                self._ensure_graph(mode, B, k)
             for _ in range(full):
                 self.eng.replay(mode, B, k)
+                self._poll_transport()
             if rem:
-                if not self.eng.has_graph(mode, B, rem):
-                    self.eng.capture(mode, B, rem)
+                self._ensure_graph(mode, B, rem)
                 self.eng.replay(mode, B, rem)
+                self._poll_transport()
             return
         for _ in range(n):
             self._dist_step(mode, B, use_graph)
@@ -221,8 +286,7 @@ class LeNetStepEngine:
     def _dist_step(self, mode: int, B: int, use_graph: bool) -> None:
         import torch.distributed as dist
         if use_graph:
-            if not self.eng.has_graph(mode, B, 1):
-                self.eng.capture(mode, B, 1)
+            self._ensure_graph(mode, B, 1)
             self.eng.replay(mode, B, 1)
         else:
             self.eng.run(mode, B)

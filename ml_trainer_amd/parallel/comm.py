@@ -73,6 +73,7 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     x, ok = None, True
     try:
         x = C.XgmiAllReduce(int(capacity), world, rank, dev.index)
+        x.timeout_ms = int(os.environ.get("MLT_XGMI_TIMEOUT_MS", "2000"))
         h = x.handle()
     except RuntimeError:
         ok, h = False, b""

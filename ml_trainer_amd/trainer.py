@@ -55,7 +55,7 @@ from ml_trainer_amd.utils import checkpoint as ckpt
 from ml_trainer_amd.utils.flat import FlatParams
 from ml_trainer_amd.utils.functions import custom_loss_function
 from ml_trainer_amd.utils.logging import get_logger
-from ml_trainer_amd.utils.profiling import range_ctx
+from ml_trainer_amd.utils.profiling import StepTimer, range_ctx
 from ml_trainer_amd.utils.watchdog import Watchdog
 
 logger = get_logger("__name__")  # the reference names its logger with the literal string (src/trainer.py:19)
@@ -206,7 +206,10 @@ class Trainer:
         self._val_engine = None
         self._dev_train: Optional[DeviceDataset] = None
         self._dev_val: Optional[DeviceDataset] = None
-        self._watchdog = Watchdog(self.opts.watchdog_s) if self.opts.watchdog_s > 0 else None
+        wd = self.opts.watchdog_s
+        if wd is None:  # default: on for multi-rank jobs (a dead peer must not hang the others)
+            wd = 600.0 if (self.is_parallel and mdist.world_size() > 1) else 0.0
+        self._watchdog = Watchdog(wd) if wd > 0 else None
         if self.opts.resume:
             self._resume()
 
@@ -307,6 +310,12 @@ class Trainer:
                                      augment=True, pad=s["pad"], flip=s["flip"], mean=s["mean"], std=s["std"],
                                      perm_capacity=n_idx)
             self._engine.ctrl[0:1].fill_(self.global_step)
+            eng = self._engine
+            if self._watchdog is not None and eng.comm is not None and eng.dp_transport == "rccl":
+                self._watchdog.add_probe(eng.comm.async_error, eng.comm.abort)
+            if self._watchdog is not None and eng.xgmi is not None and eng.dp_transport == "xgmi-oneshot":
+                x = eng.xgmi
+                self._watchdog.add_probe(lambda: "xGMI all-reduce peer timeout" if x.error() else "")
         return self._engine
 
     def _get_val_engine(self):
@@ -384,15 +393,12 @@ class Trainer:
         if self.train_sampler is not None:
             self.train_sampler.set_epoch(epoch)  # B11 fix
         n = len(self.train_loader)
-        t0 = time.perf_counter()
-        with range_ctx(f"train_epoch_{epoch}", self.opts.profile_ranges):
+        with StepTimer(self.device) as tm, range_ctx(f"train_epoch_{epoch}", self.opts.profile_ranges):
             if self._engine_eligible():
                 loss, metric, samples = self._engine_train_epoch(epoch, n)
             else:
                 loss, metric, samples = self._generic_train_epoch(epoch, n)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        dt = tm.wall_ms / 1e3
         if self.scheduler_type == "StepLR":
             self.scheduler.step()
         if self.opts.global_metrics and mdist.is_dist():
@@ -403,7 +409,7 @@ class Trainer:
         rec = {"epoch": epoch, "train_time_s": dt, "steps": n, "samples_rank": samples,
                "samples_per_s_rank": samples / dt if dt > 0 else 0.0,
                "samples_per_s_node": samples * self.world_size / dt if dt > 0 else 0.0,
-               "ms_per_step": dt / max(n, 1) * 1e3}
+               "ms_per_step": dt / max(n, 1) * 1e3, "device_ms_per_step": tm.device_ms / max(n, 1)}
         self.throughput.append(rec)
         logger.info("train throughput", samples_per_s=round(rec["samples_per_s_node"], 1),
                     ms_per_step=round(rec["ms_per_step"], 4), epoch=epoch)
@@ -586,10 +592,8 @@ class Trainer:
             logger.warning("resume requested but no checkpoint found", model_dir=self.model_dir)
             return
         sd = torch.load(path, map_location="cpu", weights_only=True)
-        target = self.model
-        if not isinstance(target, DistributedDataParallel):
-            sd = ckpt.strip_module_prefix(sd)
-        target.load_state_dict(sd)
+        # checkpoints of wrapped (module.-prefixed) and unwrapped runs both resume either way
+        self._core.load_state_dict(ckpt.strip_module_prefix(sd))
         if self.flat is not None:
             self.flat.rebind_params()
         if self._zero is not None:
@@ -645,12 +649,14 @@ class Trainer:
                 logger.info(f"{'-' * 30} EPOCH {epoch} / {self.epochs} {'-' * 30}")
                 self._train_one_epoch(epoch)
                 self.clear()
-                self._validate_one_epoch()
+                with self._no_step_phase():
+                    self._validate_one_epoch()
                 self.clear()
                 if self.scheduler_type == "ReduceLROnPlateau":
                     self.scheduler.step(self.val_losses[-1])  # B8 fix: the reference never steps it
-                self._determinism_check()
-                self._checkpoint(epoch)
+                with self._no_step_phase():
+                    self._determinism_check()
+                    self._checkpoint(epoch)
                 if self.metric:
                     logger.info(f"train loss: {self.train_losses[-1]} - "
                                 f"train {self.metric}: {self.train_metrics[-1]}")
@@ -697,9 +703,9 @@ class Trainer:
             if kwarg not in allowed_kwargs:
                 raise TypeError(error_message, kwarg)
 
-    # aliases named after the reference's private API
-    def _train_one_epoch_alias(self, epoch):  # pragma: no cover - kept for discoverability
-        return self._train_one_epoch(epoch)
+    def _no_step_phase(self):
+        """Validation / checkpoint: pause the watchdog's no-progress timer (probes stay on)."""
+        return self._watchdog.paused() if self._watchdog is not None else _nullctx()
 
 
 class _nullctx:

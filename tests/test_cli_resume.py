@@ -99,3 +99,38 @@ def test_cli_bert_tiny_cpu(tmp_path):
     import torch
     sd = torch.load(out / "model.pth", weights_only=True)
     assert "layers.0.qkv.weight" in sd
+
+
+def test_watchdog_probe_aborts_and_pause():
+    fired, aborted = [], []
+    health = {"err": ""}
+    w = Watchdog(0.2, on_timeout=lambda: fired.append(1), poll_s=0.05)
+    w.add_probe(lambda: health["err"], lambda: aborted.append(1))
+    w.start()
+    with w.paused():  # validation / checkpoint: no steps, no firing
+        time.sleep(0.5)
+    assert not fired
+    health["err"] = "ncclRemoteError"
+    time.sleep(0.3)
+    w.stop()
+    assert fired and aborted and w.reason == "ncclRemoteError"
+
+
+def test_resume_across_wrapped_and_unwrapped(tmp_path):
+    """A checkpoint of an unwrapped run resumes under DDP keys and vice versa (module. prefix)."""
+    from ml_trainer_amd.utils import checkpoint as ckpt
+    tr, va = TensorCifar(64, 0), TensorCifar(32, 1)
+    opts = {"progress": False}
+    torch.manual_seed(5)
+    a = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=1, batch_size=32, model_dir=str(tmp_path),
+                options=opts)
+    a.fit()
+    sd = torch.load(tmp_path / "model.pth", weights_only=True)
+    assert not any(k.startswith("module.") for k in sd)
+    torch.save({"module." + k: v for k, v in sd.items()}, tmp_path / "model.pth")  # as a DDP run writes it
+    b = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=2, batch_size=32, model_dir=str(tmp_path),
+                options={**opts, "resume": True})
+    assert b.start_epoch == 2
+    for k, v in b._core.state_dict().items():
+        assert torch.equal(v, sd[k])
+    assert ckpt.strip_module_prefix({"module.x": 1, "y": 2}) == {"x": 1, "y": 2}

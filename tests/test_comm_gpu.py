@@ -1,0 +1,178 @@
+"""The native collectives on hardware (reference src/trainer.py:59,98):
+
+* the RCCL ``Communicator`` at world size 1 on the box's GPU -- every collective against its
+  torch-computed expectation, plus the health query;
+* the LeNet data-parallel step with a real ``ncclAllReduce`` captured inside multi-step
+  hipGraphs (W=1 rehearsal of the 8-GPU path) against the fused single-rank step;
+* the one-shot xGMI all-reduce failing loudly and fail-stop when a peer never arrives
+  (two processes on the one GPU, gloo rendezvous).
+"""
+import os
+import tempfile
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import dist_env, free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _comm(dev):
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    return C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index)
+
+
+def test_rccl_world1_collectives(dev):
+    c = _comm(dev)
+    assert c.size == 1 and c.rank == 0 and c.async_error() == ""
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(1 << 20, device=dev, generator=g)
+    for op in ("sum", "avg", "max", "min"):
+        t = x.clone()
+        c.all_reduce(t, op)
+        torch.testing.assert_close(t, x, rtol=0, atol=0)
+    xb = x.to(torch.bfloat16)
+    tb = xb.clone()
+    c.all_reduce(tb, "sum")
+    assert torch.equal(tb, xb)
+    out = torch.empty_like(x)
+    c.reduce_scatter(x, out, "sum")
+    assert torch.equal(out, x)
+    out.zero_()
+    c.all_gather(x, out)
+    assert torch.equal(out, x)
+    t = x.clone()
+    c.broadcast(t, 0)
+    assert torch.equal(t, x)
+    out.zero_()
+    c.all_to_all(x, out)
+    assert torch.equal(out, x)
+    i64 = torch.arange(1000, device=dev)
+    c.all_reduce(i64, "sum")
+    assert torch.equal(i64, torch.arange(1000, device=dev))
+    torch.cuda.synchronize()
+    assert c.async_error() == ""
+
+
+def _lenet_engine(dev, seed=0):
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(seed)
+    m = MLModel().to(dev)
+    flat = FlatParams(m.parameters())
+    opt = build_optimizer("sgd", m.parameters(), lr=1e-2, momentum=0.9, flat=flat)
+    eng = LeNetStepEngine(m, flat, max_batch=32, optimizer=opt)
+    g = torch.Generator().manual_seed(3)
+    N = 512
+    data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=g)
+    targets = torch.randint(0, 10, (N,), generator=g)
+    eng.set_dataset(data, targets, batch_size=32)
+    eng.start_epoch(torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32))
+    return eng, flat
+
+
+def test_lenet_step_with_rccl_allreduce_in_graph(dev):
+    """W=1 data-parallel step: backward -> ncclAllReduce(AVG) -> flat optimizer, 4-step graphs."""
+    ref, fref = _lenet_engine(dev)
+    ref.train_steps(32, 8, use_graph=True, steps_per_graph=4)
+    eng, flat = _lenet_engine(dev)
+    eng.use_transport(comm=_comm(dev))
+    assert eng.dp_transport == "rccl" and not eng.fused
+    eng.train_steps(32, 8, use_graph=True, steps_per_graph=4)
+    eng.check_transport()
+    assert eng.ctrl.tolist() == [8, 8]
+    assert eng.captures == 1
+    torch.testing.assert_close(flat.data, fref.data, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(eng.stats, ref.stats, rtol=1e-6, atol=1e-6)
+
+
+def _late_peer_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    os.environ["MLT_XGMI_TIMEOUT_MS"] = "300"
+    from ml_trainer_amd.models.lenet_engine import TransportError
+    from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
+    eng, flat = _lenet_engine(dev)
+    xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
+    assert xe is not None and xe.timeout_ms == 300
+    eng.use_transport(xgmi=xe)
+    eng.train_steps(32, 2, use_graph=True, steps_per_graph=1)  # both ranks: healthy steps
+    eng.check_transport()
+    dist.barrier()
+    res = {}
+    if rank == 0:  # rank 1 is now "dead": it never launches again
+        before = flat.data.clone()
+        t0 = time.time()
+        raised = False
+        try:
+            eng.train_steps(32, 1, use_graph=True, steps_per_graph=1)
+            eng.check_transport()
+        except TransportError:
+            raised = True
+        res["raised"] = raised
+        res["secs"] = time.time() - t0
+        res["unchanged"] = bool(torch.equal(flat.data, before))  # the failed step was not applied
+        t1 = time.time()
+        eng.train_steps(32, 3, use_graph=True, steps_per_graph=1)  # sticky: returns at once
+        torch.cuda.synchronize()
+        res["sticky_secs"] = time.time() - t1
+        res["still_unchanged"] = bool(torch.equal(flat.data, before))
+        torch.save(res, os.path.join(out_dir, "late.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_late_peer_fails_within_one_step():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_late_peer_worker, args=(2, free_port(), d), nprocs=2, join=True)
+        r = torch.load(os.path.join(d, "late.pt"), weights_only=True)
+    assert r["raised"], r
+    assert r["secs"] < 5.0, r
+    assert r["unchanged"] and r["still_unchanged"], r
+    assert r["sticky_secs"] < 1.0, r
+
+
+def _ddp_avg_worker(rank, world, port, out_dir):
+    """Native DDP on the GPU must AVERAGE: the synced gradient equals the mean of the ranks'
+    local gradients (no_sync backward of the same batch), not their sum."""
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(rank)
+    m = BertClassifier(bert_config("bert-tiny")).to(dev)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=1.0, first_bucket_mb=0.5)
+    g = torch.Generator().manual_seed(11 + rank)
+    ids = torch.randint(5, 1000, (2, 128), generator=g).to(dev)
+    y = torch.randint(0, 2, (2,), generator=g).to(dev)
+    ddp.flat.grad.zero_()
+    with ddp.no_sync():
+        F.cross_entropy(ddp(ids), y).backward()
+    local = ddp.flat.grad.clone()
+    ddp.flat.grad.zero_()
+    F.cross_entropy(ddp(ids), y).backward()
+    torch.cuda.synchronize()
+    torch.save({"local": local.cpu(), "synced": ddp.flat.grad.cpu()}, os.path.join(out_dir, f"a{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_gpu_averages_not_sums():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ddp_avg_worker, args=(2, free_port(), d), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"a{i}.pt"), weights_only=True) for i in range(2)]
+    mean = (r[0]["local"] + r[1]["local"]) / 2
+    assert not torch.equal(r[0]["local"], r[1]["local"])
+    for i in range(2):
+        torch.testing.assert_close(r[i]["synced"], mean, rtol=1e-5, atol=1e-7)
