@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--zero", type=int, default=0, choices=(0, 1),
                     help="BERT modes, N>1: 1 = ZeRO-1 sharded optimizer state instead of replicated DDP")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (BERT modes)")
+    ap.add_argument("--bucket-mb", type=float, default=None, help="BERT modes, N>1: DDP bucket cap (MB)")
+    ap.add_argument("--first-bucket-mb", type=float, default=None, help="BERT modes, N>1: first DDP bucket (MB)")
+    ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
+                    help="BERT modes, N>1: gradient all-reduce wire dtype (bf16 = cast in the bucket, reduce, "
+                         "cast back into the fp32 gradient)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="LeNet steps per captured hipGraph (0 = auto: min(steps, 64))")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
@@ -92,7 +97,8 @@ def bench_bert(args, world, rank, dev):
         opt = ddp.make_optimizer(FusedAdamW, lr=1e-4, weight_decay=0.01)
         fwd = ddp
     elif world > 1:
-        ddp = DistributedDataParallel(model)
+        ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+                                      comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, timing=True)
         opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, flat=ddp.flat)
         fwd = ddp
     else:
@@ -123,6 +129,8 @@ def bench_bert(args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+        if hasattr(ddp, "reset_comm_stats"):
+            ddp.reset_comm_stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps, args.warmup)
@@ -138,6 +146,13 @@ def bench_bert(args, world, rank, dev):
     elapsed = float(t.item())
     total = per_gpu * world * args.steps * accum
     value = total / elapsed
+    comm = None
+    if world > 1 and hasattr(ddp, "comm_stats"):
+        comm = ddp.comm_stats()  # hipEvent bucket timings (synchronises after the timed region)
+        vals = torch.tensor([comm.get("allreduce_ms", 0.0), comm.get("exposed_ms", 0.0)], dtype=torch.float64,
+                            device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        comm["allreduce_ms_max_rank"], comm["exposed_ms_max_rank"] = [round(float(v), 4) for v in vals.tolist()]
     return {
         "metric": "samples/sec/node",
         "value": round(value, 1),
@@ -160,6 +175,7 @@ def bench_bert(args, world, rank, dev):
                    "tokens_per_s": round(value * args.seq_len, 1),
                    "model_tflops": round(model.flops_per_token(args.seq_len) * value * args.seq_len / 1e12, 1),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+                   "ddp_comm": comm,
                    "loss_finite": math.isfinite(float(loss_acc.item()))},
     }
 
@@ -411,6 +427,18 @@ def main():
     engine.check_transport()
     value = total_samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    nodes = engine.eng.graph_nodes(engine._train_mode(), per_gpu, spg) if use_graph else 0
+    tt = getattr(engine, "transport_times_ms", None)
+    comm = None
+    if world > 1:
+        # the one 248 KB bucket is reduced inside the step's hipGraph between backward and the
+        # update (latency-bound, serial by construction): its cost is the standalone per-call time
+        # of the transport the engine chose, measured at set-up on every rank (max over ranks, the
+        # same vote that picked the transport)
+        key = {"xgmi-oneshot": "xgmi", "rccl": "rccl"}.get(engine.dp_transport)
+        comm = {"buckets": 1, "bucket_mb": [round(flat.numel * 4 / 2 ** 20, 3)], "comm_dtype": "float32",
+                "in_graph": engine.in_graph_collective, "overlap_pct": 0.0,
+                "allreduce_ms": round(tt[key], 4) if (tt and key in tt) else None}
     out = {
         "metric": "samples/sec/node",
         "value": round(value, 1),
@@ -429,6 +457,8 @@ def main():
                    "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
                    "hipgraph_steps": 0 if args.no_graph else spg,
+                   "kernels_per_step": round(nodes / spg, 2) if nodes else None,
+                   "ddp_comm": comm,
                    "device_ms_per_step": round(device_s / args.steps * 1e3, 5),
                    "dp_transport": engine.dp_transport,
                    "comm_ranks": engine.comm.size if engine.comm is not None else None,

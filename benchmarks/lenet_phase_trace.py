@@ -4,7 +4,7 @@ stamps at every phase boundary; printed as cycles and microseconds (calibrated a
 import os
 import sys
 
-os.environ.setdefault("MLT_LENET_FUSED", "1")  # LENET_TRACE stamps exist only in the fused kernel
+os.environ.setdefault("MLT_LENET_VARIANT", "1")  # LENET_TRACE stamps exist only in the fused kernel
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -1042,6 +1042,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);
   }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("set_gemm_split_mode", &set_gemm_split_mode, py::arg("mode"));
+  m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
+  m.def("get_lenet_variant", &get_lenet_variant);
   m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("fmt") = 0);
   m.def("fp8_amax", &fp8_amax);

@@ -12,6 +12,23 @@
 
 #define MLT_WAVE 64
 
+// Device-side index checks, compiled in by `python -m ml_trainer_amd.build --debug` (-DMLT_DEBUG)
+// and to nothing otherwise. A failed check prints the condition, the source line and the
+// block / thread and lets the kernel continue: no trap, because a trapping wave can take the
+// whole GPU (and its neighbours) down -- the printf is the evidence, the host checks the output.
+#ifdef MLT_DEBUG
+#define MLT_DCHECK(cond)                                                                          \
+  do {                                                                                            \
+    if (!(cond))                                                                                  \
+      printf("[mlt] MLT_DCHECK(%s) failed at %s:%d block (%d,%d,%d) thread %d\n", #cond, __FILE__, \
+             __LINE__, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);       \
+  } while (0)
+#else
+#define MLT_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 #define MLT_HIP_CHECK(expr)                                                          \
   do {                                                                               \
     hipError_t _e = (expr);                                                          \

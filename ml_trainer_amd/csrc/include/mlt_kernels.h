@@ -73,6 +73,8 @@ struct LeNetOpt {
 
 void launch_lenet(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                   hipStream_t stream);
+void set_lenet_variant(int v);  // 0 default (4 launches), 1 fully fused per-sample chain, 2 split conv2 / fc
+int get_lenet_variant();
 
 // Standalone GPU augmentation (RandomCrop(32,pad) + HFlip + ToTensor + Normalize) for the
 // generic (non-LeNet) device data path: out [B,3,32,32] fp32.

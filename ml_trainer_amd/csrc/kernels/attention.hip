@@ -117,6 +117,7 @@ __device__ __forceinline__ void block_coords(int S, int rows_per_block, int H, i
   rb = id % nrb;
   h = (id / nrb) % H;
   b = id / (nrb * H);
+  MLT_DCHECK((int)gridDim.x % (nrb * H) == 0 && rb * rows_per_block < S);  // grid = B * H * row blocks
 }
 
 // ---------------------------------------------------------------------------
@@ -135,6 +136,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   const int64_t ld = 3 * (int64_t)D;
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
+  MLT_DCHECK(len >= 0 && len <= S);
   int q[NQ];
   bf16x8 qf[NQ][2];  // Q fragments (B operand of K.Q^T): Q[q][32kh + 8g + j]
 #pragma unroll
@@ -937,6 +939,7 @@ __global__ __launch_bounds__(256) void attn_fwd_ring_kernel(const uint16_t* __re
   const int64_t ld = 3 * (int64_t)D;
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
+  MLT_DCHECK(len >= 0 && len <= S);
   int q[NQ];
   bf16x8 qf[NQ][2];
 #pragma unroll

@@ -152,6 +152,8 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
     tn = r / gsize;
   }
   const int m0 = tm * BM, n0 = tn * BN;
+  MLT_DCHECK(m0 < M && n0 < N && tiles % tiles_n == 0);  // tile grid = ceil(M/BM) x ceil(N/BN)
+  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && blockIdx.y * ksteps < (unsigned)(K / (F8A >= 0 ? 128 : T_BK)));
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = (wid / WARPS_N) * WTM, wn = (wid % WARPS_N) * WTN;
   constexpr bool F8 = F8A >= 0;
@@ -439,6 +441,8 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
     tn = r / gsize;
   }
   const int m0 = tm * BM, n0 = tn * BN;
+  MLT_DCHECK(m0 < M && n0 < N && tiles % tiles_n == 0);  // tile grid = ceil(M/BM) x ceil(N/BN)
+  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && blockIdx.y * ksteps < (unsigned)(K / (F8A >= 0 ? 128 : T_BK)));
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = K / (F8 ? 128 : T_BK);

@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
     int64_t pos = sie * aug.batch_stride + b;
     if (pos >= aug.perm_len) pos %= aug.perm_len;
     int64_t idx = aug.perm[pos];
+    MLT_DCHECK(idx >= 0 && idx < aug.n);  // release builds clamp a bad permutation entry
+    MLT_DCHECK(b < aug.batch_stride && pos < aug.perm_len);
     idx = idx < 0 ? 0 : (idx >= aug.n ? aug.n - 1 : idx);
     const uint64_t h = mix64(mix64(aug.seed + (uint64_t)step) ^ (uint64_t)pos);
     const int span = 2 * aug.pad + 1;
@@ -145,6 +147,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
   if (a10 > m) { m = a10; k = 2; }
   if (a11 > m) { m = a11; k = 3; }
   const int64_t o = ((int64_t)(b * D::C1 + oc) * 14 + py) * 14 + px;
+  MLT_DCHECK(oc < D::C1 && py < 14 && px < 14);
   p1[o] = m > 0.f ? m : 0.f;
   i1[o] = m > 0.f ? (uint8_t)k : (uint8_t)4;
 }
@@ -1440,28 +1443,31 @@ __global__ __launch_bounds__(256) void lenet_wgrad(int mode, LeNetPtrs P, LeNetO
 }
 
 // ---------------------------------------------------------------------------
+// Launch variant of the per-sample chain (set_lenet_variant; initial value from MLT_LENET_VARIANT):
+//   0 (default)  K1 conv1 -> KF from p1 (conv2 + fc chain) -> K4 -> K5       4 launches
+//   1            KF for the whole chain (K1..K4 fused)      -> K5            2 launches
+//   2            K1 -> K2 conv2 -> K3 fc chain -> K4 -> K5                  5 launches
+// Measured (MI355X, batch 32, bench.py): 0 is fastest -- one CU per sample leaves the fully fused
+// KF's conv phases LDS-latency bound (40-44 vs 33 us per step) and 2 pays one more boundary.
+// All three run the same arithmetic; tests/test_lenet_native.py checks each against autograd.
+static int g_lenet_variant = [] {
+  const char* v = getenv("MLT_LENET_VARIANT");
+  const int x = v ? atoi(v) : 0;
+  return (x >= 0 && x <= 2) ? x : 0;
+}();
+
+void set_lenet_variant(int v) { g_lenet_variant = (v >= 0 && v <= 2) ? v : 0; }
+int get_lenet_variant() { return g_lenet_variant; }
+
 template <class D>
 static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
   if (B <= 0) return;
   const float inv_B = 1.f / (float)B;
-  // MLT_LENET_FUSED=1 runs K1..K4 as the fused per-sample kernel KF in every mode (engine steps,
-  // evaluation and the autograd halves alike). Measured (MI355X, batch 32, bench.py): the
-  // four-kernel path is still faster (40.2 vs ~40-44 us per step): one CU per sample leaves
-  // KF's conv phases LDS-latency bound, so it stays opt-in.
-  static const bool fused_ok = [] {
-    const char* v = getenv("MLT_LENET_FUSED");
-    return v != nullptr && atoi(v) != 0;
-  }();
-  const bool fused = fused_ok && (mode & (LENET_FWD | LENET_CE | LENET_BWD));
+  const bool fused = g_lenet_variant == 1 && (mode & (LENET_FWD | LENET_CE | LENET_BWD));
   if (fused) {
     hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode, P, A, inv_B);
   } else {
-    // MLT_LENET_C2FC=0: conv2 (K2) and the fc chain (K3) as two launches instead of the fused
-    // per-sample conv2 -> fc kernel (KF from p1)
-    static const bool c2fc = [] {
-      const char* v = getenv("MLT_LENET_C2FC");
-      return v == nullptr || atoi(v) != 0;
-    }();
+    const bool c2fc = g_lenet_variant != 2;  // conv2 + fc chain as the per-sample KF launch (from p1)
     if (mode & LENET_FWD) {
       hipLaunchKernelGGL(lenet_conv1_fwd<D>, dim3(B, D::C1), dim3(256), 0, st, A, P.w1, P.b1, P.x, P.p1, P.i1,
                          A.data ? P.targets : nullptr, P.dtargets);
@@ -1491,11 +1497,16 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     constexpr int NR1 = (D::C1 * kTaps1 + 255) / 256, NR2 = (D::C2 * D::C1 * 25 + D::C2 + 255) / 256;
     const int nblk = k4wg ? NR1 + NR2  // K4 ran the fc roles too
                           : (B + kSpb1 - 1) / kSpb1 * D::C1 + D::C2 * D::C1 + NB3 + NB4 + NB5;
-    // MLT_LENET_WGRAD_SKIP=<mask> (profiling only): 1 conv1 / 2 conv2 / 4 fc roles return at once
+#ifdef MLT_DEBUG
+    // MLT_LENET_WGRAD_SKIP=<mask> (debug builds, role profiling only): 1 conv1 / 2 conv2 / 4 fc
+    // roles return at once -- never compiled into a release build, where it would skip training work
     static const int skip = [] {
       const char* v = getenv("MLT_LENET_WGRAD_SKIP");
       return v ? (atoi(v) & 7) : 0;
     }();
+#else
+    constexpr int skip = 0;
+#endif
     hipLaunchKernelGGL(lenet_wgrad<D>, dim3(nblk), dim3(256), 0, st, mode | (skip << 9) | k4wg, P, O, B, A.ctrl);
   }
 }

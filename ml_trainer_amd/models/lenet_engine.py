@@ -102,24 +102,31 @@ class LeNetStepEngine:
                 self.dp_transport = "xgmi-oneshot"
             return
         use_xgmi = False
+        t = self.flat.grad.clone()
+        cands = [("rccl", lambda: self.comm.all_reduce(t, "avg"))]
         if self.xgmi is not None:
-            t = self.flat.grad.clone()
-            times = []
-            for fn in (lambda: self.xgmi.all_reduce(t, True), lambda: self.comm.all_reduce(t, "avg")):
-                for _ in range(5):
-                    fn()
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(50):
-                    fn()
-                e.record()
-                e.synchronize()
-                times.append(s.elapsed_time(e) / 50)
-            decision = torch.tensor([1.0 if times[0] < times[1] else 0.0] + times, device=self.device)
-            dist.broadcast(decision, src=0 if process_group is None else dist.get_global_rank(process_group, 0),
-                           group=process_group)
-            use_xgmi = bool(decision[0].item() > 0.5)
-            self.transport_times_ms = {"xgmi": float(decision[1]), "rccl": float(decision[2])}
+            cands.insert(0, ("xgmi", lambda: self.xgmi.all_reduce(t, True)))
+        times = {}
+        for name, fn in cands:
+            for _ in range(5):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(50):
+                fn()
+            e.record()
+            e.synchronize()
+            times[name] = s.elapsed_time(e) / 50
+        # every rank votes with its own timings and health: the slowest rank decides (MAX), and
+        # an xGMI error word raised on ANY rank during the trial rules the one-shot kernel out
+        bad = 1.0 if (self.xgmi is not None and self.xgmi.error()) else 0.0
+        vote = torch.tensor([bad, times.get("xgmi", float("inf")), times["rccl"]], device=self.device)
+        dist.all_reduce(vote, op=dist.ReduceOp.MAX, group=process_group)
+        bad, tx, tr = (float(v) for v in vote.tolist())
+        use_xgmi = self.xgmi is not None and bad == 0.0 and tx < tr
+        self.transport_times_ms = {"rccl": tr, **({"xgmi": tx} if self.xgmi is not None else {})}
+        if self.xgmi is not None and bad != 0.0:
+            warnings.warn("xGMI one-shot all-reduce failed its timing trial on some rank; using RCCL")
         if use_xgmi:
             self.eng.set_xgmi(self.xgmi)
             self.dp_transport = "xgmi-oneshot"

@@ -20,7 +20,14 @@ SMDDP backend (``src/trainer.py:97-101``) and its dead manual
 * ``ReduceOp.AVG`` on RCCL (no separate divide kernel); gloo gets SUM + scale;
 * ``no_sync()`` skips communication for gradient accumulation;
 * ``mode='manual'``: one flat all-reduce after backward (the reference's
-  ``_average_gradients`` semantics, non-overlapped; A/B baseline).
+  ``_average_gradients`` semantics, non-overlapped; A/B baseline);
+* ``comm_dtype=torch.bfloat16``: each bucket is cast into a persistent bf16 image, reduced
+  in bf16 (half the xGMI bytes: BERT-base 220 MB instead of 440 MB per step) and cast back
+  into the fp32 gradient; the fp32 masters and the optimizer are unchanged;
+* ``timing=True``: hipEvents around every bucket's collective (on a dedicated high-priority
+  comm stream) and around forward/backward; :meth:`comm_stats` reports all-reduce device
+  time, the share of it hidden under backward (``overlap_pct``) and the bucket layout
+  (SURVEY.md §5.1 / §7.6 "all-reduce time, overlap %").
 
 ``state_dict()`` keys carry the ``module.`` prefix, exactly as the reference's
 DDP checkpoints.
@@ -28,7 +35,7 @@ DDP checkpoints.
 from __future__ import annotations
 
 import contextlib
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -43,7 +50,8 @@ DEFAULT_FIRST_BUCKET_MB = 4.0
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_parameters: bool = True,
-                 mode: str = "overlap", flat: Optional[FlatParams] = None):
+                 mode: str = "overlap", flat: Optional[FlatParams] = None,
+                 comm_dtype: Optional[torch.dtype] = None, timing: bool = False):
         super().__init__()
         if mode not in ("overlap", "manual"):
             raise ValueError("mode must be 'overlap' or 'manual'")
@@ -56,6 +64,18 @@ class DistributedDataParallel(nn.Module):
         self._bucket_cap = int((bucket_cap_mb or DEFAULT_BUCKET_MB) * 2 ** 20)
         self._first_cap = int((first_bucket_mb or DEFAULT_FIRST_BUCKET_MB) * 2 ** 20)
         self._build_buckets()
+        if comm_dtype is not None and comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("comm_dtype must be torch.float32 or torch.bfloat16")
+        self.comm_dtype = comm_dtype if comm_dtype != self.flat.grad.dtype else None
+        self._cbuf = (torch.zeros(self.flat.numel, dtype=self.comm_dtype, device=self.flat.device)
+                      if self.comm_dtype is not None else None)
+        self.timing = bool(timing)
+        cuda = self.flat.device.type == "cuda"
+        # collectives that need work of their own (casts, timing events) run on a side stream
+        self._comm_stream = (torch.cuda.Stream(device=self.flat.device, priority=-1)
+                             if cuda and (self.timing or self.comm_dtype is not None) else None)
+        self._step_rec: Optional[Dict] = None
+        self._records: List[Dict] = []
         self.require_sync = True
         self._works: List = []
         self._pending: List[int] = list(self._bucket_counts)
@@ -110,10 +130,50 @@ class DistributedDataParallel(nn.Module):
     def _reduce_bucket(self, bi: int, async_op: bool = True):
         s, e = self._buckets[bi]
         view = self.flat.grad[s:e]
+        if self._comm_stream is not None:
+            return self._reduce_bucket_side(bi, view)
+        if self._cbuf is not None:  # CPU / gloo with a narrower wire dtype: synchronous cast round trip
+            cv = self._cbuf[s:e]
+            cv.copy_(view)
+            dist.all_reduce(cv, op=dist.ReduceOp.SUM, group=self.process_group)
+            view.copy_(cv)
+            view.mul_(1.0 / self.world_size)
+            return None
         if self.backend == "nccl":
             return dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=async_op)
         w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.process_group, async_op=async_op)
         return (w, view)
+
+    def _reduce_bucket_side(self, bi: int, view: torch.Tensor):
+        """GPU bucket collective on the comm stream: wait for the producing kernels, [cast to the
+        wire dtype], all-reduce (AVG), [cast back], with timing events around the collective. The
+        host never blocks; ``_finish`` makes the compute stream wait for the comm stream."""
+        s, e = self._buckets[bi]
+        cs = self._comm_stream
+        ready = torch.cuda.Event(enable_timing=self.timing)
+        ready.record()
+        rec = self._step_rec if self.timing else None
+        with torch.cuda.stream(cs):
+            cs.wait_event(ready)
+            ev0 = torch.cuda.Event(enable_timing=True) if rec is not None else None
+            if ev0 is not None:
+                ev0.record(cs)
+            buf = view
+            if self._cbuf is not None:
+                buf = self._cbuf[s:e]
+                buf.copy_(view)
+            op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+            w = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
+            w.wait()  # comm stream waits for the collective (no host block on RCCL)
+            if self.backend != "nccl":
+                buf.mul_(1.0 / self.world_size)
+            if buf is not view:
+                view.copy_(buf)
+            if rec is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(cs)
+                rec["buckets"].append((bi, ready, ev0, ev1))
+        return None
 
     def _make_hook(self, i: int):
         def hook(p):
@@ -135,10 +195,22 @@ class DistributedDataParallel(nn.Module):
             if not self._launched[b] and self._bucket_counts[b] > 0:
                 self._launched[b] = True
                 self._works.append(self._reduce_bucket(b))
+        if self._comm_stream is not None:
+            if self.timing and self._step_rec is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()  # backward compute done (compute stream)
+                self._step_rec["bwd_end"] = ev
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._comm_stream)
+            if self.timing and self._step_rec is not None:
+                self._records.append(self._step_rec)
+                del self._records[:-256]  # bounded history
+                self._step_rec = None
         self._wait_all()
 
     def _wait_all(self) -> None:
         for w in self._works:
+            if w is None:
+                continue
             if isinstance(w, tuple):
                 w[0].wait()
                 w[1].mul_(1.0 / self.world_size)
@@ -148,6 +220,42 @@ class DistributedDataParallel(nn.Module):
         self._pending = list(self._bucket_counts)
         self._launched = [False] * len(self._buckets)
         self._callback_queued = False
+
+    # ------------------------------------------------------------------ observability
+    def reset_comm_stats(self) -> None:
+        self._records.clear()
+
+    def comm_stats(self) -> Dict:
+        """Per-step averages over the recorded steps (``timing=True``; synchronises the events):
+        ``allreduce_ms`` device time of the bucket collectives (incl. wire-dtype casts),
+        ``exposed_ms`` comm time after backward compute ended (what the step waits for),
+        ``overlap_pct`` share of the collective time hidden under forward/backward,
+        ``fwd_bwd_ms`` forward start -> backward compute end, plus the bucket layout."""
+        out = {"buckets": len(self._buckets), "bucket_mb": [round(b / 2 ** 20, 3) for b in self.bucket_sizes_bytes],
+               "comm_dtype": str(self.comm_dtype or self.flat.grad.dtype).replace("torch.", ""),
+               "steps_timed": 0}
+        recs = [r for r in self._records if r.get("t0") is not None and r.get("bwd_end") is not None and r["buckets"]]
+        if not recs:
+            return out
+        tot = hidden = exposed = fb = 0.0
+        for r in recs:
+            r["bwd_end"].synchronize()
+            for _, _, ev0, ev1 in r["buckets"]:
+                ev1.synchronize()
+            t0 = r["t0"]
+            bend = t0.elapsed_time(r["bwd_end"])
+            fb += bend
+            last = 0.0
+            for _, _, ev0, ev1 in r["buckets"]:
+                a, b = t0.elapsed_time(ev0), t0.elapsed_time(ev1)
+                tot += b - a
+                hidden += max(0.0, min(b, bend) - a)
+                last = max(last, b)
+            exposed += max(0.0, last - bend)
+        n = len(recs)
+        out.update(steps_timed=n, allreduce_ms=round(tot / n, 4), exposed_ms=round(exposed / n, 4),
+                   fwd_bwd_ms=round(fb / n, 4), overlap_pct=round(100.0 * hidden / tot, 1) if tot > 0 else 0.0)
+        return out
 
     def sync_gradients(self) -> None:
         """Manual mode (or after no_sync accumulation): all-reduce the whole flat gradient."""
@@ -172,6 +280,10 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         if self.flat.rebind_params():
             pass  # something replaced p.data (e.g. .to()); views restored
+        if self.timing and self._comm_stream is not None and self.require_sync and torch.is_grad_enabled():
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._step_rec = {"t0": ev, "buckets": []}
         return self.module(*args, **kwargs)
 
     def after_backward(self) -> None:

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Time the LeNet weight-gradient kernel with each role dropped (MLT_LENET_WGRAD_SKIP), to find
+# Time the LeNet weight-gradient kernel with each role dropped (MLT_LENET_WGRAD_SKIP; needs a
+# debug build: python -m ml_trainer_amd.build --debug), to find
 # which role sets its critical path. rocprofv3 kernel stats per mask under gpurun_out/wgrad_roles/.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -102,3 +102,21 @@ def test_bench_self_launch_two_ranks_gloo():
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
               "data"):
         assert k in out
+
+
+def test_debug_checks_compile_for_gfx950():
+    """-DMLT_DEBUG turns MLT_DCHECK into device printf checks in the LeNet / GEMM / attention
+    index math; they must parse for host and gfx950 device (syntax-only compile, no codegen)."""
+    import subprocess
+    import shutil
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    inc = os.path.join(ROOT, "ml_trainer_amd", "csrc", "include")
+    for f in ("lenet.hip", "gemm_tile.hip", "attention.hip"):
+        src = os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", f)
+        r = subprocess.run([hipcc, "-fsyntax-only", "-std=c++17", "--offload-arch=gfx950", "-DMLT_DEBUG=1",
+                            f"-I{inc}", src], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        txt = open(src).read()
+        assert "MLT_DCHECK(" in txt

@@ -115,3 +115,38 @@ def test_fault_injection_surfaces_on_all_ranks():
             pass
         s = [open(os.path.join(d, f"s{i}.txt")).read() for i in range(world)]
         assert s[1].startswith("error") and "completed" not in s[0], s
+
+
+def _bf16_comm_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    out = {}
+    for tag, cd in (("fp32", None), ("bf16", torch.bfloat16)):
+        torch.manual_seed(1234)
+        model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+        ddp = DistributedDataParallel(model, bucket_cap_mb=0.004, first_bucket_mb=0.002, comm_dtype=cd)
+        g = torch.Generator().manual_seed(11 + rank)
+        x, y = torch.randn(16, 32, generator=g), torch.randn(16, 8, generator=g)
+        ((ddp(x) - y) ** 2).mean().backward()
+        ddp.after_backward()
+        out[tag] = ddp.flat.grad.clone()
+        out[tag + "_buckets"] = len(ddp.bucket_sizes_bytes)
+        out[tag + "_dtype"] = ddp.comm_stats()["comm_dtype"]
+    torch.save(out, os.path.join(out_dir, f"b{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_bf16_gradient_comm_close_to_fp32():
+    """comm_dtype=bf16: buckets are cast to bf16, reduced, cast back -- within bf16 rounding
+    of the fp32 all-reduce, identical on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_bf16_comm_worker, args=(world, free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"b{i}.pt"), weights_only=True) for i in range(world)]
+        assert r[0]["bf16_buckets"] >= 2 and r[0]["bf16_dtype"] == "bfloat16" and r[0]["fp32_dtype"] == "float32"
+        assert torch.equal(r[0]["bf16"], r[1]["bf16"])
+        a, b = r[0]["fp32"], r[0]["bf16"]
+        rel = (a - b).norm() / a.norm()
+        assert rel < 1e-2, rel
+        assert not torch.equal(a, b)  # the wire dtype really was bf16

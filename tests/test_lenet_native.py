@@ -346,3 +346,28 @@ def test_device_prefetcher_uses_native_ring(dev):
     assert torch.allclose(torch.cat(sums).cpu(), x.double().sum(dim=(1, 2, 3)))
     assert torch.equal(torch.cat(labels).cpu(), y)
     assert len(torch.cat(labels)) == 200  # includes the short last batch
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_launch_variants_match_autograd(dev, variant):
+    """Every launch variant of the per-sample chain (0 default 4-kernel, 1 fully fused KF,
+    2 split conv2 / fc kernels) gives the reference gradients and the same logits."""
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    old = C.get_lenet_variant()
+    C.set_lenet_variant(variant)
+    try:
+        assert C.get_lenet_variant() == variant
+        m = _mk("default", 3).to(dev)
+        ref = copy.deepcopy(m)
+        x = _xin(16, dev, 3)
+        y = torch.randint(0, 10, (16,), device=dev)
+        out = m(x)
+        F.cross_entropy(out, y).backward()
+        rout = ref.forward_reference(x)
+        F.cross_entropy(rout, y).backward()
+        torch.testing.assert_close(out, rout, rtol=1e-4, atol=1e-4)
+        for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=2e-3, atol=2e-5, msg=lambda s: f"{n}: {s}")
+    finally:
+        C.set_lenet_variant(old)

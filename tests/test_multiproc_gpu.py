@@ -188,3 +188,42 @@ def test_bert_zero1_two_ranks_matches_ddp():
     for k, v in r[0]["ddp"].items():
         assert torch.equal(r[0]["zero"][k], r[1]["zero"][k])
         torch.testing.assert_close(r[0]["zero"][k], v, rtol=2e-3, atol=2e-4)
+
+
+def _bert_comm_worker(rank, world, port, out_dir):
+    """The DDP side-stream path (timing events + bf16 wire dtype) around the fused BERT blocks."""
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    out = {}
+    for tag, cd in (("fp32", None), ("bf16", torch.bfloat16)):
+        torch.manual_seed(rank)
+        m = BertClassifier(bert_config("bert-tiny")).to(dev)
+        ddp = DistributedDataParallel(m, bucket_cap_mb=1.0, first_bucket_mb=0.5, comm_dtype=cd, timing=True)
+        g = torch.Generator().manual_seed(11 + rank)
+        ids = torch.randint(5, 1000, (2, 128), generator=g).to(dev)
+        y = torch.randint(0, 2, (2,), generator=g).to(dev)
+        for _ in range(3):
+            ddp.flat.zero_grad()
+            F.cross_entropy(ddp(ids), y).backward()
+        torch.cuda.synchronize()
+        out[tag] = ddp.flat.grad.cpu()
+        st = ddp.comm_stats()
+        out[tag + "_stats"] = torch.tensor([st["steps_timed"], st["buckets"], st["allreduce_ms"], st["overlap_pct"],
+                                            st["fwd_bwd_ms"]], dtype=torch.float64)
+    torch.save(out, os.path.join(out_dir, f"c{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_bert_ddp_timing_and_bf16_comm_two_ranks():
+    r = _run(_bert_comm_worker)
+    for tag in ("fp32", "bf16"):
+        assert torch.equal(r[0][tag], r[1][tag])
+        steps, buckets, ar_ms, ov, fb = r[0][tag + "_stats"].tolist()
+        assert steps == 3 and buckets >= 2 and ar_ms > 0 and 0.0 <= ov <= 100.0 and fb > 0
+    a, b = r[0]["fp32"], r[0]["bf16"]
+    assert (a - b).norm() / a.norm() < 2e-2
