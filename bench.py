@@ -387,10 +387,14 @@ def main():
                 samples += b * k
         return samples
 
+    # capture + upload every hipGraph the warmup AND the timed steps replay before any step runs
+    # (no step runs here), so the timed region holds exactly K steps of replays and nothing else,
+    # and the warmup replays end right before t0 (no capture gap lets the GPU idle down in between)
+    st_w = dict(state)
+    plan_w = list(lenet_plan(args.warmup, st_w, N, world, rank, per_gpu, spg, shard_indices))
+    precapture(engine, plan_w, use_graph)
+    precapture(engine, lenet_plan(args.steps, dict(st_w), N, world, rank, per_gpu, spg, shard_indices), use_graph)
     run(args.warmup)
-    # capture + upload every hipGraph the timed steps replay (no step runs here), so the timed
-    # region holds exactly K steps of replays and nothing else
-    precapture(engine, lenet_plan(args.steps, dict(state), N, world, rank, per_gpu, spg, shard_indices), use_graph)
     captures_before = engine.captures
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()

@@ -823,6 +823,9 @@ class LeNetEngine {
     P_.targets = get("targets", at::kLong, B).data_ptr<int64_t>();
     P_.stats = get("stats", at::kDouble, 2).data_ptr<double>();  // 16B-aligned by get()
     P_.counters = reinterpret_cast<unsigned*>(get("counters", at::kInt, C1 + 1).data_ptr<int32_t>());
+    P_.stage = bufs.contains("stage") ? get("stage", at::kByte, B * 3072).data_ptr<uint8_t>() : nullptr;
+    P_.stage_meta = bufs.contains("stage_meta") ? get("stage_meta", at::kLong, B * 4).data_ptr<int64_t>() : nullptr;
+    if (!P_.stage || !P_.stage_meta) P_.stage = nullptr, P_.stage_meta = nullptr;
     P_.dtargets = nullptr;
     A_ = LeNetAug{};
     O_ = LeNetOpt{};

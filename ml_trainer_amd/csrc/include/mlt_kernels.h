@@ -45,6 +45,8 @@ struct LeNetPtrs {
   const int64_t* dtargets;   // dataset targets [N] (augment path)
   double* stats;             // [2]: sum over batches of batch-mean loss, of batch accuracy
   unsigned* counters;        // [>= C1+1] zero-initialised arrival counters (K5 last-arriver reductions)
+  uint8_t* stage;            // [B][3072] raw uint8 images of the next step (nullptr: no staging)
+  int64_t* stage_meta;       // [B][4] (perm position, dataset row, target, 0) of each staged image; -1 = empty
 };
 
 struct LeNetAug {

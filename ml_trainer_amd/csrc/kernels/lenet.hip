@@ -55,7 +55,9 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
                                                        const float* __restrict__ b1, float* __restrict__ x,
                                                        float* __restrict__ p1, uint8_t* __restrict__ i1,
                                                        int64_t* __restrict__ targets,
-                                                       const int64_t* __restrict__ dtargets) {
+                                                       const int64_t* __restrict__ dtargets,
+                                                       const uint8_t* __restrict__ staged,
+                                                       const int64_t* __restrict__ staged_meta) {
   const int b = blockIdx.x, oc = blockIdx.y, t = threadIdx.x;
   // input image rows at a 46-float stride: the 14 lanes of a pooled row read 2 px apart, so with
   // a 32-float stride the (up to 5) pooled rows of a wave land on the same banks; 2 * 46 = 28 (mod
@@ -69,21 +71,40 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
   for (int i = 0; i < 75; ++i) wr[i] = w1[oc * 75 + i];
   const float bias = b1[oc];
   if (aug.data) {
+    // The previous step's K4 staged this step's raw images (stage / stage_meta): ctrl, the tag
+    // and the staged image are independent loads issued together -- ONE round trip instead of the
+    // ctrl -> perm -> image chain. A tag that does not match the position computed from ctrl
+    // (first step of an epoch, a new permutation, ...) falls back to the chain.
+    const bool staged_ok = staged != nullptr;
+    uint4 sv = make_uint4(0, 0, 0, 0);
+    int64_t tag = -1, sidx = 0, stgt = 0;
+    if (staged_ok) {
+      tag = staged_meta[4 * b];
+      sidx = staged_meta[4 * b + 1];
+      stgt = staged_meta[4 * b + 2];
+      if (t < 192) sv = reinterpret_cast<const uint4*>(staged + (int64_t)b * 3072)[t];
+    }
     const int64_t step = aug.ctrl[0], sie = aug.ctrl[1];
     int64_t pos = sie * aug.batch_stride + b;
     if (pos >= aug.perm_len) pos %= aug.perm_len;
-    int64_t idx = aug.perm[pos];
-    MLT_DCHECK(idx >= 0 && idx < aug.n);  // release builds clamp a bad permutation entry
     MLT_DCHECK(b < aug.batch_stride && pos < aug.perm_len);
-    idx = idx < 0 ? 0 : (idx >= aug.n ? aug.n - 1 : idx);
+    int64_t idx;
+    if (staged_ok && tag == pos) {  // block-uniform branch
+      idx = sidx;
+      if (t < 192) rawimg[t] = sv;
+    } else {
+      idx = aug.perm[pos];
+      MLT_DCHECK(idx >= 0 && idx < aug.n);  // release builds clamp a bad permutation entry
+      idx = idx < 0 ? 0 : (idx >= aug.n ? aug.n - 1 : idx);
+      stgt = -1;
+      if (t < 192) rawimg[t] = reinterpret_cast<const uint4*>(aug.data + idx * 3072)[t];
+    }
     const uint64_t h = mix64(mix64(aug.seed + (uint64_t)step) ^ (uint64_t)pos);
     const int span = 2 * aug.pad + 1;
     const int ci = aug.pad ? (int)(h % span) : 0;
     const int cj = aug.pad ? (int)((h >> 20) % span) : 0;
     const bool fl = aug.flip && ((h >> 40) & 1);
-    // stage the raw 3 KB HWC image with 16-byte loads, then crop/flip/normalise from LDS
-    const uint4* img4 = reinterpret_cast<const uint4*>(aug.data + idx * 3072);
-    if (t < 192) rawimg[t] = img4[t];
+    // the raw 3 KB HWC image (16-byte loads) is cropped / flipped / normalised from LDS
     __syncthreads();
     const uint8_t* img = reinterpret_cast<const uint8_t*>(rawimg);
 #pragma unroll
@@ -98,7 +119,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_fwd(LeNetAug aug, const float
       xs[c * XC + y * XR + xx] = v;
       if (oc == 0) x[(int64_t)b * 3072 + e] = v;
     }
-    if (oc == 0 && t == 0 && targets) targets[b] = dtargets[idx];
+    if (oc == 0 && t == 0 && targets) targets[b] = stgt >= 0 ? stgt : dtargets[idx];
   } else {
     const float4* src = reinterpret_cast<const float4*>(x + (int64_t)b * 3072);
     float4 v[3];
@@ -606,10 +627,29 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
                                                          const uint8_t* __restrict__ i1, float* __restrict__ g1,
                                                          const float* __restrict__ x, const float* __restrict__ p1,
                                                          float* __restrict__ slab, int mode, LeNetPtrs P, LeNetOpt O,
-                                                         const int64_t* __restrict__ ctrl) {
+                                                         const int64_t* __restrict__ ctrl, LeNetAug A, int stage_row) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, NZ4 = C2 * 81, NS = (FLAT + 255) / 256;
   constexpr int W2N = C2 * 25 + C2;  // conv2 wgrad outputs of one input channel (+ the biases)
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if ((int)blockIdx.y == stage_row) {
+    // next-step input staging (off the step's critical path: runs beside the dgrad blocks).
+    // ctrl still holds this step's counters here (K5 advances them after every K4 block is done),
+    // so the next step reads position (ctrl[1] + 1) * stride + b -- exactly what its conv1 computes.
+    int64_t pos = (A.ctrl[1] + 1) * A.batch_stride + b;
+    if (pos >= A.perm_len) pos %= A.perm_len;
+    int64_t idx = A.perm[pos];
+    idx = idx < 0 ? 0 : (idx >= A.n ? A.n - 1 : idx);
+    const int64_t tgt = P.dtargets ? P.dtargets[idx] : 0;
+    if (t < 192)
+      reinterpret_cast<uint4*>(P.stage + (int64_t)b * 3072)[t] = reinterpret_cast<const uint4*>(A.data + idx * 3072)[t];
+    if (t == 0) {
+      P.stage_meta[4 * b] = pos;
+      P.stage_meta[4 * b + 1] = idx;
+      P.stage_meta[4 * b + 2] = tgt;
+      P.stage_meta[4 * b + 3] = 0;
+    }
+    return;
+  }
   if (WG && (int)blockIdx.y >= 2 * C1) {  // fc wgrad (+ update) blocks: independent of the dgrad
     const int bf = ((int)blockIdx.y - 2 * C1) * (int)gridDim.x + b;
     if (bf < fc_wgrad_blocks<D>()) fc_wgrad_roles<D>(bf, (int)gridDim.x, P, O, make_optctx(mode, O, ctrl));
@@ -1470,7 +1510,8 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     const bool c2fc = g_lenet_variant != 2;  // conv2 + fc chain as the per-sample KF launch (from p1)
     if (mode & LENET_FWD) {
       hipLaunchKernelGGL(lenet_conv1_fwd<D>, dim3(B, D::C1), dim3(256), 0, st, A, P.w1, P.b1, P.x, P.p1, P.i1,
-                         A.data ? P.targets : nullptr, P.dtargets);
+                         A.data ? P.targets : nullptr, P.dtargets, A.data ? P.stage : nullptr,
+                         A.data ? P.stage_meta : nullptr);
       if (c2fc) {
         hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode | LENET_FROM_P1, P, A,
                            inv_B);
@@ -1484,9 +1525,12 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
     if (mode & LENET_BWD) {
       // K4: dgrad + conv1 wgrad slabs (y < C1), conv2 wgrad slabs (C1 <= y < 2 C1), fc wgrads
       // with their update (y >= 2 C1: fc weights are not read after K3/KF)
+      // (+ one row of next-step input staging blocks on the device-dataset path)
       const unsigned k4y = 2 * D::C1 + (fc_wgrad_blocks<D>() + B - 1) / B;
-      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, k4y), dim3(256), 0, st,
-                         P.dflat, P.i2, P.w2, P.i1, P.g1, P.x, P.p1, P.slab1, mode, P, O, A.ctrl);
+      const bool stage = A.data && A.ctrl && P.stage && P.stage_meta && B <= A.batch_stride;
+      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, k4y + (stage ? 1 : 0)), dim3(256), 0, st,
+                         P.dflat, P.i2, P.w2, P.i1, P.g1, P.x, P.p1, P.slab1, mode, P, O, A.ctrl, A,
+                         stage ? (int)k4y : -1);
     }
   }
   if ((mode & LENET_BWD) && !(fused && (mode & LENET_TRACE))) {

@@ -104,6 +104,11 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         "stats": torch.zeros(2, dtype=torch.float64, device=device),
         # arrival counters of the in-launch last-arriver reductions (zeroed once; reset by the kernel)
         "counters": torch.zeros(16, dtype=torch.int32, device=device),
+        # next-step input staging (engine path): K4 gathers the raw uint8 images of the NEXT step
+        # into `stage`, tagged in `stage_meta` [B][4] = (perm position, dataset row, target, 0);
+        # conv1 uses a staged image only when its tag matches the position it computes (-1 = none)
+        "stage": torch.zeros(B * 3072, dtype=torch.uint8, device=device),
+        "stage_meta": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
     }
     return bufs
 

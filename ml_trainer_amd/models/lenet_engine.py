@@ -182,6 +182,7 @@ class LeNetStepEngine:
         cap = int(perm_capacity or self.data.shape[0])
         self.perm = torch.zeros(max(cap, 1), dtype=torch.int32, device=self.device)
         self.batch_size = int(batch_size)
+        self.bufs["stage_meta"].fill_(-1)  # staged next-step images belong to the old dataset
         self.eng.set_aug(self.data, self.perm, self.ctrl, self.targets, self.seed, pad if augment else 0,
                          1 if (augment and flip) else 0, self.batch_size, list(mean), list(std))
 
@@ -192,6 +193,7 @@ class LeNetStepEngine:
             raise ValueError("epoch permutation larger than perm capacity")
         self.perm[:n].copy_(indices.to(torch.int32), non_blocking=True)
         self.ctrl[1:2].zero_()
+        self.bufs["stage_meta"].fill_(-1)  # images staged by the last step came from the old order
         if lr_values is not None:
             if not self._use_table:
                 raise RuntimeError("engine not configured with an lr table")

@@ -371,3 +371,40 @@ def test_launch_variants_match_autograd(dev, variant):
             torch.testing.assert_close(p.grad, q.grad, rtol=2e-3, atol=2e-5, msg=lambda s: f"{n}: {s}")
     finally:
         C.set_lenet_variant(old)
+
+
+def test_engine_next_step_staging_bitwise(dev):
+    """K4 stages the next step's raw images (tagged with their perm position); conv1 takes a
+    staged image only on a tag match. Training with staging (graphs, two epochs, a partial last
+    batch) must be bit-identical to training with every tag invalidated before each step."""
+    data, targets = _toy_data(300, 7)
+    runs = []
+    for staged in (True, False):
+        m = _mk("default", 6).to(dev)
+        eng, flat = _engine(m, "sgd", max_batch=32, lr=1e-2)
+        eng.set_dataset(data, targets, batch_size=32)
+        hits = 0
+        for ep in range(2):
+            perm = torch.randperm(300, generator=torch.Generator().manual_seed(10 + ep))
+            eng.start_epoch(perm)
+            if staged:
+                eng.train_steps(32, 9, use_graph=True, steps_per_graph=3)
+                torch.cuda.synchronize()
+                # the last full step staged step 10's images: positions 9 * 32 + b (the partial
+                # last batch holds 12 samples; positions past the epoch wrap and go unused)
+                meta = eng.bufs["stage_meta"].view(-1, 4)[:12].cpu()
+                hits += int((meta[:, 0] == torch.arange(9 * 32, 9 * 32 + 12)).all())
+                assert meta[:, 1].tolist() == perm[9 * 32:].tolist()
+                assert meta[:, 2].tolist() == targets[perm[9 * 32:]].tolist()
+            else:
+                for _ in range(9):
+                    eng.bufs["stage_meta"].fill_(-1)
+                    eng.train_steps(32, 1, use_graph=False)
+            eng.bufs["stage_meta"].fill_(-1) if not staged else None
+            eng.train_steps(300 - 9 * 32, 1, use_graph=staged, steps_per_graph=1)  # partial batch of 12
+        torch.cuda.synchronize()
+        if staged:
+            assert hits == 2
+        runs.append((flat.data.clone(), eng.stats.clone()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
