@@ -46,6 +46,8 @@ for name, M, N, K, a_mn, b_mn in shapes:
     plan = C.gemm_plan(bool(a_mn), bool(b_mn), M, N, K)
     variants = {"native": {}, "legacy128": {"cfg": 0}, "t256x256": {"cfg": 1}, "t256x128": {"cfg": 2}, "t256x192": {"cfg": 4},
                 "t128x256": {"cfg": 3}, "pp256": {"cfg": 5}}
+    if not a_mn:
+        variants["persist256"] = {"cfg": 6}
     best = {k: 1e9 for k in list(variants) + ["torch"]}
     for _ in range(3):
         for k, kw in variants.items():
@@ -64,6 +66,8 @@ for name, M, N, K, a_mn, b_mn in shapes:
         r["fp8_tflops"] = round(fl / t8 / 1e9, 1)
         t8p = min(timeit(lambda: C.gemm_f8(A8, B8, out, 0, 0, one, one, cfg=5)) for _ in range(3))
         r["fp8_pp256_tflops"] = round(fl / t8p / 1e9, 1)
+        t8q = min(timeit(lambda: C.gemm_f8(A8, B8, out, 0, 0, one, one, cfg=6)) for _ in range(3))
+        r["fp8_persist256_tflops"] = round(fl / t8q / 1e9, 1)
         r["fp8_plan"] = list(C.gemm_f8_plan(M, N, K))
     res.append(r)
     print(json.dumps(r), flush=True)

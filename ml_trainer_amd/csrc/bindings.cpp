@@ -826,6 +826,7 @@ class LeNetEngine {
     P_.stage = bufs.contains("stage") ? get("stage", at::kByte, B * 3072).data_ptr<uint8_t>() : nullptr;
     P_.stage_meta = bufs.contains("stage_meta") ? get("stage_meta", at::kLong, B * 4).data_ptr<int64_t>() : nullptr;
     if (!P_.stage || !P_.stage_meta) P_.stage = nullptr, P_.stage_meta = nullptr;
+    P_.cestat = bufs.contains("cestat") ? get("cestat", at::kDouble, B * 2).data_ptr<double>() : nullptr;
     P_.dtargets = nullptr;
     A_ = LeNetAug{};
     O_ = LeNetOpt{};

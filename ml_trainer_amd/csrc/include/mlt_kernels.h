@@ -34,6 +34,7 @@ enum LeNetMode : int {
   LENET_SKIP_CONV1 = 512, LENET_SKIP_CONV2 = 1024, LENET_SKIP_FC = 2048,  // K5 roles skipped (profiling)
   LENET_K4WG = 4096,    // internal: K4 wrote the conv wgrad slabs, K5 only reduces them
   LENET_FROM_P1 = 8192, // internal: the per-sample kernel starts from p1 (conv2 -> fc chain) and stops there
+  LENET_STATS_DEFER = 16384,  // internal: CE writes per-sample loss / hit to cestat; K4 sums them in sample order
 };
 
 struct LeNetPtrs {
@@ -47,6 +48,7 @@ struct LeNetPtrs {
   unsigned* counters;        // [>= C1+1] zero-initialised arrival counters (K5 last-arriver reductions)
   uint8_t* stage;            // [B][3072] raw uint8 images of the next step (nullptr: no staging)
   int64_t* stage_meta;       // [B][4] (perm position, dataset row, target, 0) of each staged image; -1 = empty
+  double* cestat;            // [B][2] per-sample (loss / B, hit / B) for the fixed-order stats sum (or nullptr)
 };
 
 struct LeNetAug {

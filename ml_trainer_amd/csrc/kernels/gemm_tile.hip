@@ -27,25 +27,10 @@
 
 #include "mlt_common.h"
 #include "mlt_gemm.h"
+#include "mlt_gemm_tile.h"
 #include "mlt_kernels.h"
 
 namespace mlt {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef __attribute__((address_space(3))) void lds_void;
-
-constexpr int T_BK = 64, T_NT = 512;
-
-// mn-contiguous images XOR-swizzle the 16-B chunk index within aligned groups of 16 (or 8
-// when a k-row holds 24 chunks) so the permutation never leaves the row
-template <int CPR>
-struct MnSwz {
-  static constexpr int MASK = CPR % 16 == 0 ? 15 : 7;
-};
 
 template <int BM, int BN, int WARPS_M>
 struct TileGeom {
@@ -56,72 +41,6 @@ struct TileGeom {
   static constexpr int EPI_BYTES = 8 * EPR * EPS * 4;
   static constexpr int SMEM = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
 };
-
-// ---- fragments --------------------------------------------------------------------------
-__device__ __forceinline__ bf16x8 tfrag_k(const uint8_t* lds, int row, int kh) {
-  const int lane = threadIdx.x & 63;
-  const int r = row + (lane & 15), c = kh * 4 + (lane >> 4);
-  return *reinterpret_cast<const bf16x8*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
-}
-template <int RB>  // row bytes of the mn-contiguous image (2 * BM or 2 * BN)
-__device__ __forceinline__ bf16x8 tfrag_mn(const uint8_t* lds, int mn, int kh) {
-  constexpr int SW = MnSwz<RB / 16>::MASK;
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int col = mn + 4 * p;
-  const int c = col >> 3, half = (col & 7) * 2;
-  const int k0 = kh * 32 + 8 * g + q, k1 = k0 + 4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ (k0 & SW)) << 4) + half));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ (k1 & SW)) << 4) + half));
-  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-// ---- per-thread glds sources -----------------------------------------------------------
-// Chunk e = i * 512 + threadIdx.x of an operand image lands at LDS byte e * 16. Byte
-// addressing: ES = element size (2 bf16, 1 fp8); a k-contiguous row holds 128 bytes per K-step.
-template <int ROWS, bool MN, int ES>  // ROWS = extent of the operand's M (or N) side of the tile
-__device__ __forceinline__ const uint8_t* glds_src(const uint8_t* __restrict__ base, int64_t ld, int i, int mn0,
-                                                   int nmn) {
-  const int e = i * T_NT + threadIdx.x;
-  if (!MN) {  // [ROWS][128 B]: 8 chunks per row
-    const int r = e >> 3, p = e & 7, c = p ^ (r & 7);
-    const int row = min(mn0 + r, nmn - 1);
-    return base + ((int64_t)row * ld) * ES + c * 16;
-  } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row (bf16 only)
-    constexpr int CPR = ROWS / 8;
-    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
-    const int col = min(mn0 + c * 8, nmn - 8);
-    return base + ((int64_t)kk * ld + col) * ES;
-  }
-}
-
-// the same source as a 32-bit byte offset from the operand base (ping-pong kernel: a uniform
-// 64-bit base in SGPRs + a 32-bit per-lane offset is the glds SADDR form, half the VGPRs)
-template <int ROWS, bool MN, int ES>
-__device__ __forceinline__ uint32_t glds_off(int64_t ld, int i, int mn0, int nmn) {
-  const int e = i * T_NT + threadIdx.x;
-  if (!MN) {
-    const int r = e >> 3, p = e & 7, c = p ^ (r & 7);
-    const int row = min(mn0 + r, nmn - 1);
-    return (uint32_t)(row * ld * ES + c * 16);
-  } else {
-    constexpr int CPR = ROWS / 8;
-    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
-    const int col = min(mn0 + c * 8, nmn - 8);
-    return (uint32_t)((kk * ld + col) * ES);
-  }
-}
-
-// fp8 operand fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row (l&15), k bytes
-// 32(l>>4) .. +31 = chunks 2(l>>4), 2(l>>4)+1 of the 128-byte row (positional k pairing with B)
-typedef int i32x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ i32x8 tfrag_f8(const uint8_t* lds, int row) {
-  const int lane = threadIdx.x & 63;
-  const int r = row + (lane & 15), c0 = 2 * (lane >> 4);
-  const uint4 lo = *reinterpret_cast<const uint4*>(lds + r * 128 + ((c0 ^ (r & 7)) << 4));
-  const uint4 hi = *reinterpret_cast<const uint4*>(lds + r * 128 + (((c0 + 1) ^ (r & 7)) << 4));
-  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-}
 
 // F8A / F8B: -1 = bf16 operands; 0 = fp8 e4m3, 1 = bf8 e5m2 (OCP) through the MX-scaled
 // 16x16x128 MFMA at unit block scales (per-tensor scales are folded into the epilogue alpha).
@@ -717,7 +636,7 @@ struct CfgDesc {
   int per_cu;    // resident blocks per CU
   double fixed;  // per-block fixed cost (prologue fill + epilogue), s
 };
-constexpr int kNumCfg = 6;
+constexpr int kNumCfg = 7;
 // cfg 5 (ping-pong) fitted to the 64K-token BERT shapes (profiles/gemm_bf16_64k_tokens.jsonl):
 // 5 % slower than cfg 1 at K = 768 (12 K-steps: its deeper pipeline fill does not amortise),
 // 8-10 % faster at K = 2304-3072 -> a faster steady state with a larger fixed cost.
@@ -726,7 +645,8 @@ const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2, 1.0e-6},
                                {256, 128, 0.92e15 / kCUs, 1, 1.0e-6},
                                {128, 256, 0.92e15 / kCUs, 1, 1.0e-6},
                                {256, 192, 1.05e15 / kCUs, 1, 1.0e-6},
-                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6}};  // 5: ping-pong
+                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6},   // 5: ping-pong
+                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6}};  // 6: persistent ping-pong (fill once)
 
 // split-K combine override: -1 planner, 0 in-kernel, 1 external (env MLT_GEMM_SPLIT_EXT, or
 // set_gemm_split_mode() from tests / benchmarks)
@@ -764,25 +684,35 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
   const int nk = (K + kstep - 1) / kstep, ks = (nk + splits - 1) / splits;
   const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + c.fixed;
   double t = rounds * t_block;
+  if (cfg == 6) t = rounds * (t_block - c.fixed) + c.fixed;  // prologue / epilogue overlap the next tile
   if (splits > 1) t += split_cost(cfg, splits, M, N, nullptr);
   return t;
 }
 
 GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
-                    bool allow_pp = true) {
+                    bool allow_pp = true, bool allow_persist = true) {
   GemmPlan p{0, 1, 0, 0, 0};
   const bool big_ok = K % kstep == 0 && K >= kstep && M >= 64 && N >= 64;
   const double speed = kstep == 128 ? 1.8 : 1.0;
   int best_cfg = 0, best_s = 1;
   if (force_cfg >= 0) {
     best_cfg = (force_cfg >= 1 && force_cfg < kNumCfg && big_ok) ? force_cfg : 0;
-    best_s = best_cfg ? (force_splits > 0 ? force_splits : 1) : 1;
+    if (best_cfg == 6 && !allow_persist) best_cfg = 1;
+    best_s = best_cfg ? (force_splits > 0 && best_cfg != 6 ? force_splits : 1) : 1;
   } else if (big_ok) {
     double best = allow_legacy ? est_time(0, 1, M, N, K, 64, 1.0) : 1e30;
     const int nk = K / kstep;
     for (int cfg = 1; cfg < kNumCfg; ++cfg)
       for (int s = 1; s <= 16; ++s) {
         if (cfg == 5 && !allow_pp) break;
+        // persistent ping-pong: no split-K, even K-tile count, >= one tile per CU; measured to win
+        // only with fp8 operands at N <= 2304 (64K tokens: QKV +8 %, out-proj +12 %, FFN2 +4 %
+        // over cfg 5; FFN1 at N = 3072 -7 %). With bf16 its swapped-operand MFMA order costs ~6 %
+        // of the main loop, which the saved fill / drain does not pay back
+        // (profiles/gemm_persist_64k_tokens.jsonl) -- bf16 takes it only when forced.
+        if (cfg == 6 && (!allow_persist || s > 1 || nk % 2 || kstep != 128 || N > 2304 ||
+                         (int64_t)((M + 255) / 256) * ((N + 255) / 256) < kCUs))
+          break;
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
         if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
@@ -794,7 +724,10 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
           best_s = s;
         }
       }
-    if (force_splits > 0 && best_cfg) best_s = force_splits;
+    if (force_splits > 0 && best_cfg) {
+      if (best_cfg == 6) best_cfg = 1;  // an explicit split-K request takes the split-capable tile
+      best_s = force_splits;
+    }
   }
   p.cfg = best_cfg;
   p.splits = best_s;
@@ -886,6 +819,20 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
     case 3: launch_tile<128, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 4: launch_tile<256, 192, 4, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
     case 5: launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st); break;
+    case 6:
+      // persistent ping-pong (gemm_persist.hip): k-contiguous A, an even K-tile count, no split
+      if constexpr (!AM) {
+        if ((K / (F8A >= 0 ? 128 : T_BK)) % 2 == 0 && p.splits == 1) {
+          static const int group_m = [] {
+            const char* v = getenv("MLT_GEMM_GROUP_M");
+            return v ? atoi(v) : 8;
+          }();
+          launch_gemm_persist<AM, BNL, OutT, F8A, F8B>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, kCUs, st);
+          break;
+        }
+      }
+      launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
+      break;
     default: break;
   }
 }
@@ -923,7 +870,7 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
   (void)b_mn;
   // the ping-pong kernel's fit covers the k-contiguous-A (forward / dgrad) shapes; weight
   // gradients (A = dY^T, mn-contiguous) stay on the 256-wide tiles with split-K
-  return plan_tiles(M, N, K, force_cfg, force_splits, 64, true, a_mn == 0);
+  return plan_tiles(M, N, K, force_cfg, force_splits, 64, true, a_mn == 0, a_mn == 0);
 }
 
 GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {

@@ -440,8 +440,13 @@ __device__ __forceinline__ void fc_chain(int mode, const LeNetPtrs& P, int b, in
         if (mode & LENET_BWD) P.dlogits[(int64_t)b * NC + lane] = dl;
       }
       if (lane == 0 && P.stats) {
-        atomicAdd(&P.stats[0], (double)loss * (double)inv_B);
-        atomicAdd(&P.stats[1], (am == tgt) ? (double)inv_B : 0.0);
+        if ((mode & LENET_STATS_DEFER) && P.cestat) {  // K4 adds them up in sample order (bitwise reproducible)
+          P.cestat[2 * b] = (double)loss * (double)inv_B;
+          P.cestat[2 * b + 1] = (am == tgt) ? (double)inv_B : 0.0;
+        } else {  // evaluation / fused variant: no K4 follows
+          atomicAdd(&P.stats[0], (double)loss * (double)inv_B);
+          atomicAdd(&P.stats[1], (am == tgt) ? (double)inv_B : 0.0);
+        }
       }
     }
     __syncthreads();
@@ -627,10 +632,40 @@ __global__ __launch_bounds__(256) void lenet_conv2_dgrad(const float* __restrict
                                                          const uint8_t* __restrict__ i1, float* __restrict__ g1,
                                                          const float* __restrict__ x, const float* __restrict__ p1,
                                                          float* __restrict__ slab, int mode, LeNetPtrs P, LeNetOpt O,
-                                                         const int64_t* __restrict__ ctrl, LeNetAug A, int stage_row) {
+                                                         const int64_t* __restrict__ ctrl, LeNetAug A, int stage_row,
+                                                         int stats_row) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, NZ4 = C2 * 81, NS = (FLAT + 255) / 256;
   constexpr int W2N = C2 * 25 + C2;  // conv2 wgrad outputs of one input channel (+ the biases)
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if ((int)blockIdx.y == stats_row) {
+    // the step's loss / accuracy: per-sample terms (written by the CE) summed in a fixed order --
+    // thread partials over a fixed stride, then a fixed xor tree -- so the epoch statistics are
+    // bitwise reproducible (a per-sample atomicAdd orders the double sums by arrival). One block,
+    // off the critical path (beside the dgrad blocks).
+    if (b != 0) return;
+    __shared__ double sred[2][4];
+    const int B = (int)gridDim.x;
+    double s0 = 0.0, s1 = 0.0;
+    for (int i = t; i < B; i += 256) {
+      s0 += P.cestat[2 * i];
+      s1 += P.cestat[2 * i + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+    }
+    if (lane == 0) {
+      sred[0][wid] = s0;
+      sred[1][wid] = s1;
+    }
+    __syncthreads();
+    if (t == 0) {
+      P.stats[0] += ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+      P.stats[1] += ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+    }
+    return;
+  }
   if ((int)blockIdx.y == stage_row) {
     // next-step input staging (off the step's critical path: runs beside the dgrad blocks).
     // ctrl still holds this step's counters here (K5 advances them after every K4 block is done),
@@ -1499,6 +1534,11 @@ static int g_lenet_variant = [] {
 void set_lenet_variant(int v) { g_lenet_variant = (v >= 0 && v <= 2) ? v : 0; }
 int get_lenet_variant() { return g_lenet_variant; }
 
+// non-fused training steps: the CE leaves per-sample stats terms for K4's fixed-order sum
+static int kFcDefer(int mode, const LeNetPtrs& P) {
+  return ((mode & LENET_CE) && (mode & LENET_BWD) && P.stats && P.cestat) ? LENET_STATS_DEFER : 0;
+}
+
 template <class D>
 static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
   if (B <= 0) return;
@@ -1513,24 +1553,27 @@ static void run_lenet(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, co
                          A.data ? P.targets : nullptr, P.dtargets, A.data ? P.stage : nullptr,
                          A.data ? P.stage_meta : nullptr);
       if (c2fc) {
-        hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads), 0, st, mode | LENET_FROM_P1, P, A,
-                           inv_B);
+        hipLaunchKernelGGL(lenet_sample_fused<D>, dim3(B), dim3(kFusedThreads),
+                           0, st, mode | LENET_FROM_P1 | kFcDefer(mode, P), P, A, inv_B);
       } else {
         hipLaunchKernelGGL(lenet_conv2_fwd<D>, dim3(B, D::C2 / 4), dim3(128), 0, st, P.p1, P.w2, P.b2, P.p2, P.i2);
-        hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
+        hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode | kFcDefer(mode, P), P, inv_B);
       }
     } else if (mode & (LENET_CE | LENET_BWD)) {
-      hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode, P, inv_B);
+      hipLaunchKernelGGL(lenet_fc<D>, dim3(B), dim3(kFcThreads), 0, st, mode | kFcDefer(mode, P), P, inv_B);
     }
     if (mode & LENET_BWD) {
       // K4: dgrad + conv1 wgrad slabs (y < C1), conv2 wgrad slabs (C1 <= y < 2 C1), fc wgrads
       // with their update (y >= 2 C1: fc weights are not read after K3/KF)
       // (+ one row of next-step input staging blocks on the device-dataset path)
       const unsigned k4y = 2 * D::C1 + (fc_wgrad_blocks<D>() + B - 1) / B;
+      // (+ one block row summing the deferred per-sample loss / accuracy terms in sample order)
       const bool stage = A.data && A.ctrl && P.stage && P.stage_meta && B <= A.batch_stride;
-      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, k4y + (stage ? 1 : 0)), dim3(256), 0, st,
+      const bool defer = kFcDefer(mode, P) != 0;
+      const int rows = (int)k4y + (stage ? 1 : 0) + (defer ? 1 : 0);
+      hipLaunchKernelGGL((lenet_conv2_dgrad<D, true>), dim3(B, rows), dim3(256), 0, st,
                          P.dflat, P.i2, P.w2, P.i1, P.g1, P.x, P.p1, P.slab1, mode, P, O, A.ctrl, A,
-                         stage ? (int)k4y : -1);
+                         stage ? (int)k4y : -1, defer ? rows - 1 : -1);
     }
   }
   if ((mode & LENET_BWD) && !(fused && (mode & LENET_TRACE))) {

@@ -109,6 +109,8 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         # conv1 uses a staged image only when its tag matches the position it computes (-1 = none)
         "stage": torch.zeros(B * 3072, dtype=torch.uint8, device=device),
         "stage_meta": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
+        # per-sample (loss / B, hit / B) of a training step, summed in sample order by K4
+        "cestat": torch.zeros(B * 2, dtype=torch.float64, device=device),
     }
     return bufs
 

@@ -60,7 +60,7 @@ def test_cast_transpose_and_scale_update(dev):
     torch.testing.assert_close(scale, 448.0 / (w.abs().max().view(1) * 2))
 
 
-@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (1, 2), (4, 3), (5, 3)])
+@pytest.mark.parametrize("cfg,splits", [(1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (6, 1), (1, 2), (4, 3), (5, 3)])
 @pytest.mark.parametrize("fmts", [(0, 0), (1, 0), (0, 1)])
 def test_gemm_f8(dev, cfg, splits, fmts):
     C = require_native()
@@ -90,9 +90,10 @@ def test_gemm_f8_identity_asymmetric(dev):
     A = torch.eye(M, 256).to(torch.float8_e4m3fn).to(dev)                            # [M][K]
     B = ((torch.arange(64 * 256).view(64, 256) % 13) - 6).float().to(torch.float8_e4m3fn).to(dev)  # [N][K]
     one = torch.ones(1, device=dev)
-    out = torch.empty(M, 64, dtype=torch.float32, device=dev)
-    C.gemm_f8(A, B, out, 0, 0, one, one, cfg=1)
-    torch.testing.assert_close(out, B.float()[:, :M].t())
+    for cfg in (1, 6):  # 6: persistent kernel with swapped MFMA operands (C^T fragments)
+        out = torch.empty(M, 64, dtype=torch.float32, device=dev)
+        C.gemm_f8(A, B, out, 0, 0, one, one, cfg=cfg)
+        torch.testing.assert_close(out, B.float()[:, :M].t())
 
 
 def _tiny_fp8_pair(dev):

@@ -139,7 +139,7 @@ def test_identity_asymmetric_tile(dev):
     M = 256
     A = torch.eye(M, dtype=torch.bfloat16, device=dev)
     B = (torch.arange(M * 128, device=dev).view(128, M) % 251).to(torch.bfloat16)
-    for cfg in (1, 2, 3, 4, 5):
+    for cfg in (1, 2, 3, 4, 5, 6):
         out = torch.empty(M, 128, dtype=torch.float32, device=dev)
         C.gemm(A, B, out, False, False, cfg=cfg)
         torch.testing.assert_close(out, B.float().t())
@@ -208,3 +208,59 @@ def test_split_k_external_reduce_bitwise(dev, cfg):
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
     torch.testing.assert_close(outs[1][0], A.float().t() @ B.float() + 0.25, rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("b_mn", [0, 1])
+def test_persistent_kernel(dev, b_mn):
+    """Config 6 (persistent tile loop, next tile's first K-step staged under the current tile's
+    last MFMAs, register epilogue from swapped-operand C^T fragments): more tiles than CUs (every
+    workgroup walks several), M / N tails, a strided A, every epilogue, bf16 and fp32 outputs."""
+    C = require_native()
+    M, N, K = 8200, 2312, 256  # 33 x 10 = 330 tiles > 256 workgroups; tails in M and N; 4 K-tiles
+    g = torch.Generator().manual_seed(50 + b_mn)
+    A = _mk((M, K + 64), dev, g)[:, :K]
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    ref = _ref(A, B, 0, b_mn)
+    assert C.gemm_plan(False, bool(b_mn), M, N, K, 6, 0)[0] == 6
+    for out_dtype in (torch.bfloat16, torch.float32):
+        out = torch.empty(M, N, dtype=out_dtype, device=dev)
+        C.gemm(A, B, out, False, bool(b_mn), cfg=6)
+        tol = 2e-2 if out_dtype == torch.bfloat16 else 2e-3
+        torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * 8)
+    bias = torch.randn(N, device=dev)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, out, False, bool(b_mn), bias=bias, aux=aux, mode=1, cfg=6)
+    torch.testing.assert_close(aux.float(), ref + bias, rtol=2e-2, atol=0.15)
+    torch.testing.assert_close(out.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=0.15)
+    res = _mk((M, N), dev, g)
+    C.gemm(A, B, out, False, bool(b_mn), res=res, alpha=0.5, cfg=6)
+    torch.testing.assert_close(out.float(), 0.5 * ref + res.float(), rtol=2e-2, atol=0.15)
+    acc = torch.ones(M, N, device=dev)
+    C.gemm(A, B, acc, False, bool(b_mn), accumulate=True, cfg=6)
+    torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-2)
+    pre = _mk((M, N), dev, g)
+    C.gemm(A, B, out, False, bool(b_mn), aux=pre, mode=2, cfg=6)
+    x = pre.float()
+    dg = 0.5 * (1 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+    torch.testing.assert_close(out.float(), ref * dg, rtol=2e-2, atol=0.15)
+
+
+def test_persistent_kernel_repeatable_full_chip(dev):
+    """Race screen for the cross-tile pipeline: repeated full-chip runs are bit-identical, and
+    agree with the one-tile-per-workgroup kernel to fp32 rounding."""
+    C = require_native()
+    M, N, K = 8192, 2304, 768
+    g = torch.Generator().manual_seed(77)
+    A = _mk((M, K), dev, g)
+    B = _mk((N, K), dev, g)
+    ref = torch.empty(M, N, device=dev)
+    C.gemm(A, B, ref, False, False, cfg=1)
+    first = None
+    for _ in range(6):
+        out = torch.full((M, N), float("nan"), device=dev)
+        C.gemm(A, B, out, False, False, cfg=6)
+        if first is None:
+            first = out.clone()
+        assert torch.equal(out, first)
+    torch.testing.assert_close(first, ref, rtol=1e-5, atol=1e-4)
