@@ -82,8 +82,8 @@ def bench_bert(args, world, rank, dev):
     """BERT classifier training step: synthetic token ids, random-init weights, bf16 compute."""
     import torch
     import torch.distributed as dist
-    import torch.nn.functional as F
     from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops.losses import CrossEntropyLoss
     from ml_trainer_amd.ops.optim import FusedAdamW
     from ml_trainer_amd.parallel.ddp import DistributedDataParallel
 
@@ -111,6 +111,7 @@ def bench_bert(args, world, rank, dev):
     loss_acc = torch.zeros((), device=dev)
 
     accum = max(1, args.grad_accum)
+    ce = CrossEntropyLoss()
 
     def run(n, start):
         for i in range(n):
@@ -120,7 +121,7 @@ def bench_bert(args, world, rank, dev):
                 sync = a == accum - 1
                 ctxm = ddp.no_sync() if (world > 1 and not sync) else contextlib.nullcontext()
                 with ctxm:
-                    loss = F.cross_entropy(fwd(ids[j]), labels[j])
+                    loss = ce(fwd(ids[j]), labels[j])  # native fused softmax-CE (src/trainer.py:141-142)
                     (loss / accum if accum > 1 else loss).backward()
                 loss_acc.add_(loss.detach())
             opt.step()

@@ -212,6 +212,33 @@ void ce_fwd(Tensor logits, Tensor tgt, Tensor dl, Tensor acc, c10::optional<Tens
                 cur_stream());
 }
 
+// BERT classifier layer (num_labels outputs): logits = pooled . W_c^T + b_c (fp32)
+void head_cls_fwd(Tensor pooled, Tensor wc, c10::optional<Tensor> bc, Tensor logits) {
+  TORCH_CHECK(pooled.dim() == 2 && wc.dim() == 2 && wc.size(1) == pooled.size(1), "head: pooled [B,h], W_c [L,h]");
+  const int64_t B = pooled.size(0), h = pooled.size(1), L = wc.size(0);
+  check_dev(pooled, "pooled", at::kFloat, B * h, 4);
+  check_dev(wc, "W_c", at::kFloat, L * h, 4);
+  if (bc.has_value()) check_dev(*bc, "b_c", at::kFloat, L, 4);
+  check_dev(logits, "logits", at::kFloat, B * L, 4);
+  launch_head_cls_fwd(pooled.data_ptr<float>(), (int)B, (int)h, wc.data_ptr<float>(),
+                      bc.has_value() ? bc->data_ptr<float>() : nullptr, (int)L, logits.data_ptr<float>(), cur_stream());
+}
+
+// backward of the classifier layer + the pooler's tanh: dpre (bf16) and dW_c / db_c (fp32)
+void head_cls_bwd(Tensor dlogits, Tensor pooled, Tensor wc, Tensor dpre, Tensor dwc, c10::optional<Tensor> dbc,
+                  bool accumulate) {
+  const int64_t B = pooled.size(0), h = pooled.size(1), L = wc.size(0);
+  check_dev(dlogits, "dlogits", at::kFloat, B * L, 4);
+  check_dev(pooled, "pooled", at::kFloat, B * h, 4);
+  check_dev(wc, "W_c", at::kFloat, L * h, 4);
+  check_dev(dpre, "dpre", at::kBFloat16, B * h, 2);
+  check_dev(dwc, "dW_c", at::kFloat, L * h, 4);
+  if (dbc.has_value()) check_dev(*dbc, "db_c", at::kFloat, L, 4);
+  launch_head_cls_bwd(dlogits.data_ptr<float>(), pooled.data_ptr<float>(), wc.data_ptr<float>(), (int)B, (int)h,
+                      (int)L, (uint16_t*)dpre.data_ptr(), dwc.data_ptr<float>(),
+                      dbc.has_value() ? dbc->data_ptr<float>() : nullptr, accumulate, cur_stream());
+}
+
 void ce_bwd(Tensor dl, Tensor gout, Tensor acc, Tensor out) {
   check_dev(dl, "dl", at::kFloat, dl.numel(), 4);
   check_dev(gout, "grad_out", at::kFloat, 1, 4);
@@ -325,8 +352,8 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
     check_dev(*bias, "bias", at::kFloat, N, 4);
     bp = bias->data_ptr<float>();
   }
-  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm mode");
-  if (mode != 0) {
+  TORCH_CHECK(mode >= 0 && mode <= 3, "gemm mode (0 none, 1 gelu, 2 dgelu, 3 tanh)");
+  if (mode == 1 || mode == 2) {
     TORCH_CHECK(aux.has_value(), "gemm GELU modes need aux");
     TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
                     aux->stride(1) == 1 && aux->is_cuda(), "aux must be bf16 [M,N]");
@@ -382,7 +409,7 @@ void gemm_f8(Tensor A, Tensor B, Tensor C, int fmt_a, int fmt_b, Tensor inv_scal
     check_dev(*bias, "bias", at::kFloat, N, 4);
     bp = bias->data_ptr<float>();
   }
-  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm mode");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "gemm mode (0 none, 1 gelu, 2 dgelu, 3 tanh)");
   if (mode != 0) {
     TORCH_CHECK(aux.has_value() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
                     aux->size(1) == N && aux->stride(1) == 1 && aux->is_cuda(), "aux must be bf16 [M,N]");
@@ -1026,6 +1053,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cifar_augment", &cifar_augment);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
+  m.def("head_cls_fwd", &head_cls_fwd, py::arg("pooled"), py::arg("wc"), py::arg("bc"), py::arg("logits"));
+  m.def("head_cls_bwd", &head_cls_bwd, py::arg("dlogits"), py::arg("pooled"), py::arg("wc"), py::arg("dpre"),
+        py::arg("dwc"), py::arg("dbc"), py::arg("accumulate") = false);
   m.def("accuracy", &accuracy);
   m.def("pointwise_loss_fwd", &pointwise_loss_fwd);
   m.def("nll_fwd", &nll_fwd);

@@ -14,7 +14,7 @@ struct GemmEpi {
   const uint16_t* res;   // residual [M,N] bf16 (added) or nullptr
   int64_t ldaux, ldres;
   float alpha;
-  int mode;              // 0 none, 1 gelu (writes aux), 2 dgelu (reads aux)
+  int mode;              // 0 none, 1 gelu (writes aux), 2 dgelu (reads aux), 3 tanh
   int accumulate;        // C += result (fp32 output only)
   const float* inv_scale_a = nullptr;  // fp8: device-side 1/scale of A and B (multiplied into alpha)
   const float* inv_scale_b = nullptr;
@@ -63,6 +63,9 @@ __device__ __forceinline__ void epilogue_store4(OutT* __restrict__ C, int64_t ld
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) vv[q] = gelu_f(bf16_to_f32(f32_to_bf16(vv[q])));
+  } else if (epi.mode == 3) {  // tanh (BERT pooler)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vv[q] = tanhf(vv[q]);
   } else if (epi.mode == 2) {
     const uint16_t* aux = epi.aux + (int64_t)gm * epi.ldaux + gn;
     if (full && (((uintptr_t)aux) & 7) == 0) {

@@ -77,6 +77,11 @@ struct LeNetOpt {
 
 void launch_lenet(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                   hipStream_t stream);
+// BERT classifier head (head.hip): classifier layer of num_labels outputs on the VALU
+void launch_head_cls_fwd(const float* pooled, int B, int h, const float* wc, const float* bc, int L, float* logits,
+                         hipStream_t st);
+void launch_head_cls_bwd(const float* dlogits, const float* pooled, const float* wc, int B, int h, int L,
+                         uint16_t* dpre, float* dwc, float* dbc, bool accumulate, hipStream_t st);
 void set_lenet_variant(int v);  // 0 default (4 launches), 1 fully fused per-sample chain, 2 split conv2 / fc
 int get_lenet_variant();
 

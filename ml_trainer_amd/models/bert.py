@@ -11,8 +11,9 @@ model-config decision is recorded in SURVEY.md §7.1 and the README:
 Post-LN BERT: embeddings(word+pos+type) -> LN -> N x [attention block -> LN -> FFN
 block -> LN] -> pooler tanh(W h_CLS) -> classifier. On the GPU every heavy op runs
 on the native kernels (ops/transformer.py: MFMA GEMMs with fused epilogues,
-flash attention, LayerNorm, embedding gather/scatter) with fp32 master weights
-and bf16 activations; the tiny pooler/classifier head stays fp32. On CPU the
+flash attention, LayerNorm, embedding gather/scatter, and the classifier head: pooler
+GEMM with a tanh epilogue + the num_labels-wide classifier layer of head.hip) with fp32
+master weights and bf16 activations. On CPU the
 same math runs in plain torch (and serves as the numerics oracle in tests).
 Dropout is 0 (deterministic training; the benchmark measures the compute path).
 """
@@ -146,7 +147,11 @@ class BertClassifier(nn.Module):
             x = T.layer_norm(x, self.emb_ln.weight, self.emb_ln.bias, self.config.ln_eps)
             for layer in self.layers:
                 x = layer.forward_native(x, lens, B, S)
-            cls = x.view(B, S, -1)[:, 0].float()
+            cls = x.view(B, S, -1)[:, 0]  # strided row view: the pooler GEMM reads it in place
+            if cls.shape[1] % 8 == 0 and self.pooler.weight.shape[0] % 8 == 0:
+                return T.classifier_head(cls, self.pooler.weight, self.pooler.bias, self.classifier.weight,
+                                         self.classifier.bias)
+            cls = cls.float()
         else:
             cls = self.forward_reference_hidden(input_ids, lens, token_type_ids)
         pooled = torch.tanh(self.pooler(cls))

@@ -387,6 +387,52 @@ class _Embeddings(torch.autograd.Function):
         return (None, None) + ret + (None,)
 
 
+class _ClassifierHead(torch.autograd.Function):
+    """BERT pooler + classifier (reference criterion input, src/trainer.py:141-142) on the native
+    kernels: pooled = tanh(cls . W_p^T + b_p) is the bf16 GEMM with the tanh epilogue (fp32 out),
+    logits = pooled . W_c^T + b_c and its backward (dpre = (dlogits . W_c) * (1 - pooled^2), dW_c,
+    db_c) run in head.hip; the pooler's wgrad / bias grad / dgrad are the native GEMMs / colsum."""
+
+    @staticmethod
+    def forward(ctx, cls, wp, bp, wc, bc):
+        C = require_native()
+        B, h = cls.shape
+        pooled = torch.empty(B, wp.shape[0], dtype=torch.float32, device=cls.device)
+        C.gemm(cls, bf16_weight(wp), pooled, False, False, bias=bp, mode=3)
+        logits = torch.empty(B, wc.shape[0], dtype=torch.float32, device=cls.device)
+        C.head_cls_fwd(pooled, wc.detach().float().contiguous(), bc.detach().float().contiguous(), logits)
+        ctx.save_for_backward(cls, pooled)
+        ctx.params = (wp, bp, wc, bc)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        C = require_native()
+        cls, pooled = ctx.saved_tensors
+        wp, bp, wc, bc = ctx.params
+        G = _Grads()
+        dpre = torch.empty(pooled.shape, dtype=torch.bfloat16, device=pooled.device)
+        gwc, gbc = G.sink(wc), G.sink(bc)
+        both = gwc is not None and gbc is not None
+        dwc = gwc if both else torch.empty(wc.shape, dtype=torch.float32, device=wc.device)
+        dbc = gbc if both else torch.empty(bc.shape, dtype=torch.float32, device=bc.device)
+        if not both:
+            G.ready = [p for p in G.ready if p is not wc and p is not bc]
+        C.head_cls_bwd(dlogits.contiguous().float(), pooled, wc.detach().float().contiguous(), dpre, dwc, dbc,
+                       accumulate=both)
+        dwp = G.wgrad(wp, dpre, cls)
+        dbp = G.colsum(bp, dpre)
+        dcls = torch.empty(cls.shape, dtype=torch.bfloat16, device=cls.device)
+        C.gemm(dpre, bf16_weight(wp), dcls, False, True)
+        G.done()
+        return dcls, dwp, dbp, (None if both else dwc), (None if both else dbc)
+
+
+def classifier_head(cls, wp, bp, wc, bc):
+    """cls [B, h] bf16 (may be a strided row view) -> logits [B, num_labels] fp32."""
+    return _ClassifierHead.apply(cls, wp, bp, wc, bc)
+
+
 def _mark_training(impl) -> None:
     # autograd runs Function.forward with grad mode off: tell the linear implementation here
     # whether a backward will follow (fp8 keeps transposed activations only then)

@@ -79,6 +79,7 @@ class DistributedDataParallel(nn.Module):
         self.require_sync = True
         self._works: List = []
         self._pending: List[int] = list(self._bucket_counts)
+        self._counted: List[bool] = [False] * len(self.flat.params)
         self._launched: List[bool] = [False] * len(self._buckets)
         self._callback_queued = False
         self._hooks = []
@@ -179,6 +180,14 @@ class DistributedDataParallel(nn.Module):
         def hook(p):
             if not self.require_sync or self.world_size == 1:
                 return
+            # A fused backward that wrote p's gradient straight into the flat buffer notifies here
+            # (FlatParams.notify_grad_ready) AND autograd still runs p's AccumulateGrad node, whose
+            # post-accumulate hook fires even for the None gradient the Function returned. Count
+            # each parameter once per backward: a double count drains a bucket that spans two
+            # fused blocks early and all-reduces it before the second block wrote its gradients.
+            if self._counted[i]:
+                return
+            self._counted[i] = True
             if not self._callback_queued:
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish)
                 self._callback_queued = True
@@ -218,6 +227,7 @@ class DistributedDataParallel(nn.Module):
                 w.wait()
         self._works.clear()
         self._pending = list(self._bucket_counts)
+        self._counted = [False] * len(self.flat.params)
         self._launched = [False] * len(self._buckets)
         self._callback_queued = False
 

@@ -150,3 +150,88 @@ def test_bf16_gradient_comm_close_to_fp32():
         rel = (a - b).norm() / a.norm()
         assert rel < 1e-2, rel
         assert not torch.equal(a, b)  # the wire dtype really was bf16
+
+
+_EVENTS = []
+
+
+class _DirectLinear(torch.autograd.Function):
+    """A fused-block stand-in: y = x W^T + b whose backward accumulates dW / db straight into the
+    flat gradient buffer, notifies the owner, and returns None for the parameters (as
+    ops/transformer.py's blocks do)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x)
+        ctx.p = (w, b)
+        return x @ w.detach().t() + b.detach()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ml_trainer_amd.utils.flat import FlatParams
+        (x,) = ctx.saved_tensors
+        w, b = ctx.p
+        fp = FlatParams.owner(w)
+        fp.grad_sink(w).add_(dy.t() @ x)
+        fp.grad_sink(b).add_(dy.sum(0))
+        _EVENTS.append("bwd")  # before the notifications: the last one launches the bucket
+        fp.notify_grad_ready(w)
+        fp.notify_grad_ready(b)
+        return dy @ w.detach(), None, None
+
+
+class _TwoBlocks(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.l1 = torch.nn.Linear(8, 16)
+        self.l2 = torch.nn.Linear(16, 4)
+
+    def forward(self, x):
+        return _DirectLinear.apply(torch.relu(_DirectLinear.apply(x, self.l1.weight, self.l1.bias)), self.l2.weight,
+                                   self.l2.bias)
+
+
+def _direct_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(5)
+    model = _TwoBlocks()
+    ddp = DistributedDataParallel(model, bucket_cap_mb=1.0, first_bucket_mb=1.0)  # ONE bucket over both blocks
+    assert len(ddp.bucket_sizes_bytes) == 1
+    red = ddp._reduce_bucket
+
+    def traced(bi, async_op=True):
+        _EVENTS.append("launch")
+        return red(bi, async_op)
+    ddp._reduce_bucket = traced
+    g = torch.Generator().manual_seed(21 + rank)
+    x, y = torch.randn(6, 8, generator=g), torch.randn(6, 4, generator=g)
+    ((ddp(x) - y) ** 2).mean().backward()
+    assert _EVENTS == ["bwd", "bwd", "launch"], _EVENTS  # the bucket waits for BOTH blocks
+    torch.save({"g": ddp.flat.grad.clone()}, os.path.join(out_dir, f"d{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_bucket_spanning_two_direct_write_blocks():
+    """Regression: a parameter whose gradient is written by a fused backward is reported twice
+    (direct notification + the AccumulateGrad post hook, which fires even for a None gradient).
+    Counted twice, a bucket spanning two such blocks was all-reduced after the FIRST block, and
+    the second block's gradients stayed rank-local. The averaged gradient must equal the
+    full-batch gradient on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_direct_worker, args=(world, free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"d{i}.pt"), weights_only=True)["g"] for i in range(world)]
+        assert torch.equal(r[0], r[1])
+        from ml_trainer_amd.utils.flat import FlatParams
+        torch.manual_seed(5)
+        model = _TwoBlocks()
+        fp = FlatParams(model.parameters(), reverse=True)
+        xs, ys = [], []
+        for rank in range(world):
+            g = torch.Generator().manual_seed(21 + rank)
+            xs.append(torch.randn(6, 8, generator=g))
+            ys.append(torch.randn(6, 4, generator=g))
+        sum(((model(x) - y) ** 2).mean() for x, y in zip(xs, ys)).div(world).backward()
+        torch.testing.assert_close(r[0], fp.grad, rtol=1e-5, atol=1e-6)

@@ -374,3 +374,28 @@ def test_attention_fwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
             res[ring, grp] = (out, lse)
     for key, (o, l) in res.items():
         assert torch.equal(o, res["0", key[1]][0]) and torch.equal(l, res["0", key[1]][1]), key
+
+
+def test_classifier_head_native_matches_torch(dev):
+    """Pooler GEMM (tanh epilogue) + head.hip classifier layer and backward vs fp32 torch on the
+    same bf16 CLS rows (a strided row view, as in the model)."""
+    from ml_trainer_amd.ops import transformer as T
+    torch.manual_seed(3)
+    B, S, h, L = 24, 8, 256, 3
+    x = torch.randn(B * S, h, device=dev).to(torch.bfloat16)
+    cls = x.view(B, S, h)[:, 0]
+    wp = (torch.randn(h, h, device=dev) * 0.05).requires_grad_()
+    bp = (torch.randn(h, device=dev) * 0.1).requires_grad_()
+    wc = (torch.randn(L, h, device=dev) * 0.05).requires_grad_()
+    bc = (torch.randn(L, device=dev) * 0.1).requires_grad_()
+    y = torch.randint(0, L, (B,), device=dev)
+    logits = T.classifier_head(cls, wp, bp, wc, bc)
+    torch.nn.functional.cross_entropy(logits, y).backward()
+    grads = [p.grad.clone() for p in (wp, bp, wc, bc)]
+    cr = cls.float().clone().requires_grad_()
+    wpr, bpr, wcr, bcr = [p.detach().clone().requires_grad_() for p in (wp, bp, wc, bc)]
+    ref = torch.tanh(cr @ wpr.to(torch.bfloat16).float().t() + bpr) @ wcr.t() + bcr
+    torch.nn.functional.cross_entropy(ref, y).backward()
+    torch.testing.assert_close(logits, ref, rtol=2e-3, atol=2e-3)
+    for g, r in zip(grads, (wpr.grad, bpr.grad, wcr.grad, bcr.grad)):
+        torch.testing.assert_close(g, r, rtol=3e-2, atol=3e-3)
