@@ -6,7 +6,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("ATTN_BENCH_PKG") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ml_trainer_amd.ops._ext import require_native  # noqa: E402
 
 C = require_native()
@@ -40,6 +40,7 @@ q, k, v = [t.contiguous().requires_grad_() for t in (q, k, v)]
 o = F.scaled_dot_product_attention(q, k, v)
 go = dout.view(B, S, H, 64).transpose(1, 2).contiguous()
 fl_f = 4.0 * B * H * S * S * 64
+
 t = {
     "native_fwd": timeit(lambda: C.attn_fwd(qkv, out, lse, None, B, S, H, 0.125)),
     "native_bwd": timeit(lambda: C.attn_bwd(qkv, out, dout, lse, delta, None, dqkv, B, S, H, 0.125)),

@@ -73,6 +73,13 @@ def _run(cmd):
     return time.time() - t0, p.stdout
 
 
+# per-file code-generation flags. attention.hip: MFMA accumulators in arch VGPRs (gfx950's
+# register file is unified). By default hipcc puts them in AGPRs and copies every S^T tile to
+# VGPRs for the softmax VALU work and every O tile back and forth for the rescale (~80
+# v_accvgpr_read/write per 64-key block of the forward); the VGPR form removes those copies.
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
     import pybind11
     os.makedirs(BUILD_DIR, exist_ok=True)
@@ -96,7 +103,8 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
         objs.append(o)
         if force or _newer(s, o, hdrs):
             jobs_list.append([HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common,
-                              "-munsafe-fp-atomics", "-Wno-unused-result"])
+                              "-munsafe-fp-atomics", "-Wno-unused-result",
+                              *FILE_FLAGS.get(os.path.basename(s), [])])
     for s in host_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)

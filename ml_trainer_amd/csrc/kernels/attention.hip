@@ -120,13 +120,63 @@ __device__ __forceinline__ void block_coords(int S, int rows_per_block, int H, i
   MLT_DCHECK((int)gridDim.x % (nrb * H) == 0 && rb * rows_per_block < S);  // grid = B * H * row blocks
 }
 
+// Register staging with buffer loads issued as inline asm. Through the builtins, hipcc's waitcnt
+// pass puts an s_waitcnt vmcnt(0) at the top of the K/V loop (in front of the first QK^T MFMA),
+// i.e. it waits for the next block's loads right after issuing them and the staging hides no
+// latency. As asm the loads are invisible to that pass; vmem_wait_tiles is the one wait, placed
+// just before the registers are written to LDS, with the tile registers as "+v" operands so no
+// use of them can move above it (cdna_hip_programming.md §5.7 item 1). The loop issues no other
+// vector-memory instruction, so vmcnt(0) there retires exactly these loads.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 buffer_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);                 // num_records: reads past it return 0
+  r[3] = 0x00020000;
+  return r;
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 buffer_load_x4_asm(const i32x4& rs, int voff) {
+  u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rs) : "memory");
+  return v;
+}
+__device__ __forceinline__ void vmem_wait_tiles(u32x4 (&a)[2], u32x4 (&b)[2]) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]) :: "memory");
+}
+__device__ __forceinline__ void store_tile_v(uint8_t* lds, const u32x4 (&t)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    *reinterpret_cast<u32x4*>(lds + tile_off(r, c)) = t[i];
+  }
+}
+
 // ---------------------------------------------------------------------------
-// forward: NQ 16-query groups per wave (the K / V^T fragments read from LDS feed NQ MFMAs)
+// forward: NQ 16-query groups per wave (the K / V^T fragments read from LDS feed NQ MFMAs).
+// The softmax side bounded the first version of this kernel (per 64-key block a wave issued 16
+// MFMAs = 256 MFMA cycles against ~150 VALU instructions = ~600 issue cycles); it is cut to ~3.5
+// VALU per score:
+//   * the key mask runs only on the block that holds the sequence end (block-uniform branch);
+//   * the max is taken over the raw scores (scale > 0 commutes with max) and the scale is folded
+//     into the exponent: p = exp2(fma(s, scale*log2e, -m)), one FMA + one v_exp per score;
+//   * the row sum l comes from the MFMA pipe, which has slack: an all-ones A operand against the
+//     same bf16 P^T the P.V product uses (so l normalizes exactly the weights that were summed);
+//   * defer-max (cdna_hip_programming.md T13): O and l are rescaled only when some lane's max
+//     grew by more than kFwdDeferThr (base 2) since the last rescale; otherwise the stale max
+//     stays and p <= 2^kFwdDeferThr. The decision for a block is taken after its scores and
+//     before any of its p is formed, with the previous block's P.V complete -- the textbook
+//     order, so everything at the old max is scaled exactly once.
 // ---------------------------------------------------------------------------
+constexpr float kFwdDeferThr = 8.f;
+
 template <int NQ>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                                       float* __restrict__ lse, const int* __restrict__ lens, int S,
-                                                       int H, float scale) {
+__global__ __launch_bounds__(256) void attn_fwd_lean_kernel(const uint16_t* __restrict__ qkv,
+                                                            uint16_t* __restrict__ out, float* __restrict__ lse,
+                                                            const int* __restrict__ lens, int S, int H,
+                                                            float scale) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[2][AB * 128];
   __shared__ __attribute__((aligned(16))) uint8_t Vs[2][AB * 128];
   int qb, h, b;
@@ -138,7 +188,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   const int len = lens ? lens[b] : S;
   MLT_DCHECK(len >= 0 && len <= S);
   int q[NQ];
-  bf16x8 qf[NQ][2];  // Q fragments (B operand of K.Q^T): Q[q][32kh + 8g + j]
+  bf16x8 qf[NQ][2];
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
@@ -147,32 +197,49 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
                            : bf16x8{};
   }
-  f32x4 o[NQ][4];
-  float m[NQ], l[NQ];
+  f32x4 o[NQ][4], lacc[NQ];
+  float m[NQ];
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     m[n] = -INFINITY;
-    l[n] = 0.f;
+    lacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  const s16x8 ones_bits = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_bits);
   const int nkb = (len + AB - 1) / AB;
-  const float sl2 = scale * 1.4426950408889634f;  // work in base 2
-  TileRegs kr, vr;
+  const float sl2 = scale * 1.4426950408889634f;  // exponents in base 2
+  u32x4 kr[2], vr[2];
+  // loop-invariant byte offsets of this thread's two 16-byte K chunks inside a 64-row block (V:
+  // + 2 D elements): with the block base in the scalar descriptor, no per-iteration address VGPRs
+  int voff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int e = threadIdx.x + 256 * t;
+    voff[t] = (int)(((int64_t)(e >> 3) * ld + D + h * AH + (e & 7) * 8) * 2);
+  }
   if (nkb > 0) {
     stage_tile(Ks[0], qkv, ld, base, min(AB, S), D + h * AH);
     stage_tile(Vs[0], qkv, ld, base, min(AB, S), 2 * D + h * AH);
   }
   __syncthreads();
+  // retire the Q fragment loads here, on every path into the loop: the waitcnt pass merges paths
+  // at the loop header and would otherwise put this wait inside the loop, in front of every
+  // block's first MFMA (an S_WAITCNT it can see, unlike an asm one: simm16 0x0F70 = vmcnt(0))
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   for (int kb = 0; kb < nkb; ++kb) {
     const int cur = kb & 1;
     const bool more = kb + 1 < nkb;
-    if (more) {  // issue the next K/V block's loads now, land them in LDS after this block's math
+    if (more) {  // next K / V block -> registers (rows >= S read as 0), LDS after the math
       const int k1 = (kb + 1) * AB;
-      load_tile(kr, qkv, ld, base + k1, min(AB, S - k1), D + h * AH);
-      load_tile(vr, qkv, ld, base + k1, min(AB, S - k1), 2 * D + h * AH);
+      const i32x4 rs = buffer_rsrc(qkv + (base + k1) * ld, (int64_t)(S - k1) * ld * 2);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kr[t] = buffer_load_x4_asm(rs, voff[t]);
+        vr[t] = buffer_load_x4_asm(rs, voff[t] + 2 * D);
+      }
     }
-    // S^T tiles: rows = keys kt*16 + 4g + r, column = query of group n
     f32x4 s[NQ][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -185,44 +252,47 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
         for (int n = 0; n < NQ; ++n) s[n][kt] = mfma(kfr, qf[n][kh], s[n][kt]);
       }
     }
+    if ((kb + 1) * AB > len) {  // the block holding the sequence end: mask the keys past it
+#pragma unroll
+      for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kb * AB + kt * 16 + 4 * g + r >= len) s[n][kt][r] = -INFINITY;
+    }
 #pragma unroll
     for (int n = 0; n < NQ; ++n) {
-      float bm = -INFINITY;
+      float bm = s[n][0][0];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * AB + kt * 16 + 4 * g + r;
-          const float v = key < len ? s[n][kt][r] * sl2 : -INFINITY;
-          s[n][kt][r] = v;
-          bm = fmaxf(bm, v);
-        }
+        for (int r = 0; r < 4; ++r) bm = fmaxf(bm, s[n][kt][r]);
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-      const float mn = fmaxf(m[n], bm);
-      const float alpha = fast_exp2(m[n] - mn);  // m = -inf on the first block -> 0
-      float ps = 0.f;
+      const float cand = bm * sl2;  // this block's max, scaled (finite: the block has a valid key)
+      if (__any(cand - m[n] > kFwdDeferThr)) {  // wave-uniform: rescale O and l to the new max
+        const float mn = fmaxf(m[n], cand);
+        const float alpha = fast_exp2(m[n] - mn);  // m = -inf on the first block -> 0
+        m[n] = mn;
+        lacc[n] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[n][d] *= alpha;
+      }
+      const float nm = -m[n];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(s[n][kt][r] - mn);
-          s[n][kt][r] = p;
-          ps += p;
-        }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l[n] = l[n] * alpha + ps;
-      m[n] = mn;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[n][d] *= alpha;
+        for (int r = 0; r < 4; ++r) s[n][kt][r] = fast_exp2(fmaf(s[n][kt][r], sl2, nm));
     }
-    // O^T += V^T . P^T over two 32-key k-steps
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 pb[NQ];
 #pragma unroll
-      for (int n = 0; n < NQ; ++n) pb[n] = pack_acc(s[n][2 * ks], s[n][2 * ks + 1]);
+      for (int n = 0; n < NQ; ++n) {
+        pb[n] = pack_acc(s[n][2 * ks], s[n][2 * ks + 1]);
+        lacc[n] = mfma(ones, pb[n], lacc[n]);  // row sums of P on the MFMA pipe
+      }
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const bf16x8 va = frag_tr(Vs[cur], 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
@@ -230,27 +300,29 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
         for (int n = 0; n < NQ; ++n) o[n][d] = mfma(va, pb[n], o[n][d]);
       }
     }
-    if (more) {  // buffer cur^1 was last read before the previous barrier
-      store_tile(Ks[cur ^ 1], kr);
-      store_tile(Vs[cur ^ 1], vr);
+    if (more) {
+      vmem_wait_tiles(kr, vr);
+      store_tile_v(Ks[cur ^ 1], kr);
+      store_tile_v(Vs[cur ^ 1], vr);
     }
     __syncthreads();
   }
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     if (q[n] < S) {
-      const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
+      const float l = lacc[n][0];
+      const float inv = l > 0.f ? 1.f / l : 0.f;
       uint16_t* op = out + (base + q[n]) * (int64_t)D + h * AH;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        ushort4 u;  // dims d*16 + 4g + r, r = 0..3
+        ushort4 u;
         u.x = f32_to_bf16(o[n][d][0] * inv);
         u.y = f32_to_bf16(o[n][d][1] * inv);
         u.z = f32_to_bf16(o[n][d][2] * inv);
         u.w = f32_to_bf16(o[n][d][3] * inv);
         *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
       }
-      if (g == 0) lse[((int64_t)b * H + h) * S + q[n]] = m[n] + __log2f(l[n]);  // base-2 LSE of scaled scores
+      if (g == 0) lse[((int64_t)b * H + h) * S + q[n]] = m[n] + __log2f(l);
     }
   }
 }
@@ -917,148 +989,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
   }
 }
 
-// ---------------------------------------------------------------------------
-// Forward, ring-staged (opt-in, MLT_ATTN_FWD_RING=3|4): kRing-1 K/V blocks in flight through
-// LDS-DMA (glds) into a ring of stages (counted vmcnt + raw barrier, one __shared__ array, V^T
-// through the asm transpose read), like the backward ring kernels, instead of the register-staged
-// forward's one block ahead. Same arithmetic and order as attn_fwd_kernel: bit-identical outputs.
-// Measured slower than the register-staged forward on BERT shapes (see launch_attn_fwd), so
-// not the default.
-// ---------------------------------------------------------------------------
-template <int NQ, int kRing>
-__global__ __launch_bounds__(256) void attn_fwd_ring_kernel(const uint16_t* __restrict__ qkv,
-                                                            uint16_t* __restrict__ out, float* __restrict__ lse,
-                                                            const int* __restrict__ lens, int S, int H,
-                                                            float scale) {
-  constexpr int STAGE = 2 * kTile;  // K tile, V tile
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
-  int qb, h, b;
-  block_coords(S, 64 * NQ, H, qb, h, b);
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
-  const int D = H * AH;
-  const int64_t ld = 3 * (int64_t)D;
-  const int64_t base = (int64_t)b * S;
-  const int len = lens ? lens[b] : S;
-  MLT_DCHECK(len >= 0 && len <= S);
-  int q[NQ];
-  bf16x8 qf[NQ][2];
-#pragma unroll
-  for (int n = 0; n < NQ; ++n) {
-    q[n] = qb * (64 * NQ) + n * 64 + wid * 16 + i;
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-      qf[n][kh] = q[n] < S ? *reinterpret_cast<const bf16x8*>(qkv + (base + q[n]) * ld + h * AH + kh * 32 + 8 * g)
-                           : bf16x8{};
-  }
-  const int nkb = (len + AB - 1) / AB;
-  // stage = 4 glds per thread: 2 (K) + 2 (V); rows past the valid keys re-read the last valid
-  // row (finite values whose probabilities are exactly 0 after the key mask)
-  auto issue = [&](int slot, int kb) {
-    uint8_t* st = smem + slot * STAGE;
-    const int k0 = kb * AB, nv = min(AB, S - k0);
-    glds_tile(st, qkv, ld, base + k0, nv, D + h * AH);
-    glds_tile(st + kTile, qkv, ld, base + k0, nv, 2 * D + h * AH);
-  };
-#pragma unroll
-  for (int s0 = 0; s0 < kRing - 1; ++s0)
-    if (s0 < nkb) issue(s0, s0);
-  f32x4 o[NQ][4];
-  float m[NQ], l[NQ];
-#pragma unroll
-  for (int n = 0; n < NQ; ++n) {
-    m[n] = -INFINITY;
-    l[n] = 0.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const float sl2 = scale * 1.4426950408889634f;
-  for (int kb = 0; kb < nkb; ++kb) {
-    ring_wait4(min(kRing - 2, nkb - 1 - kb));
-    raw_barrier();  // stage kb visible to all waves; everyone is done with slot (kb - 1) % kRing
-    if (kb + kRing - 1 < nkb) issue((kb + kRing - 1) % kRing, kb + kRing - 1);
-    const uint8_t* Ks = smem + (kb % kRing) * STAGE;
-    const uint8_t* Vs = Ks + kTile;
-    f32x4 s[NQ][4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) s[n][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        const bf16x8 kfr = frag_row(Ks, kt * 16, kh);
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) s[n][kt] = mfma(kfr, qf[n][kh], s[n][kt]);
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-      float bm = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * AB + kt * 16 + 4 * g + r;
-          const float v = key < len ? s[n][kt][r] * sl2 : -INFINITY;
-          s[n][kt][r] = v;
-          bm = fmaxf(bm, v);
-        }
-      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-      const float mn = fmaxf(m[n], bm);
-      const float alpha = fast_exp2(m[n] - mn);
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = fast_exp2(s[n][kt][r] - mn);
-          s[n][kt][r] = pv;
-          ps += pv;
-        }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l[n] = l[n] * alpha + ps;
-      m[n] = mn;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[n][d] *= alpha;
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pb[NQ];
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) pb[n] = pack_acc(s[n][2 * ks], s[n][2 * ks + 1]);
-      bf16x8 va[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) va[d] = frag_tr_asm(Vs, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
-      frag_tr_wait(va);
-#pragma unroll
-      for (int d = 0; d < 4; ++d)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) o[n][d] = mfma(va[d], pb[n], o[n][d]);
-    }
-  }
-#pragma unroll
-  for (int n = 0; n < NQ; ++n) {
-    if (q[n] < S) {
-      const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
-      uint16_t* op = out + (base + q[n]) * (int64_t)D + h * AH;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        ushort4 u;
-        u.x = f32_to_bf16(o[n][d][0] * inv);
-        u.y = f32_to_bf16(o[n][d][1] * inv);
-        u.z = f32_to_bf16(o[n][d][2] * inv);
-        u.w = f32_to_bf16(o[n][d][3] * inv);
-        *reinterpret_cast<ushort4*>(op + d * 16 + 4 * g) = u;
-      }
-      if (g == 0) lse[((int64_t)b * H + h) * S + q[n]] = m[n] + __log2f(l[n]);
-    }
-  }
-}
-
 // 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
 // MLT_ATTN_FWD_GROUPS / MLT_ATTN_DKDV_GROUPS / MLT_ATTN_DQ_GROUPS = 1|2 override the choice
-// Measured (B32 S512 H12): forward 1 group (77.7 vs 82.2 us), dQ 2 groups. dK/dV: with the
+// Measured (B32 / B128, S512, H12): lean forward 2 groups (44.7 vs 49.7 us, 161 vs 185 us), dQ 2 groups. dK/dV: with the
 // register-staged kernel 1 group (2 need > 256 VGPRs and halve the occupancy); with the ring
 // kernels (the default) 2 groups, 10-14 % faster backward at B16..B128 (B32 198 -> 176 us,
 // B128 727 -> 629 us: each Q / dO ring stage feeds twice the MFMAs).
@@ -1072,30 +1005,10 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* 
                      float scale, hipStream_t st) {
   if (B <= 0 || S <= 0) return;
   const unsigned g2 = (unsigned)((S + 127) / 128 * H * B), g1 = (unsigned)((S + 63) / 64 * H * B);
-  // MLT_ATTN_FWD_RING: 0 = register-staged kernel (default), 3 / 4 = ring depth. Measured
-  // (B32 / B128, S512, H12): ring 3 is 4-5 % slower, ring 4 12-18 % slower -- the forward is not
-  // bound by its one-block-ahead K/V loads but by occupancy (48 / 64 KB of LDS per block vs 32).
-  const char* rv = getenv("MLT_ATTN_FWD_RING");
-  const int ring = rv ? atoi(rv) : 0;
-  const bool two = attn_groups("MLT_ATTN_FWD_GROUPS", S, 1) == 2;
-  if (ring == 3 || ring == 4) {
-    if (ring == 3) {
-      if (two)
-        hipLaunchKernelGGL((attn_fwd_ring_kernel<2, 3>), dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
-      else
-        hipLaunchKernelGGL((attn_fwd_ring_kernel<1, 3>), dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
-    } else {
-      if (two)
-        hipLaunchKernelGGL((attn_fwd_ring_kernel<2, 4>), dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
-      else
-        hipLaunchKernelGGL((attn_fwd_ring_kernel<1, 4>), dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
-    }
-    return;
-  }
-  if (two)
-    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+  if (attn_groups("MLT_ATTN_FWD_GROUPS", S, 2) == 2)
+    hipLaunchKernelGGL(attn_fwd_lean_kernel<2>, dim3(g2), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
+    hipLaunchKernelGGL(attn_fwd_lean_kernel<1>, dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
 }
 
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,

@@ -352,28 +352,41 @@ def test_attention_bwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
         assert torch.equal(res["0", grp], res["3", grp]) and torch.equal(res["0", grp], res["4", grp])
 
 
-@pytest.mark.parametrize("B,S,H,use_lens", [(2, 512, 3, False), (3, 200, 2, True), (2, 64, 1, False)])
-def test_attention_fwd_ring_matches_register_staged(dev, B, S, H, use_lens, monkeypatch):
-    """The glds ring-staged forward (MLT_ATTN_FWD_RING) keeps the register-staged forward's
-    arithmetic and order: bit-identical O and LSE, including tails and key masks."""
+@pytest.mark.parametrize("jump", [4.0, 300.0])
+@pytest.mark.parametrize("use_lens", [False, True])
+def test_attention_fwd_defer_max_branches(dev, jump, use_lens):
+    """The forward's defer-max rescale (T13) is data dependent: one key row per head is made a
+    multiple of one query row inside a LATE key block, so that query's running max jumps there --
+    by ~4 (base 2: stays deferred, p up to 2^4 enters O unrescaled) or by ~50 (forces the rescale
+    of O and l mid-sequence). Full-tensor fp64 reference, every query and head checked."""
     C = require_native()
-    g = torch.Generator().manual_seed(7 * S + H)
+    B, S, H = 2, 512, 2
     D = H * 64
-    qkv = _bf((B * S, 3 * D), g, 1.0)
-    lens = None
-    if use_lens:
-        lens = torch.randint(1, S + 1, (B,), generator=g).to(torch.int32).to(dev)
-    res = {}
-    for ring in ("0", "3", "4"):
-        monkeypatch.setenv("MLT_ATTN_FWD_RING", ring)
-        for grp in ("1", "2"):
-            monkeypatch.setenv("MLT_ATTN_FWD_GROUPS", grp)
-            out = torch.full((B * S, D), float("nan"), dtype=torch.bfloat16, device=dev)
-            lse = torch.full((B * H * S,), float("nan"), device=dev)
-            C.attn_fwd(qkv, out, lse, lens, B, S, H, 0.125)
-            res[ring, grp] = (out, lse)
-    for key, (o, l) in res.items():
-        assert torch.equal(o, res["0", key[1]][0]) and torch.equal(l, res["0", key[1]][1]), key
+    g = torch.Generator().manual_seed(11)
+    qkv = (torch.randn(B * S, 3 * D, generator=g) * 0.5)
+    x = qkv.view(B, S, 3, H, 64)
+    qi, kj = 37, 5 * 64 + 9  # query 37 of block 0; key in block 5 of 8
+    for b in range(B):
+        for h in range(H):
+            q = x[b, qi, 0, h]
+            x[b, kj, 1, h] = q * (jump / (q.double().pow(2).sum().item() * 0.125 * 1.4426950408889634))
+    qkv = qkv.to(torch.bfloat16).to(dev)
+    lens = torch.tensor([S, 400], dtype=torch.int32, device=dev) if use_lens else None
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * H * S, device=dev)
+    C.attn_fwd(qkv, out, lse, lens, B, S, H, 0.125)
+    q, k, v = qkv.double().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if lens is not None:
+        mask = torch.arange(S, device=dev)[None, :] < lens[:, None]
+        s = s.masked_fill(~mask[:, None, None, :], float("-inf"))
+    ref = (s.softmax(-1) @ v).permute(0, 2, 1, 3).reshape(B * S, D)
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 2e-2 * max(1.0, ref.abs().max().item()), err
+    row = out.view(B, S, H, 64)[:, qi].double()
+    assert (row - ref.view(B, S, H, 64)[:, qi]).abs().max().item() <= 2e-2
+    torch.testing.assert_close(lse.view(B, H, S).double(), torch.logsumexp(s, -1) / math.log(2), rtol=1e-3,
+                               atol=2e-3)
 
 
 def test_classifier_head_native_matches_torch(dev):
