@@ -14,11 +14,21 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int T_BK = 64, T_NT = 512;
 
-// mn-contiguous images XOR-swizzle the 16-B chunk index within aligned groups of 16 (or 8
-// when a k-row holds 24 chunks) so the permutation never leaves the row
+// mn-contiguous images XOR-swizzle the 16-B chunk index of k-row kk within aligned groups of 16
+// (or 8 when a k-row holds 24 chunks) so the permutation never leaves the row.
+// Rows of 256 / 512 B start at the same bank, so only the chunk position decides the bank. One
+// ds_read_b64_tr_b16 lane group (32 lanes) reads 8 k-rows {8g + q: g = 0..1, q = 0..3} x two
+// adjacent chunks {c0, c0 + 1} (c0 even) x two 8-B halves. The former XOR by (kk & 15) gave the 8
+// rows the values {0..3, 8..11}, whose pairs {x, x ^ 1} collide -> every slot read twice, a 2-way
+// conflict on every transposed read (PMC: SQ_LDS_BANK_CONFLICT = 49 % of the wgrad kernel's LDS
+// cycles). XOR by 2q + 8g (all even, distinct) puts the 16 (row, chunk) pairs on 16 distinct
+// chunk positions: conflict-free.
 template <int CPR>
 struct MnSwz {
-  static constexpr int MASK = CPR % 16 == 0 ? 15 : 7;
+  static constexpr bool WIDE = CPR % 16 == 0;
+  static __device__ __forceinline__ int x(int kk) {
+    return WIDE ? (((kk & 3) << 1) | (((kk >> 3) & 1) << 3)) : (kk & 7);
+  }
 };
 
 // ---- fragments --------------------------------------------------------------------------
@@ -29,13 +39,12 @@ __device__ __forceinline__ bf16x8 tfrag_k(const uint8_t* lds, int row, int kh) {
 }
 template <int RB>  // row bytes of the mn-contiguous image (2 * BM or 2 * BN)
 __device__ __forceinline__ bf16x8 tfrag_mn(const uint8_t* lds, int mn, int kh) {
-  constexpr int SW = MnSwz<RB / 16>::MASK;
   const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int col = mn + 4 * p;
   const int c = col >> 3, half = (col & 7) * 2;
   const int k0 = kh * 32 + 8 * g + q, k1 = k0 + 4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ (k0 & SW)) << 4) + half));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ (k1 & SW)) << 4) + half));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k0 * RB + ((c ^ MnSwz<RB / 16>::x(k0)) << 4) + half));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + k1 * RB + ((c ^ MnSwz<RB / 16>::x(k1)) << 4) + half));
   const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
@@ -53,7 +62,7 @@ __device__ __forceinline__ const uint8_t* glds_src(const uint8_t* __restrict__ b
     return base + ((int64_t)row * ld) * ES + c * 16;
   } else {    // [64 k][ROWS]: ROWS/8 chunks per k-row (bf16 only)
     constexpr int CPR = ROWS / 8;
-    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
+    const int kk = e / CPR, p = e % CPR, c = p ^ MnSwz<CPR>::x(kk);
     const int col = min(mn0 + c * 8, nmn - 8);
     return base + ((int64_t)kk * ld + col) * ES;
   }
@@ -70,7 +79,7 @@ __device__ __forceinline__ uint32_t glds_off(int64_t ld, int i, int mn0, int nmn
     return (uint32_t)(row * ld * ES + c * 16);
   } else {
     constexpr int CPR = ROWS / 8;
-    const int kk = e / CPR, p = e % CPR, c = p ^ (kk & MnSwz<CPR>::MASK);
+    const int kk = e / CPR, p = e % CPR, c = p ^ MnSwz<CPR>::x(kk);
     const int col = min(mn0 + c * 8, nmn - 8);
     return (uint32_t)((kk * ld + col) * ES);
   }

@@ -58,7 +58,12 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
-  const int id = xcd_remap(blockIdx.x, tiles);
+  // XCD-aware remap over the whole (tiles x splits) grid: workgroups are dealt to the 8 XCDs
+  // round-robin in linear order (blockIdx.y * tiles + blockIdx.x). After the remap the ids one XCD
+  // runs at once are consecutive and split-major: tiles of the SAME K-range, which share A / B
+  // panels in that XCD's L2 (remapping blockIdx.x alone scattered them over XCDs in split-K grids)
+  const int lin = xcd_remap((int)(blockIdx.y * tiles + blockIdx.x), tiles * (int)gridDim.y);
+  const int id = lin % tiles, ksplit = lin / tiles;
   // grouped raster: runs of `group_m` tile-rows are walked column by column, so the ~32 blocks
   // an XCD runs at once share a few A row-panels AND a few B column-panels in its L2
   const int tiles_m = tiles / tiles_n;
@@ -72,14 +77,14 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   }
   const int m0 = tm * BM, n0 = tn * BN;
   MLT_DCHECK(m0 < M && n0 < N && tiles % tiles_n == 0);  // tile grid = ceil(M/BM) x ceil(N/BN)
-  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && blockIdx.y * ksteps < (unsigned)(K / (F8A >= 0 ? 128 : T_BK)));
+  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && ksplit * ksteps < (K / (F8A >= 0 ? 128 : T_BK)));
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = (wid / WARPS_N) * WTM, wn = (wid % WARPS_N) * WTN;
   constexpr bool F8 = F8A >= 0;
   constexpr int ES = F8 ? 1 : 2;
   static_assert(!F8 || (F8B >= 0 && !AM && !BNL), "fp8 operands must both be fp8 and k-contiguous");
   const int nk = K / (F8 ? 128 : T_BK);
-  const int kt0 = blockIdx.y * ksteps, kt1 = min(nk, kt0 + ksteps);
+  const int kt0 = ksplit * ksteps, kt1 = min(nk, kt0 + ksteps);
 
   const uint8_t* asrc[A_CH];
   const uint8_t* bsrc[B_CH];
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   const bool ext = gridDim.y > 1 && cnt == nullptr;
   if (gridDim.y > 1 && !ext) {
     constexpr int SLAB = BM * BN;
-    float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB;
+    float* slab = ws + ((int64_t)ksplit * tiles + id) * SLAB;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
   if (ext) alpha = 1.f;
-  float* const wsz = ws + (int64_t)blockIdx.y * M * N;
+  float* const wsz = ws + (int64_t)ksplit * M * N;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (EPR * EPS);
   float bv[TJ];
@@ -349,7 +354,12 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tiles = gridDim.x, tiles_n = (N + BN - 1) / BN;
-  const int id = xcd_remap(blockIdx.x, tiles);
+  // XCD-aware remap over the whole (tiles x splits) grid: workgroups are dealt to the 8 XCDs
+  // round-robin in linear order (blockIdx.y * tiles + blockIdx.x). After the remap the ids one XCD
+  // runs at once are consecutive and split-major: tiles of the SAME K-range, which share A / B
+  // panels in that XCD's L2 (remapping blockIdx.x alone scattered them over XCDs in split-K grids)
+  const int lin = xcd_remap((int)(blockIdx.y * tiles + blockIdx.x), tiles * (int)gridDim.y);
+  const int id = lin % tiles, ksplit = lin / tiles;
   int tm, tn;
   {
     const int tiles_m = tiles / tiles_n;
@@ -361,11 +371,11 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   }
   const int m0 = tm * BM, n0 = tn * BN;
   MLT_DCHECK(m0 < M && n0 < N && tiles % tiles_n == 0);  // tile grid = ceil(M/BM) x ceil(N/BN)
-  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && blockIdx.y * ksteps < (unsigned)(K / (F8A >= 0 ? 128 : T_BK)));
+  MLT_DCHECK(K % (F8A >= 0 ? 128 : T_BK) == 0 && ksplit * ksteps < (K / (F8A >= 0 ? 128 : T_BK)));
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = K / (F8 ? 128 : T_BK);
-  const int kt0 = blockIdx.y * ksteps, kt1 = min(nk, kt0 + ksteps);
+  const int kt0 = ksplit * ksteps, kt1 = min(nk, kt0 + ksteps);
 
   // glds sources of the four half-tiles (0 A0, 1 A1, 2 B0, 3 B1), two 16-B chunks per thread
   // each: 32-bit offsets from the uniform operand bases (the host guarantees < 4 GiB spans)
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   if (gridDim.y > 1 && !ext) {
     constexpr int SLAB = BM * BN;
     const int64_t fo = ((int64_t)wid * NF * 64 + lane) * 4;
-    float* slab = ws + ((int64_t)blockIdx.y * tiles + id) * SLAB + fo;
+    float* slab = ws + ((int64_t)ksplit * tiles + id) * SLAB + fo;
 #pragma unroll
     for (int f = 0; f < NF; ++f) *reinterpret_cast<f32x4*>(slab + f * 256) = acc[f];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -553,7 +563,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
   if (ext) alpha = 1.f;
-  float* const wsz = ws + (int64_t)blockIdx.y * M * N;
+  float* const wsz = ws + (int64_t)ksplit * M * N;
   const int g = lane >> 4, cl = lane & 15;
   float* cs = reinterpret_cast<float*>(smem) + wid * (64 * EPS);
   const EpiSide side = epi_side<OutT>(epi, C, ldc, N, ext);
