@@ -720,7 +720,10 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
         // over cfg 5; FFN1 at N = 3072 -7 %). With bf16 its swapped-operand MFMA order costs ~6 %
         // of the main loop, which the saved fill / drain does not pay back
         // (profiles/gemm_persist_64k_tokens.jsonl) -- bf16 takes it only when forced.
-        if (cfg == 6 && (!allow_persist || s > 1 || nk % 2 || kstep != 128 || N > 2304 ||
+        // At K >= 3072 (the `large` model's FFN2 forward and QKV / FFN1 dgrad, 131K tokens) the
+        // ping-pong tile is 8-11 % faster (profiles/fp8_cfg_large_131k_tokens.jsonl): the fill /
+        // drain it saves is amortised there, its swapped-operand order is not -> only nk <= 8.
+        if (cfg == 6 && (!allow_persist || s > 1 || nk % 2 || nk > 8 || kstep != 128 || N > 2304 ||
                          (int64_t)((M + 255) / 256) * ((N + 255) / 256) < kCUs))
           break;
         if (s > nk) break;
