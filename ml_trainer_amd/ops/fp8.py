@@ -130,7 +130,8 @@ def _state(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
 
 def _weight_key(w: torch.Tensor):
     fp = FlatParams.owner(w)
-    return (fp.generation if fp is not None else w._version, w.data_ptr())
+    # generation: optimizer updates; data._version: load_state_dict / manual edits of the masters
+    return ((fp.generation, fp.data._version) if fp is not None else w._version, w.data_ptr())
 
 
 def weight_fp8(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:

@@ -29,6 +29,7 @@ Linear layout conventions (nn.Linear weight [out, in]):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -50,6 +51,23 @@ def bf16_weight(p: torch.Tensor) -> torch.Tensor:
     return w
 
 
+def bf16_weight_t(p: torch.Tensor) -> torch.Tensor:
+    """W^T (bf16, contiguous [in, out]) of a weight [out, in], re-made once per optimizer update
+    (FlatParams.generation) -- the k-contiguous B operand of the input-gradient GEMM."""
+    fp = FlatParams.owner(p)
+    # generation: optimizer updates; data._version: load_state_dict / manual edits of the masters
+    key = ((fp.generation, fp.data._version) if fp is not None else p._version, p.data_ptr())
+    cache = getattr(p, "_mlt_bf16_t", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    w16 = bf16_weight(p)
+    t = cache[1] if cache is not None else torch.empty(w16.shape[1], w16.shape[0], dtype=torch.bfloat16,
+                                                        device=w16.device)
+    t.copy_(w16.t())
+    p._mlt_bf16_t = (key, t)
+    return t
+
+
 class Bf16Linear:
     """bf16 operands (bf16 shadows of the fp32 masters), fp32 accumulate, fused epilogues."""
 
@@ -59,9 +77,15 @@ class Bf16Linear:
 
     @staticmethod
     def dgrad(dy, w, out, aux=None, res=None):
-        """out = dy . W  (* gelu'(aux) when aux is given) (+ res)."""
-        require_native().gemm(dy, bf16_weight(w), out, False, True, aux=aux, mode=2 if aux is not None else 0,
-                              res=res)
+        """out = dy . W  (* gelu'(aux) when aux is given) (+ res). Large token counts take W^T as
+        a k-contiguous copy (one transpose per weight per step): the forward-layout tile runs
+        8-11 % faster than the n-contiguous-B one on the BERT dgrad shapes."""
+        C = require_native()
+        mode = 2 if aux is not None else 0
+        if dy.shape[0] >= 4096 and os.environ.get("MLT_DGRAD_WT", "1") != "0":
+            C.gemm(dy, bf16_weight_t(w), out, False, False, aux=aux, mode=mode, res=res)
+        else:
+            C.gemm(dy, bf16_weight(w), out, False, True, aux=aux, mode=mode, res=res)
         return out
 
 

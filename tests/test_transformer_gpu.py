@@ -412,3 +412,35 @@ def test_classifier_head_native_matches_torch(dev):
     torch.testing.assert_close(logits, ref, rtol=2e-3, atol=2e-3)
     for g, r in zip(grads, (wpr.grad, bpr.grad, wcr.grad, bcr.grad)):
         torch.testing.assert_close(g, r, rtol=3e-2, atol=3e-3)
+
+
+@pytest.mark.parametrize("with_aux", [False, True])
+def test_dgrad_transposed_weight_matches_n_contiguous(dev, monkeypatch, with_aux):
+    """Large-token dgrads use a cached k-contiguous W^T copy (MLT_DGRAD_WT, default on); the
+    result must match the n-contiguous-B GEMM on the same operands, with and without the dGELU
+    epilogue and the residual, and the cache must follow an optimizer update of the weight."""
+    from ml_trainer_amd.ops import transformer as T
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(4)
+    rows, n_out, k_in = 4096, 256, 192
+    lin = torch.nn.Linear(k_in, n_out).to(dev)
+    fp = FlatParams(lin.parameters())
+    dy = torch.randn(rows, n_out, device=dev).to(torch.bfloat16)
+    res = torch.randn(rows, k_in, device=dev).to(torch.bfloat16)
+    aux = torch.randn(rows, k_in, device=dev).to(torch.bfloat16) if with_aux else None
+    outs = {}
+    for wt in ("1", "0"):
+        monkeypatch.setenv("MLT_DGRAD_WT", wt)
+        out = torch.empty(rows, k_in, dtype=torch.bfloat16, device=dev)
+        outs[wt] = T.BF16.dgrad(dy, lin.weight, out, aux=aux, res=res).clone()
+    torch.testing.assert_close(outs["1"].float(), outs["0"].float(), rtol=1e-2, atol=1e-2)
+    # a manual edit of the fp32 masters (version bump, no optimizer generation) -> rebuilt copy
+    with torch.no_grad():
+        fp.data.mul_(-1.0)
+    monkeypatch.setenv("MLT_DGRAD_WT", "1")
+    out = torch.empty(rows, k_in, dtype=torch.bfloat16, device=dev)
+    T.BF16.dgrad(dy, lin.weight, out, aux=aux, res=res)
+    monkeypatch.setenv("MLT_DGRAD_WT", "0")
+    ref = torch.empty(rows, k_in, dtype=torch.bfloat16, device=dev)
+    T.BF16.dgrad(dy, lin.weight, ref, aux=aux, res=res)
+    torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
