@@ -136,6 +136,16 @@ void cast_bf16(Tensor x, Tensor y) {
   launch_cast_bf16(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), cur_stream());
 }
 
+void transpose_bf16(Tensor src, Tensor dst) {
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && dst.size(0) == src.size(1) && dst.size(1) == src.size(0),
+              "transpose_bf16: dst must be [C, R] for src [R, C]");
+  check_dev(src, "src", at::kBFloat16, src.numel(), 2);
+  check_dev(dst, "dst", at::kBFloat16, dst.numel(), 2);
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "transpose_bf16: contiguous tensors");
+  launch_transpose_bf16(reinterpret_cast<const uint16_t*>(src.data_ptr()), reinterpret_cast<uint16_t*>(dst.data_ptr()),
+                        (int)src.size(0), (int)src.size(1), cur_stream());
+}
+
 // ----------------------------------------------------------------------------
 // CIFAR device augmentation
 // ----------------------------------------------------------------------------
@@ -1050,6 +1060,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sq_norm", &sq_norm);
   m.def("clip_coef", &clip_coef);
   m.def("cast_bf16", &cast_bf16);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("cifar_augment", &cifar_augment);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

@@ -19,6 +19,8 @@ void launch_flat_optim(float* p, const float* g, float* s1, float* s2, int64_t n
 void launch_sq_norm(const float* x, int64_t n, float* out, hipStream_t stream);
 void launch_clip_coef(const float* sq, float max_norm, float* coef, float* total_norm, hipStream_t stream);
 void launch_cast_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
+// dst[C][R] = src[R][C], bf16 (transpose.hip)
+void launch_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t stream);
 
 // ----------------------------------------------------------------------------
 // LeNet-5 (reference src/model.py:7-24) fused forward/backward (lenet.hip)

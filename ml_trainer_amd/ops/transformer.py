@@ -63,7 +63,7 @@ def bf16_weight_t(p: torch.Tensor) -> torch.Tensor:
     w16 = bf16_weight(p)
     t = cache[1] if cache is not None else torch.empty(w16.shape[1], w16.shape[0], dtype=torch.bfloat16,
                                                         device=w16.device)
-    t.copy_(w16.t())
+    require_native().transpose_bf16(w16, t)
     p._mlt_bf16_t = (key, t)
     return t
 

@@ -444,3 +444,14 @@ def test_dgrad_transposed_weight_matches_n_contiguous(dev, monkeypatch, with_aux
     ref = torch.empty(rows, k_in, dtype=torch.bfloat16, device=dev)
     T.BF16.dgrad(dy, lin.weight, ref, aux=aux, res=res)
     torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("R,C,off", [(768, 2304, 0), (3072, 768, 4), (100, 37, 0), (64, 64, 4), (130, 200, 0)])
+def test_transpose_bf16(dev, R, C, off):
+    """transpose.hip vs torch, incl. edge tiles and an only-8-byte-aligned source view."""
+    C_ = require_native()
+    buf = torch.randn(R * C + off, device=dev).to(torch.bfloat16)
+    src = buf[off:off + R * C].view(R, C)
+    dst = torch.full((C, R), float("nan"), dtype=torch.bfloat16, device=dev)
+    C_.transpose_bf16(src, dst)
+    assert torch.equal(dst, src.t())
