@@ -228,4 +228,65 @@ __device__ __forceinline__ int epi_side_kind(const EpiSide& s, const GemmEpi& ep
   return sizeof(OutT) == 4 ? EPI_ACC : 0;
 }
 
+// 16-byte-store epilogue pass for bf16 outputs without a side operand (plain / GELU + saved
+// pre-activation / tanh) of a tile wholly inside C: each lane takes 8 consecutive columns of the
+// staged fp32 image (two float4 LDS reads) and writes them with ONE 16-byte store (two for GELU:
+// pre-activation + output). The epilogue's store tail is issue-bound (MI355X_MICROARCH.md: store
+// tail; cdna_hip_programming.md T21), so half the store instructions of the 8-byte-per-group
+// path. `rc8(it, gm, gn, off)` gives group it's output coordinates / image offset (off % 4 == 0).
+__device__ __forceinline__ bool epi_store8_ok(const GemmEpi& epi, const void* C, int64_t ldc, int N, bool interior,
+                                              bool ext) {
+  if (ext || !interior || epi.res || epi.accumulate || epi.mode == 2 || N % 8 || ldc % 8 ||
+      (((uintptr_t)C) & 15))
+    return false;
+  return epi.mode != 1 || (epi.ldaux % 8 == 0 && (((uintptr_t)epi.aux) & 15) == 0);
+}
+
+__device__ __forceinline__ uint4 pack_bf16x8(const float (&v)[8]) {
+  uint4 o;
+  o.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+  o.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+  o.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
+  o.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
+  return o;
+}
+
+template <int MODE, int EIT8, class RC8>
+__device__ __forceinline__ void epi_store8_loop(uint16_t* __restrict__ C, int64_t ldc, const GemmEpi& epi,
+                                                const float* cs, RC8 rc8) {
+#pragma unroll 4
+  for (int it = 0; it < EIT8; ++it) {
+    int gm, gn, off;
+    rc8(it, gm, gn, off);
+    const float4 a = *reinterpret_cast<const float4*>(cs + off);
+    const float4 b = *reinterpret_cast<const float4*>(cs + off + 4);
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if constexpr (MODE == 1) {
+      const uint4 pre = pack_bf16x8(v);
+      *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) = pre;
+      const uint32_t w[4] = {pre.x, pre.y, pre.z, pre.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] = gelu_f(bf16_to_f32((uint16_t)(w[q] & 0xffff)));
+        v[2 * q + 1] = gelu_f(bf16_to_f32((uint16_t)(w[q] >> 16)));
+      }
+    } else if constexpr (MODE == 3) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = tanhf(v[q]);
+    }
+    *reinterpret_cast<uint4*>(C + (int64_t)gm * ldc + gn) = pack_bf16x8(v);
+  }
+}
+
+template <int EIT8, class RC8>
+__device__ __forceinline__ void epi_store8(uint16_t* __restrict__ C, int64_t ldc, const GemmEpi& epi, const float* cs,
+                                           RC8 rc8) {
+  if (epi.mode == 1)
+    epi_store8_loop<1, EIT8>(C, ldc, epi, cs, rc8);
+  else if (epi.mode == 3)
+    epi_store8_loop<3, EIT8>(C, ldc, epi, cs, rc8);
+  else
+    epi_store8_loop<0, EIT8>(C, ldc, epi, cs, rc8);
+}
+
 }  // namespace mlt

@@ -32,6 +32,9 @@
 
 namespace mlt {
 
+template <int V>
+using PIC = std::integral_constant<int, V>;
+
 template <int BM, int BN, int WARPS_M>
 struct TileGeom {
   static constexpr int A_BYTES = BM * T_BK * 2, B_BYTES = BN * T_BK * 2, BUF = A_BYTES + B_BYTES;
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   };
   // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
   const int sk = epi_side_kind<OutT>(side, epi, m0 + BM <= M && n0 + BN <= N);
+  const bool st8 = sk == 0 && epi_store8_ok(epi, C, ldc, N, m0 + BM <= M && n0 + BN <= N, ext);
   constexpr int HF = WTN % 3 == 0 ? EIT / 3 : EIT / 2;
 #pragma unroll
   for (int h = 0; h < TI / RI; ++h) {
@@ -253,6 +257,18 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
       }
     }
     stage_pass(h);
+    if constexpr (sizeof(OutT) == 2 && (WTN % 8) == 0 && EIT % 2 == 0) {
+      if (st8) {
+        epi_store8<EIT / 2>(reinterpret_cast<uint16_t*>(C), ldc, epi, cs,
+                            [&](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
+                              const int e = it * 64 + lane, row = e / (WTN / 8), c8 = (e % (WTN / 8)) * 8;
+                              gm = m0 + wm + EPR * h + row;
+                              gn = n0 + wn + c8;
+                              off = row * EPS + c8;
+                            });
+        continue;
+      }
+    }
 #pragma unroll 4
     for (int it = 0; it < EIT; ++it) {
       const int e = it * 64 + lane, row = e / (WTN / 4), c4 = (e % (WTN / 4)) * 4;
@@ -589,8 +605,11 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   };
   // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
   const int sk = epi_side_kind<OutT>(side, epi, m0 + 256 <= M && n0 + 256 <= N);
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) {
+  const bool st8 = sk == 0 && epi_store8_ok(epi, C, ldc, N, m0 + 256 <= M && n0 + 256 <= N, ext);
+  // one quadrant per call with a compile-time index: the accumulator array must stay in registers
+  // (a runtime quadrant index -- e.g. a loop the compiler declines to unroll -- puts it on the stack)
+  auto quadrant = [&](auto qc) __attribute__((always_inline)) {
+    constexpr int qd = decltype(qc)::value;
     auto rc = [&](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
       const int e = it * 64 + lane, row = e >> 3, c4 = (e & 7) * 4;
       gm = q_gm0(qd) + row;
@@ -600,20 +619,32 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
     auto stg = [&]() __attribute__((always_inline)) { stage_q(qd); };
     if (sk == EPI_RES) {
       epi_pass_side<EPI_RES, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
-      continue;
+      return;
     }
     if (sk == EPI_DGELU) {
       epi_pass_side<EPI_DGELU, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
-      continue;
+      return;
     }
     if constexpr (sizeof(OutT) == 4) {
       if (sk == EPI_ACC) {
         epi_pass_side<EPI_ACC, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
-        continue;
+        return;
       }
     }
     stage_q(qd);
     const int gm0 = q_gm0(qd), gn0 = q_gn0(qd);
+    if constexpr (sizeof(OutT) == 2) {
+      if (st8) {  // 64 x 32 quadrant: 4 lanes per row, 8 columns each
+        const int row0 = lane >> 2, c8 = (lane & 3) * 8;
+        epi_store8<4>(reinterpret_cast<uint16_t*>(C), ldc, epi, cs,
+                      [=](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
+                        gm = gm0 + 16 * it + row0;
+                        gn = gn0 + c8;
+                        off = (16 * it + row0) * EPS + c8;
+                      });
+        return;
+      }
+    }
 #pragma unroll 4
     for (int it = 0; it < 8; ++it) {
       const int e = it * 64 + lane, row = e >> 3, c4 = (e & 7) * 4;
@@ -627,7 +658,11 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       float vv[4] = {v.x, v.y, v.z, v.w};
       epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
     }
-  }
+  };
+  quadrant(PIC<0>{});
+  quadrant(PIC<1>{});
+  quadrant(PIC<2>{});
+  quadrant(PIC<3>{});
 }
 #undef MLT_PP_SYNC_READS
 #undef MLT_PP_BARRIER
@@ -648,14 +683,15 @@ struct CfgDesc {
 };
 constexpr int kNumCfg = 7;
 // cfg 5 (ping-pong) fitted to the 64K-token BERT shapes (profiles/gemm_bf16_64k_tokens.jsonl):
-// 5 % slower than cfg 1 at K = 768 (12 K-steps: its deeper pipeline fill does not amortise),
-// 8-10 % faster at K = 2304-3072 -> a faster steady state with a larger fixed cost.
+// 8-10 % faster than cfg 1 at K = 2304-3072; since the 16-byte-store epilogue also 3-8 % faster
+// at K = 768 (profiles/gemm_epi16_64k_tokens.jsonl) -> a faster steady state, a small extra
+// fixed cost.
 const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2, 1.0e-6},
                                {256, 256, 1.15e15 / kCUs, 1, 1.0e-6},
                                {256, 128, 0.92e15 / kCUs, 1, 1.0e-6},
                                {128, 256, 0.92e15 / kCUs, 1, 1.0e-6},
                                {256, 192, 1.05e15 / kCUs, 1, 1.0e-6},
-                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6},   // 5: ping-pong
+                               {256, 256, 1.335e15 / kCUs, 1, 2.5e-6},   // 5: ping-pong
                                {256, 256, 1.335e15 / kCUs, 1, 5.6e-6}};  // 6: persistent ping-pong (fill once)
 
 // split-K combine override: -1 planner, 0 in-kernel, 1 external (env MLT_GEMM_SPLIT_EXT, or
@@ -692,9 +728,10 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
   const int64_t slots = (int64_t)kCUs * c.per_cu;
   const int64_t rounds = (blocks + slots - 1) / slots;
   const int nk = (K + kstep - 1) / kstep, ks = (nk + splits - 1) / splits;
-  const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + c.fixed;
+  const double fixed = c.fixed;
+  const double t_block = 2.0 * c.bm * c.bn * kstep * ks / (speed * c.rate / c.per_cu) + fixed;
   double t = rounds * t_block;
-  if (cfg == 6) t = rounds * (t_block - c.fixed) + c.fixed;  // prologue / epilogue overlap the next tile
+  if (cfg == 6) t = rounds * (t_block - fixed) + fixed;  // prologue / epilogue overlap the next tile
   if (splits > 1) t += split_cost(cfg, splits, M, N, nullptr);
   return t;
 }
@@ -715,17 +752,11 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
     for (int cfg = 1; cfg < kNumCfg; ++cfg)
       for (int s = 1; s <= 16; ++s) {
         if (cfg == 5 && !allow_pp) break;
-        // persistent ping-pong: no split-K, even K-tile count, >= one tile per CU; measured to win
-        // only with fp8 operands at N <= 2304 (64K tokens: QKV +8 %, out-proj +12 %, FFN2 +4 %
-        // over cfg 5; FFN1 at N = 3072 -7 %). With bf16 its swapped-operand MFMA order costs ~6 %
-        // of the main loop, which the saved fill / drain does not pay back
-        // (profiles/gemm_persist_64k_tokens.jsonl) -- bf16 takes it only when forced.
-        // At K >= 3072 (the `large` model's FFN2 forward and QKV / FFN1 dgrad, 131K tokens) the
-        // ping-pong tile is 8-11 % faster (profiles/fp8_cfg_large_131k_tokens.jsonl): the fill /
-        // drain it saves is amortised there, its swapped-operand order is not -> only nk <= 8.
-        if (cfg == 6 && (!allow_persist || s > 1 || nk % 2 || nk > 8 || kstep != 128 || N > 2304 ||
-                         (int64_t)((M + 255) / 256) * ((N + 255) / 256) < kCUs))
-          break;
+        // persistent ping-pong (cfg 6): only when forced. It won 4-12 % on the fp8 K = 768 / 1024
+        // shapes while the tile kernels stored 8 bytes per lane; with their 16-byte-store
+        // epilogue the ping-pong tile beats it by 13-20 % there (profiles/gemm_epi16_64k_tokens.jsonl,
+        // profiles/fp8_cfg_large_131k_tokens.jsonl), and at K >= 3072 it already lost by 8-11 %.
+        if (cfg == 6) break;
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
         if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
