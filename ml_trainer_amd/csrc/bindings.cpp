@@ -443,6 +443,63 @@ void gemm_f8(Tensor A, Tensor B, Tensor C, int fmt_a, int fmt_b, Tensor inv_scal
                  ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
 }
 
+// fp8 GEMM whose epilogue quantises its own output: Y (fp8 [M,N]) and Yt (fp8 [N,M]) for the
+// consumer GEMMs, amax into out_amax, and (colsum_out) the column sums of the unquantised output
+void gemm_f8_q(Tensor A, Tensor B, Tensor Y, Tensor Yt, int fmt_a, int fmt_b, Tensor inv_scale_a, Tensor inv_scale_b,
+               int out_fmt, Tensor out_scale, Tensor out_amax, c10::optional<Tensor> bias, c10::optional<Tensor> aux,
+               int mode, c10::optional<Tensor> colsum_out, bool colsum_accumulate) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && Y.dim() == 2 && Yt.dim() == 2, "gemm_f8_q operands must be 2-D");
+  TORCH_CHECK(is_fp8_storage(A) && is_fp8_storage(B) && is_fp8_storage(Y) && is_fp8_storage(Yt),
+              "gemm_f8_q A/B/Y/Yt must be fp8 (or uint8) storage");
+  TORCH_CHECK((fmt_a == 0 || fmt_a == 1) && fmt_b == 0, "gemm_f8_q formats: A e4m3/e5m2, B e4m3");
+  TORCH_CHECK(out_fmt == 0 || out_fmt == 1, "out_fmt: 0 = e4m3, 1 = e5m2");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm_f8_q inner dimensions differ");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0,
+              "gemm_f8_q needs M % 256 == 0, N % 256 == 0, K % 128 == 0");
+  for (const Tensor* t : {&A, &B, &Y, &Yt}) {
+    TORCH_CHECK(t->is_cuda() && t->stride(1) == 1 && t->stride(0) % 16 == 0,
+                "gemm_f8_q operands: device tensors, unit column stride, row stride % 16 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f8_q operands must be 16-byte aligned");
+  }
+  TORCH_CHECK(Y.size(0) == M && Y.size(1) == N && Yt.size(0) == N && Yt.size(1) == M, "gemm_f8_q Y / Yt shapes");
+  check_dev(inv_scale_a, "inv_scale_a", at::kFloat, 1, 4);
+  check_dev(inv_scale_b, "inv_scale_b", at::kFloat, 1, 4);
+  check_dev(out_scale, "out_scale", at::kFloat, 1, 4);
+  check_dev(out_amax, "out_amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    check_dev(*bias, "bias", at::kFloat, N, 4);
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm_f8_q mode (0 none, 1 gelu, 2 dgelu)");
+  const uint16_t* ap = nullptr;
+  int64_t ldaux = 0;
+  if (mode != 0) {
+    TORCH_CHECK(aux.has_value() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
+                    aux->size(1) == N && aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->is_cuda() &&
+                    reinterpret_cast<uintptr_t>(aux->data_ptr()) % 16 == 0,
+                "aux must be a 16-byte aligned bf16 [M,N] with row stride % 8 == 0");
+    ap = bf16_ptr(*aux);
+    ldaux = aux->stride(0);
+  }
+  Tensor part;
+  if (colsum_out.has_value()) {
+    check_dev(*colsum_out, "colsum_out", at::kFloat, N, 16);
+    part = at::empty({M / 64 * N}, A.options().dtype(at::kFloat));
+  }
+  launch_gemm_f8_q(fmt_a, fmt_b, u8(A), u8(B), reinterpret_cast<uint8_t*>(Y.data_ptr()),
+                   reinterpret_cast<uint8_t*>(Yt.data_ptr()), (int)M, (int)N, (int)K, A.stride(0), B.stride(0),
+                   Y.stride(0), Yt.stride(0), inv_scale_a.data_ptr<float>(), inv_scale_b.data_ptr<float>(), bp, ap,
+                   ldaux, mode, out_fmt, out_scale.data_ptr<float>(), out_amax.data_ptr<float>(),
+                   part.defined() ? part.data_ptr<float>() : nullptr, cur_stream());
+  if (part.defined()) {
+    SegOut o{{colsum_out->data_ptr<float>(), nullptr, nullptr}};
+    launch_reduce_rows(part.data_ptr<float>(), (int)(M / 64), N, (int)N, (int)N, o, colsum_accumulate ? 1 : 0,
+                       cur_stream());
+  }
+}
+
 void fp8_cast(Tensor x, Tensor y, Tensor scale, c10::optional<Tensor> amax, int fmt) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
               "fp8_cast x: contiguous bf16/fp32 device tensor");
@@ -1082,6 +1139,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("inv_scale_a"), py::arg("inv_scale_b"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("res") = py::none(), py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false,
         py::arg("cfg") = -1, py::arg("splits") = 0);
+  m.def("gemm_f8_q", &gemm_f8_q, py::arg("A"), py::arg("B"), py::arg("Y"), py::arg("Yt"), py::arg("fmt_a"),
+        py::arg("fmt_b"), py::arg("inv_scale_a"), py::arg("inv_scale_b"), py::arg("out_fmt"), py::arg("out_scale"),
+        py::arg("out_amax"), py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("mode") = 0,
+        py::arg("colsum_out") = py::none(), py::arg("colsum_accumulate") = false);
   m.def("gemm_f8_plan", [](int64_t M, int64_t N, int64_t K, int cfg, int splits) {
     const GemmPlan p = plan_gemm_f8((int)M, (int)N, (int)K, cfg, splits);
     return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);

@@ -18,6 +18,16 @@ struct GemmEpi {
   int accumulate;        // C += result (fp32 output only)
   const float* inv_scale_a = nullptr;  // fp8: device-side 1/scale of A and B (multiplied into alpha)
   const float* inv_scale_b = nullptr;
+  // quantising ("q8") epilogue -- gemm_pp_kernel with OutT = uint8_t: C is the fp8 output [M,N];
+  // the kernel also writes C^T, records amax of the (unscaled) output and optionally the column
+  // partial sums (bias gradient of a dGELU output) -- the consumer GEMM's operands straight from
+  // the producer, no bf16 round trip through HBM
+  uint8_t* qt = nullptr;           // fp8 C^T [N, M], row stride ldqt
+  int64_t ldqt = 0;
+  const float* q_scale = nullptr;  // quantisation scale (device)
+  float* q_amax = nullptr;         // kAmaxSlots amax slots of the output
+  float* q_colpart = nullptr;      // [M / 64, N] fp32 column partial sums, or nullptr
+  int q_fmt = 0;                   // 0 e4m3, 1 e5m2
 };
 
 // erf(z) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 output's ulp):

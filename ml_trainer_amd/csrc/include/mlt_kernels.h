@@ -146,6 +146,14 @@ void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, co
                     const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux,
                     const uint16_t* res, int64_t ldres, float alpha, int mode, int accumulate, float* ws,
                     unsigned* cnt, hipStream_t st);
+// fp8 GEMM with a quantising epilogue (gemm_pp_kernel, OutT = uint8_t): Y = fp8(act(A.B^T*ia*ib
+// + bias) * out_scale) [M,N] and Y^T [N,M] (mode 0 none, 1 GELU writing the bf16 pre-activation
+// to aux, 2 dGELU reading it), amax of act(..) into out_amax, optional [M/64, N] column partials.
+// M % 256 == 0, N % 256 == 0, K % 128 == 0; fmt_a e4m3 or e5m2, fmt_b e4m3.
+void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, uint8_t* Y, uint8_t* Yt, int M, int N,
+                      int K, int64_t lda, int64_t ldb, int64_t ldy, int64_t ldyt, const float* inv_scale_a,
+                      const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux, int mode,
+                      int out_fmt, const float* out_scale, float* out_amax, float* colpart, hipStream_t st);
 // fp8 quantisation (fp8.hip); every amax argument points at kAmaxSlots slots spaced
 // kAmaxStride floats apart (kAmaxSlots * kAmaxStride floats per tensor)
 constexpr int kAmaxSlots = 64, kAmaxStride = 32;

@@ -10,44 +10,10 @@
 //     window, scale = fmt_max / (max(history) * 2^margin), inv_scale = 1 / scale, reset amax.
 // Conversions use v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32 after clamping to the finite range.
 #include "mlt_common.h"
+#include "mlt_fp8.h"
 #include "mlt_kernels.h"
 
 namespace mlt {
-
-template <int FMT>
-__device__ __forceinline__ float fp8_max() {
-  return FMT == 0 ? 448.f : 57344.f;
-}
-
-template <int FMT>
-__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
-  const float m = fp8_max<FMT>();
-  a = fminf(fmaxf(a, -m), m);
-  b = fminf(fmaxf(b, -m), m);
-  c = fminf(fmaxf(c, -m), m);
-  d = fminf(fmaxf(d, -m), m);
-  int r;
-  if constexpr (FMT == 0) {
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  } else {
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
-  }
-  return (uint32_t)r;
-}
-
-// amax is recorded into kAmaxSlots sub-slots (block b -> slot b % kAmaxSlots) so that thousands
-// of blocks do not serialise on one device-scope atomic; update_scale reduces the slots.
-// Slots sit kAmaxStride floats apart (one 128-B line each), and a block only issues the
-// atomic when its maximum beats the slot's current value -- after the first few blocks almost
-// none do, so the tail of thousands of same-line device-scope atomics disappears.
-__device__ __forceinline__ void atomic_max_pos(float* slots, float v) {
-  // |x| >= 0: IEEE ordering of non-negative floats equals their integer ordering
-  unsigned* a = reinterpret_cast<unsigned*>(slots + ((blockIdx.x + blockIdx.y * gridDim.x) % kAmaxSlots) * kAmaxStride);
-  const unsigned u = __float_as_uint(v);
-  if (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < u) atomicMax(a, u);
-}
 
 __device__ __forceinline__ void load8(const uint16_t* p, float (&v)[8]) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);

@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "mlt_common.h"
+#include "mlt_fp8.h"
 #include "mlt_gemm.h"
 #include "mlt_gemm_tile.h"
 #include "mlt_kernels.h"
@@ -357,6 +358,89 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <int V>
 using IC = std::integral_constant<int, V>;
 
+// ---- quantising ("q8") epilogue of one 64x32 quadrant -------------------------------------
+// cs: the wave's staged fp32 image of the quadrant (row stride 36, alpha and bias applied),
+// rows gm0 + 0..63, columns gn0 + 0..31, wholly inside C. Row pass: 2 lanes per row, 16 columns
+// each -- the activation (GELU: pre-activation saved as bf16; dGELU: times gelu'(aux)), amax, one
+// 16-byte fp8 store of C; the final fp32 values go back into the image. Column pass: one column
+// per lane, 32 rows per half-wave (conflict-free: the 32 lanes of a half read 32 consecutive
+// banks) -> two 16-byte stores of C^T (the consumer GEMM's k-contiguous operand) and the
+// column partial sum of the quadrant (bias gradient), both halves combined by one shuffle.
+template <int FMT>
+__device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc, const GemmEpi& epi, float* cs,
+                                            int gm0, int gn0, int N, int lane, float& amx) {
+  constexpr int EPS = 36;
+  const float s = *epi.q_scale;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int row = it * 32 + (lane >> 1), c16 = (lane & 1) * 16;
+    float* p = cs + row * EPS + c16;
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 t = reinterpret_cast<const float4*>(p)[q];
+      v[4 * q] = t.x;
+      v[4 * q + 1] = t.y;
+      v[4 * q + 2] = t.z;
+      v[4 * q + 3] = t.w;
+    }
+    const int64_t gm = gm0 + row;
+    const int gn = gn0 + c16;
+    if (epi.mode == 1) {  // GELU: save the bf16 pre-activation, activate its rounded value
+      uint16_t* ap = const_cast<uint16_t*>(epi.aux) + gm * epi.ldaux + gn;
+      float lo[8], hi[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        lo[q] = v[q];
+        hi[q] = v[8 + q];
+      }
+      reinterpret_cast<uint4*>(ap)[0] = pack_bf16x8(lo);
+      reinterpret_cast<uint4*>(ap)[1] = pack_bf16x8(hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = gelu_f(bf16_to_f32(f32_to_bf16(v[q])));
+    } else if (epi.mode == 2) {  // dGELU: times gelu'(pre-activation)
+      const uint4* ap = reinterpret_cast<const uint4*>(epi.aux + gm * epi.ldaux + gn);
+      const uint4 a0 = ap[0], a1 = ap[1];
+      const uint32_t w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v[2 * q] *= gelu_grad(__uint_as_float(w[q] << 16));
+        v[2 * q + 1] *= gelu_grad(__uint_as_float(w[q] & 0xffff0000u));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      reinterpret_cast<float4*>(p)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v[4 * q]), fabsf(v[4 * q + 1])), fmaxf(fabsf(v[4 * q + 2]), fabsf(v[4 * q + 3]))));
+      o[q] = pack4_fp8<FMT>(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
+    }
+    *reinterpret_cast<uint4*>(C + gm * ldc + gn) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  const int col = lane & 31, r0 = (lane >> 5) * 32;
+  const float* p = cs + r0 * EPS + col;
+  uint32_t w[8];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = p[(4 * k + j) * EPS];
+    sum += (x[0] + x[1]) + (x[2] + x[3]);
+    w[k] = pack4_fp8<FMT>(x[0] * s, x[1] * s, x[2] * s, x[3] * s);
+  }
+  uint4* tp = reinterpret_cast<uint4*>(epi.qt + (int64_t)(gn0 + col) * epi.ldqt + gm0 + r0);
+  tp[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  tp[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  if (epi.q_colpart) {
+    sum += __shfl_xor(sum, 32);
+    if (lane < 32) epi.q_colpart[(int64_t)(gm0 >> 6) * N + gn0 + col] = sum;
+  }
+}
+
 template <bool AM, bool BNL, typename OutT, int F8A = -1, int F8B = -1>
 __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restrict__ A,
                                                           const uint8_t* __restrict__ B, OutT* __restrict__ C,
@@ -608,6 +692,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   const bool st8 = sk == 0 && epi_store8_ok(epi, C, ldc, N, m0 + 256 <= M && n0 + 256 <= N, ext);
   // one quadrant per call with a compile-time index: the accumulator array must stay in registers
   // (a runtime quadrant index -- e.g. a loop the compiler declines to unroll -- puts it on the stack)
+  float q_amx = 0.f;  // q8: max |output| over this wave's quadrants
   auto quadrant = [&](auto qc) __attribute__((always_inline)) {
     constexpr int qd = decltype(qc)::value;
     auto rc = [&](int it, int& gm, int& gn, int& off) __attribute__((always_inline)) {
@@ -616,6 +701,14 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       gn = q_gn0(qd) + c4;
       off = row * EPS + c4;
     };
+    if constexpr (sizeof(OutT) == 1) {  // quantising epilogue (interior tiles, no split: host-checked)
+      stage_q(qd);
+      if (epi.q_fmt == 0)
+        q8_quadrant<0>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx);
+      else
+        q8_quadrant<1>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx);
+      return;
+    } else {
     auto stg = [&]() __attribute__((always_inline)) { stage_q(qd); };
     if (sk == EPI_RES) {
       epi_pass_side<EPI_RES, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
@@ -658,11 +751,18 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       float vv[4] = {v.x, v.y, v.z, v.w};
       epilogue_store4<OutT>(C, ldc, epi, gm, gn, N, vv);
     }
+    }
   };
   quadrant(PIC<0>{});
   quadrant(PIC<1>{});
   quadrant(PIC<2>{});
   quadrant(PIC<3>{});
+  if constexpr (sizeof(OutT) == 1) {
+    if (epi.q_amax) {
+      q_amx = wave_max(q_amx);
+      if (lane == 0) atomic_max_pos(epi.q_amax, q_amx);
+    }
+  }
 }
 #undef MLT_PP_SYNC_READS
 #undef MLT_PP_BARRIER
@@ -977,6 +1077,25 @@ void launch_gemm_f8(const GemmPlan& plan, int fmt_a, int fmt_b, bool out_f32, co
   MLT_F8_CASE(1, 0)
   MLT_F8_CASE(0, 1)
 #undef MLT_F8_CASE
+}
+
+void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, uint8_t* Y, uint8_t* Yt, int M, int N,
+                      int K, int64_t lda, int64_t ldb, int64_t ldy, int64_t ldyt, const float* inv_scale_a,
+                      const float* inv_scale_b, const float* bias, const uint16_t* aux, int64_t ldaux, int mode,
+                      int out_fmt, const float* out_scale, float* out_amax, float* colpart, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;  // the host binding checks M % 256, N % 256, K % 128
+  GemmEpi e{bias, aux, nullptr, ldaux, 0, 1.f, mode, 0, inv_scale_a, inv_scale_b};
+  e.qt = Yt;
+  e.ldqt = ldyt;
+  e.q_scale = out_scale;
+  e.q_amax = out_amax;
+  e.q_colpart = colpart;
+  e.q_fmt = out_fmt;
+  GemmPlan p{5, 1, K / 128, 0, 0};
+  if (fmt_a == 0 && fmt_b == 0)
+    launch_pp<false, false, uint8_t, 0, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);
+  else if (fmt_a == 1 && fmt_b == 0)
+    launch_pp<false, false, uint8_t, 1, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);
 }
 
 }  // namespace mlt

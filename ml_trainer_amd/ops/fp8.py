@@ -19,6 +19,7 @@ Everything else in the block (bias, GELU, residual, LayerNorm, attention) is unc
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import torch
@@ -107,7 +108,7 @@ def context(device: torch.device) -> Fp8Context:
 
 
 class _WeightState:
-    __slots__ = ("mx", "mw", "mdy", "w8", "w8t", "key", "xt", "dy8")
+    __slots__ = ("mx", "mw", "mdy", "w8", "w8t", "key", "xt", "dy8", "dyt")
 
     def __init__(self, ctx: Fp8Context):
         self.mx = ctx.new_meta(E4M3)
@@ -118,6 +119,7 @@ class _WeightState:
         self.key = None
         self.xt = None   # (x.data_ptr(), X^T in e4m3) of the last forward, for the fp8 weight gradient
         self.dy8 = None  # (dy.data_ptr(), dY in e5m2) cast by wgrad, reused by the dgrad that follows
+        self.dyt = None  # dY^T in e5m2 written by the producing GEMM's quantising epilogue (FFN1)
 
 
 def _state(w: torch.Tensor, ctx: Fp8Context) -> _WeightState:
@@ -173,7 +175,11 @@ class Fp8Linear:
         C = require_native()
         ctx = context(x.device)
         st = weight_fp8(w, ctx)
-        if Fp8Linear.training and _fp8_wgrad_ok(x, w):
+        if x.dtype == _DT[E4M3]:
+            # quantised by the producer's epilogue with this weight's input scale (fwd_gelu_q),
+            # which also left X^T in st.xt
+            x8 = x
+        elif Fp8Linear.training and _fp8_wgrad_ok(x, w):
             x8, x8t = ctx.cast_t(x, st.mx, E4M3)
             st.xt = (x.data_ptr(), x8t)
         else:
@@ -194,8 +200,14 @@ class Fp8Linear:
             return None
         C = require_native()
         ctx = context(dy.device)
-        dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2, colsum_out=db_out, colsum_accumulate=db_acc)
-        st.dy8 = (dy.data_ptr(), dy8)
+        if dy.dtype == _DT[E5M2]:
+            # dY (+ dY^T, + bias gradient) from the producer's quantising epilogue (dgrad_gelu_q)
+            if st.dyt is None or st.dy8 is None or st.dy8[0] != dy.data_ptr():
+                raise RuntimeError("fp8 wgrad: pre-quantised dY without its transpose")
+            dy8t, st.dyt = st.dyt, None
+        else:
+            dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2, colsum_out=db_out, colsum_accumulate=db_acc)
+            st.dy8 = (dy.data_ptr(), dy8)
         acc = out is not None
         if out is None:
             out = torch.empty(w.shape[0], w.shape[1], dtype=torch.float32, device=dy.device)
@@ -208,7 +220,9 @@ class Fp8Linear:
         C = require_native()
         ctx = context(dy.device)
         st = weight_fp8(w, ctx)
-        if st.dy8 is not None and st.dy8[0] == dy.data_ptr():
+        if dy.dtype == _DT[E5M2]:
+            dy8 = dy
+        elif st.dy8 is not None and st.dy8[0] == dy.data_ptr():
             dy8 = st.dy8[1]
         else:
             dy8 = ctx.cast(dy, st.mdy, E5M2)
@@ -216,6 +230,74 @@ class Fp8Linear:
         C.gemm_f8(dy8, st.w8t, out, E5M2, E4M3, ctx.inv(st.mdy), ctx.inv(st.mw), aux=aux,
                   mode=2 if aux is not None else 0, res=res)
         return out
+
+
+    # ---- FFN fusion: the GEMM epilogues quantise for the next GEMM ------------------------------
+    # FFN1's forward epilogue writes GELU(.) as FFN2's e4m3 input and its transpose (FFN2's wgrad
+    # operand); FFN2's dgrad epilogue writes dGELU(.) as FFN1's e5m2 dY, its transpose and FFN1's
+    # bias gradient. The bf16 intermediate [tokens, 4H] and its cast-transpose pass (one read +
+    # two writes of the widest activation of the layer, twice per step) disappear.
+    fuse_q = os.environ.get("MLT_FP8_FUSE", "1") != "0"
+
+    @staticmethod
+    def _q_shape_ok(x, w1) -> bool:
+        return (x.shape[0] % 256 == 0 and w1.shape[0] % 256 == 0 and x.shape[1] % 128 == 0
+                and _fp8_wgrad_ok(x, w1))
+
+    @staticmethod
+    def fwd_gelu_q(x, w1, b1, pre, w2):
+        """a = GELU(x . W1^T + b1) quantised with W2's input scale: returns e4m3 ``a`` [M, F]
+        (pre-activation saved in ``pre``; a^T kept for W2's wgrad), or None when not applicable
+        (inference, shapes, or W2's input scale not initialised yet -- the first step)."""
+        if not (Fp8Linear.fuse_q and Fp8Linear.training and Fp8Linear._q_shape_ok(x, w1)):
+            return None
+        C = require_native()
+        ctx = context(x.device)
+        st2 = _state(w2, ctx)
+        if not ctx._ready[st2.mx]:
+            return None
+        st1 = weight_fp8(w1, ctx)
+        x8, x8t = ctx.cast_t(x, st1.mx, E4M3)
+        st1.xt = (x.data_ptr(), x8t)
+        M, F = x.shape[0], w1.shape[0]
+        a8 = torch.empty(M, F, dtype=_DT[E4M3], device=x.device)
+        a8t = torch.empty(F, M, dtype=_DT[E4M3], device=x.device)
+        C.gemm_f8_q(x8, st1.w8, a8, a8t, E4M3, E4M3, ctx.inv(st1.mx), ctx.inv(st1.mw), E4M3,
+                    ctx.scale[st2.mx:st2.mx + 1], ctx.amax[st2.mx], bias=b1, aux=pre, mode=1)
+        st2.xt = (a8.data_ptr(), a8t)
+        return a8
+
+    @staticmethod
+    def dgrad_gelu_q_ready(w1, x) -> bool:
+        """Whether dgrad_gelu_q can produce W1's dY: its e5m2 scale exists and the forward left
+        X^T for W1's fp8 wgrad."""
+        st1 = getattr(w1, "_mlt_f8", None)
+        return (st1 is not None and context(x.device)._ready[st1.mdy] and st1.xt is not None
+                and st1.xt[0] == x.data_ptr())
+
+    @staticmethod
+    def dgrad_gelu_q(dy, w2, pre, w1, db_out, db_acc: bool):
+        """dpre = (dy . W2) * gelu'(pre) quantised with W1's dY scale: returns e5m2 dpre [M, F];
+        dpre^T is left for W1's wgrad, sum over rows of dpre goes to ``db_out`` (set or
+        accumulated). Call only when dgrad_gelu_q_ready(w1, x)."""
+        C = require_native()
+        ctx = context(dy.device)
+        st2 = weight_fp8(w2, ctx)
+        st1 = _state(w1, ctx)
+        if st2.dy8 is not None and st2.dy8[0] == dy.data_ptr():
+            dy8 = st2.dy8[1]
+        else:
+            dy8 = ctx.cast(dy, st2.mdy, E5M2)
+        st2.dy8 = None
+        M, F = dy.shape[0], w2.shape[1]
+        d8 = torch.empty(M, F, dtype=_DT[E5M2], device=dy.device)
+        d8t = torch.empty(F, M, dtype=_DT[E5M2], device=dy.device)
+        C.gemm_f8_q(dy8, st2.w8t, d8, d8t, E5M2, E4M3, ctx.inv(st2.mdy), ctx.inv(st2.mw), E5M2,
+                    ctx.scale[st1.mdy:st1.mdy + 1], ctx.amax[st1.mdy], aux=pre, mode=2,
+                    colsum_out=db_out, colsum_accumulate=db_acc)
+        st1.dy8 = (d8.data_ptr(), d8)
+        st1.dyt = d8t
+        return d8
 
 
 FP8 = Fp8Linear()

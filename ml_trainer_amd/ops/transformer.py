@@ -210,7 +210,10 @@ def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
 
 def _ffn_fwd(x, w1, b1, w2, b2, impl=BF16):
     pre = torch.empty(x.shape[0], w1.shape[0], dtype=torch.bfloat16, device=x.device)
-    a = impl.fwd(x, w1, b1, gelu_aux=pre)  # a = gelu(pre), pre saved
+    # fp8: FFN1's epilogue may emit FFN2's quantised input directly (Fp8Linear.fwd_gelu_q)
+    a = impl.fwd_gelu_q(x, w1, b1, pre, w2) if hasattr(impl, "fwd_gelu_q") else None
+    if a is None:
+        a = impl.fwd(x, w1, b1, gelu_aux=pre)  # a = gelu(pre), pre saved
     y = impl.fwd(a, w2, b2, res=x)
     return y, (x, pre, a)
 
@@ -221,6 +224,14 @@ def _ffn_bwd(saved, params, dy, G, db2="colsum", impl=BF16):
     dw2 = G.wgrad(w2, dy, a, impl)
     if isinstance(db2, str):
         db2 = G.colsum(b2, dy)
+    if a.dtype == torch.float8_e4m3fn and impl.dgrad_gelu_q_ready(w1, x):
+        # fp8 FFN fusion: FFN2's dgrad epilogue emits FFN1's e5m2 dY, dY^T and bias gradient
+        gb = G.sink(b1)
+        db1 = gb if gb is not None else torch.empty(w1.shape[0], dtype=torch.float32, device=dy.device)
+        d8 = impl.dgrad_gelu_q(dy, w2, pre, w1, db1, gb is not None)
+        dw1 = G.wgrad(w1, d8, x, impl)
+        dx = impl.dgrad(d8, w1, torch.empty_like(x), res=dy)
+        return dx, dw1, (None if gb is not None else db1), dw2, db2
     dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
     dw1, db1 = G.wgrad_bias(w1, b1, dpre, x, impl)
     dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)

@@ -1,0 +1,144 @@
+"""fp8 GEMM with a quantising epilogue (gemm_tile.hip q8_quadrant, C.gemm_f8_q) and the fused
+FFN path built on it (ops/fp8.py fwd_gelu_q / dgrad_gelu_q) vs plain torch fp32 references."""
+import math
+
+import pytest
+import torch
+
+from ml_trainer_amd.ops._ext import require_native
+
+pytestmark = pytest.mark.gpu
+
+F8 = {0: torch.float8_e4m3fn, 1: torch.float8_e5m2}
+FMAX = {0: 448.0, 1: 57344.0}
+
+
+def _rand_f8(shape, fmt, g, dev, scale=1.0):
+    x = torch.randn(*shape, generator=g) * scale
+    return x.clamp(-FMAX[fmt], FMAX[fmt]).to(F8[fmt]).to(dev)
+
+
+def _gelu(x):
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+
+def _gelu_grad(x):
+    return 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2.0 * math.pi)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024)])
+def test_gemm_f8_q_matches_fp32(dev, mode, shape):
+    C = require_native()
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K + mode)
+    fa = 1 if mode == 2 else 0        # dgrad: e5m2 dY x e4m3 W^T
+    fo = 1 if mode == 2 else 0        # dgrad output is a gradient (e5m2)
+    A = _rand_f8((M, K), fa, g, dev, 2.0)
+    B = _rand_f8((N, K), 0, g, dev, 2.0)
+    isa = torch.tensor([0.5], device=dev)
+    isb = torch.tensor([0.125], device=dev)
+    scale = torch.tensor([3.0], device=dev)
+    amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
+    acc = (A.float() @ B.float().t()) * (0.5 * 0.125)
+    bias = torch.randn(N, generator=g).to(dev) if mode != 2 else None
+    if bias is not None:
+        acc = acc + bias
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    if mode == 1:
+        ref = _gelu(acc.to(torch.bfloat16).float())
+    elif mode == 2:
+        aux.copy_((torch.randn(M, N, generator=g) * 2).to(torch.bfloat16))
+        ref = acc * _gelu_grad(aux.float())
+    else:
+        ref = acc
+    Y = torch.empty(M, N, dtype=F8[fo], device=dev)
+    Yt = torch.empty(N, M, dtype=F8[fo], device=dev)
+    cs = torch.full((N,), 7.0, device=dev) if mode == 2 else None
+    C.gemm_f8_q(A, B, Y, Yt, fa, 0, isa, isb, fo, scale, amax, bias=bias, aux=aux if mode else None, mode=mode,
+                colsum_out=cs, colsum_accumulate=True)
+    # the transposed copy is the same bytes
+    assert torch.equal(Yt.view(torch.uint8), Y.view(torch.uint8).t().contiguous())
+    if mode == 1:  # saved pre-activation
+        torch.testing.assert_close(aux.float(), acc, rtol=1e-2, atol=1e-2 * acc.abs().max().item())
+    q_ref = (ref * 3.0).clamp(-FMAX[fo], FMAX[fo])
+    # one fp8 ulp (2^-3 e4m3, 2^-2 e5m2 relative) for values near a rounding boundary of a
+    # differently-ordered fp32 accumulation
+    rel = 0.13 if fo == 0 else 0.26
+    torch.testing.assert_close(Y.float(), q_ref, rtol=rel, atol=1e-2 * q_ref.abs().max().item())
+    exact = (Y.float() == q_ref.to(F8[fo]).float()).float().mean().item()
+    assert exact > 0.97, exact
+    torch.testing.assert_close(amax.max().view(1), ref.abs().max().view(1), rtol=1e-3, atol=1e-5)
+    if cs is not None:
+        torch.testing.assert_close(cs, 7.0 + ref.sum(0), rtol=1e-3, atol=1e-3 * ref.abs().sum(0).max().item())
+
+
+def test_gemm_f8_q_rejects_edge_shapes(dev):
+    C = require_native()
+    A = torch.zeros(320, 128, dtype=torch.float8_e4m3fn, device=dev)
+    B = torch.zeros(256, 128, dtype=torch.float8_e4m3fn, device=dev)
+    Y = torch.empty(320, 256, dtype=torch.float8_e4m3fn, device=dev)
+    Yt = torch.empty(256, 320, dtype=torch.float8_e4m3fn, device=dev)
+    one = torch.ones(1, device=dev)
+    amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
+    with pytest.raises(RuntimeError):
+        C.gemm_f8_q(A, B, Y, Yt, 0, 0, one, one, 0, one, amax)
+
+
+def _ffn_step(dev, fuse, seed=0):
+    """Two forward/backward passes of one fp8 FFN block (the first initialises the scales, the
+    second takes the fused path when ``fuse``); returns output and gradients of the second."""
+    from ml_trainer_amd.ops import fp8 as f8
+    from ml_trainer_amd.ops.transformer import ffn_block
+    f8._CTX.clear()
+    old = f8.Fp8Linear.fuse_q
+    f8.Fp8Linear.fuse_q = fuse
+    try:
+        g = torch.Generator().manual_seed(seed)
+        H, F, M = 256, 1024, 512
+        w1 = (torch.randn(F, H, generator=g) * 0.05).to(dev).requires_grad_()
+        b1 = (torch.randn(F, generator=g) * 0.1).to(dev).requires_grad_()
+        w2 = (torch.randn(H, F, generator=g) * 0.05).to(dev).requires_grad_()
+        b2 = (torch.randn(H, generator=g) * 0.1).to(dev).requires_grad_()
+        x = torch.randn(M, H, generator=g).to(dev).to(torch.bfloat16).requires_grad_()
+        dy = torch.randn(M, H, generator=g).to(dev).to(torch.bfloat16)
+        out = None
+        for _ in range(2):
+            for p in (w1, b1, w2, b2, x):
+                p.grad = None
+            out = ffn_block(x, w1, b1, w2, b2, impl=f8.FP8)
+            out.backward(dy)
+            f8.context(dev).update()
+        return out.detach().float(), [p.grad.detach().float().clone() for p in (x, w1, b1, w2, b2)]
+    finally:
+        f8.Fp8Linear.fuse_q = old
+        f8._CTX.clear()
+
+
+def test_fused_ffn_matches_unfused(dev):
+    """Fused (quantising epilogues) and unfused (bf16 intermediate + cast kernels) fp8 FFN agree
+    to fp8 precision, and the fused path really ran (no bf16 intermediate was saved)."""
+    from ml_trainer_amd.ops import fp8 as f8
+    called = {"f": 0, "b": 0}
+    fwd0, bwd0 = f8.Fp8Linear.fwd_gelu_q, f8.Fp8Linear.dgrad_gelu_q
+
+    def fwd_spy(*a, **k):
+        r = fwd0(*a, **k)
+        called["f"] += r is not None
+        return r
+
+    def bwd_spy(*a, **k):
+        called["b"] += 1
+        return bwd0(*a, **k)
+
+    f8.Fp8Linear.fwd_gelu_q, f8.Fp8Linear.dgrad_gelu_q = staticmethod(fwd_spy), staticmethod(bwd_spy)
+    try:
+        yf, gf = _ffn_step(dev, True)
+    finally:
+        f8.Fp8Linear.fwd_gelu_q, f8.Fp8Linear.dgrad_gelu_q = staticmethod(fwd0), staticmethod(bwd0)
+    assert called["f"] == 1 and called["b"] == 1, called  # second pass only (first initialises scales)
+    yu, gu = _ffn_step(dev, False)
+    assert ((yf - yu).norm() / yu.norm()).item() < 3e-2
+    for name, a, b in zip(("x", "w1", "b1", "w2", "b2"), gf, gu):
+        r = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert r < 6e-2, (name, r)
