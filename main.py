@@ -14,7 +14,7 @@ CIFAR-shaped dataset and says so in the log.
 
 Extension flags (not in the reference): ``--model`` (default/tiny/bert-base/
 large), ``--synthetic``, ``--per_device_batch``, ``--no_engine``,
-``--no_parallel``, ``--resume``, ``--amp bf16``, ``--metrics_jsonl``, ``--zero_stage``.
+``--no_parallel``, ``--resume``, ``--amp bf16``, ``--metrics_jsonl``, ``--log_jsonl``, ``--zero_stage``.
 """
 from __future__ import annotations
 
@@ -92,6 +92,9 @@ def main(args):
                "zero_stage": args.zero_stage}
     if args.no_engine:
         options["use_engine"] = False
+    if args.log_jsonl:  # every structured log record, one JSON object per line
+        from ml_trainer_amd.utils.logging import add_jsonl_sink
+        add_jsonl_sink(args.log_jsonl)
     trainer = Trainer(model, datasets=datasets, epochs=args.epochs, batch_size=args.batch_size,
                       is_parallel=not args.no_parallel, save_history=True, options=options, **config)
     trainer.fit()
@@ -137,6 +140,7 @@ def build_parser() -> argparse.ArgumentParser:
                         help="1: ZeRO-1 sharded optimizer state (reduce-scatter / all-gather) under DDP")
     parser.add_argument("--amp", type=str, default=None, choices=[None, "bf16"])
     parser.add_argument("--metrics_jsonl", type=str, default=None)
+    parser.add_argument("--log_jsonl", type=str, default=None, help="mirror log records into this JSON-lines file")
     parser.add_argument("--no_progress", action="store_true")
     return parser
 

@@ -34,10 +34,14 @@ def test_cli_end_to_end_cpu_gloo(tmp_path):
                PYTHONPATH=ROOT)
     cmd = [sys.executable, os.path.join(ROOT, "main.py"), "--epochs", "2", "--batch_size", "32", "--synthetic",
            "--synthetic_size", "96", "--model", "tiny", "--metric", "accuracy", "--backend", "gloo",
-           "--custom_function", "true", "--model_dir", str(tmp_path), "--no_progress"]
+           "--custom_function", "true", "--model_dir", str(tmp_path), "--no_progress",
+           "--log_jsonl", str(tmp_path / "log.jsonl")]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     assert "Training Complete." in p.stdout and "EPOCH 2 / 2" in p.stdout
+    import json
+    recs = [json.loads(line) for line in open(tmp_path / "log.jsonl")]
+    assert recs and all(isinstance(r, dict) for r in recs)  # --log_jsonl mirrors the log records
     assert (tmp_path / "model.pth").exists() and (tmp_path / "history.pkl").exists()
     from ml_trainer_amd.utils.utils import load_history
     h = load_history(str(tmp_path))
