@@ -337,7 +337,8 @@ static const uint16_t* bf16_ptr(const Tensor& t) { return reinterpret_cast<const
 // A, B, C are 2-D (row-major, unit column stride). a_mn / b_mn describe the storage:
 //   A: [M,K] (a_mn=0) or [K,M] (a_mn=1);  B: [N,K] (b_mn=0) or [K,N] (b_mn=1);  C: [M,N].
 void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tensor> bias, c10::optional<Tensor> aux,
-          c10::optional<Tensor> res, double alpha, int mode, bool accumulate, int cfg, int splits) {
+          c10::optional<Tensor> res, double alpha, int mode, bool accumulate, int cfg, int splits,
+          c10::optional<Tensor> colsum_out, bool colsum_accumulate) {
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm A/B must be bf16");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm C must be bf16 or fp32");
@@ -377,12 +378,33 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
     ldres = res->stride(0);
   }
   TORCH_CHECK(!accumulate || C.scalar_type() == at::kFloat, "accumulate needs an fp32 output");
+  Tensor part;
+  if (colsum_out.has_value()) {
+    // column sums of the dGELU output (the bias gradient of the layer that produced aux) from the
+    // ping-pong kernel's epilogue: every tile must take its dGELU side-operand pass
+    TORCH_CHECK(mode == 2 && !res.has_value() && !accumulate && C.scalar_type() == at::kBFloat16 && !a_mn,
+                "colsum_out: dGELU mode, bf16 output, k-contiguous A, no residual / accumulate");
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && C.stride(0) % 8 == 0 && ldaux % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(ap) % 16 == 0,
+                "colsum_out needs M % 256 == 0, N % 256 == 0, K % 64 == 0 and 16-byte aligned rows of C / aux");
+    check_dev(*colsum_out, "colsum_out", at::kFloat, N, 16);
+    cfg = 5;
+    splits = 1;
+    part = at::empty({M / 64 * N}, A.options().dtype(at::kFloat));
+  }
   const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
+  TORCH_CHECK(!part.defined() || (plan.cfg == 5 && plan.splits == 1), "colsum_out: ping-pong plan expected");
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, A.options().dtype(at::kFloat));
   launch_gemm_bf16(plan, a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M,
                    (int)N, (int)K, A.stride(0), B.stride(0), C.stride(0), bp, ap, ldaux, rp, ldres, (float)alpha, mode,
-                   accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
+                   accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream(),
+                   part.defined() ? part.data_ptr<float>() : nullptr);
+  if (part.defined()) {
+    SegOut o{{colsum_out->data_ptr<float>(), nullptr, nullptr}};
+    launch_reduce_rows(part.data_ptr<float>(), (int)(M / 64), N, (int)N, (int)N, o, colsum_accumulate ? 1 : 0,
+                       cur_stream());
+  }
 }
 
 // ---------------------------------------------------------------------------- fp8
@@ -1134,7 +1156,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("a_mn"), py::arg("b_mn"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("res") = py::none(),
         py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false, py::arg("cfg") = -1,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("colsum_out") = py::none(), py::arg("colsum_accumulate") = false);
   m.def("gemm_f8", &gemm_f8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("fmt_a"), py::arg("fmt_b"),
         py::arg("inv_scale_a"), py::arg("inv_scale_b"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("res") = py::none(), py::arg("alpha") = 1.0, py::arg("mode") = 0, py::arg("accumulate") = false,

@@ -26,7 +26,8 @@ struct GemmEpi {
   int64_t ldqt = 0;
   const float* q_scale = nullptr;  // quantisation scale (device)
   float* q_amax = nullptr;         // kAmaxSlots amax slots of the output
-  float* q_colpart = nullptr;      // [M / 64, N] fp32 column partial sums, or nullptr
+  float* q_colpart = nullptr;      // [M / 64, N] fp32 column partial sums, or nullptr (also the bf16
+                                   // pp kernel's dGELU epilogue: fused bias gradient)
   int q_fmt = 0;                   // 0 e4m3, 1 e5m2
 };
 
@@ -182,9 +183,11 @@ __device__ __forceinline__ EpiSide epi_side(const GemmEpi& epi, const OutT* C, i
 // output coordinates and its float offset in the staged LDS image.
 enum { EPI_RES = 1, EPI_DGELU = 2, EPI_ACC = 3 };
 
-template <int KIND, typename OutT, int EIT, int HF, class RC, class STAGE>
+// CS: also accumulate the lane's final values per column into csum[0..3] (the pass's 4 columns
+// of a lane are fixed: column partial sums for a fused bias gradient).
+template <int KIND, typename OutT, int EIT, int HF, bool CS = false, class RC, class STAGE>
 __device__ __forceinline__ void epi_pass_side(OutT* __restrict__ C, int64_t ldc, const EpiSide& s, const float* cs,
-                                              RC rc, STAGE stage) {
+                                              RC rc, STAGE stage, float* __restrict__ csum = nullptr) {
   constexpr int H = KIND == EPI_ACC ? HF : (EIT >= 8 ? EIT / 2 : EIT);
   using X = std::conditional_t<KIND == EPI_ACC, float4, ushort4>;
   X x[H];
@@ -215,6 +218,10 @@ __device__ __forceinline__ void epi_pass_side(OutT* __restrict__ C, int64_t ldc,
       const float xv[4] = {bf16_to_f32(a.x), bf16_to_f32(a.y), bf16_to_f32(a.z), bf16_to_f32(a.w)};
 #pragma unroll
       for (int q = 0; q < 4; ++q) vv[q] = KIND == EPI_DGELU ? vv[q] * gelu_grad(xv[q]) : vv[q] + xv[q];
+      if constexpr (CS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) csum[q] += vv[q];
+      }
       if constexpr (sizeof(OutT) == 4) {
         *reinterpret_cast<float4*>(cp) = make_float4(vv[0], vv[1], vv[2], vv[3]);
       } else {

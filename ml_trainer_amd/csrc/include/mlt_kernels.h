@@ -137,7 +137,7 @@ void set_gemm_split_mode(int mode);  // -1 planner, 0 in-kernel last-arriver, 1 
 void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
                       const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
-                      int accumulate, float* ws, unsigned* cnt, hipStream_t st);
+                      int accumulate, float* ws, unsigned* cnt, hipStream_t st, float* colpart = nullptr);
 // fp8 GEMM (gemm_tile.hip): A [M][K], B [N][K] both k-contiguous fp8 (fmt 0 = e4m3, 1 = e5m2),
 // K % 128 == 0; alpha *= inv_scale_a[0] * inv_scale_b[0] (device scalars, delayed scaling).
 GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits);

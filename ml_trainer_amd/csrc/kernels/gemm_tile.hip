@@ -715,9 +715,22 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       return;
     }
     if (sk == EPI_DGELU) {
-      epi_pass_side<EPI_DGELU, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
+      if (epi.q_colpart) {  // + column sums (bias gradient): lanes with equal lane & 7 share 4 columns
+        float csum[4] = {0.f, 0.f, 0.f, 0.f};
+        epi_pass_side<EPI_DGELU, OutT, 8, 4, true>(C, ldc, side, cs, rc, stg, csum);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int off = 8; off < 64; off <<= 1) csum[q] += __shfl_xor(csum[q], off);
+        if (lane < 8)
+          *reinterpret_cast<float4*>(epi.q_colpart + (int64_t)(q_gm0(qd) >> 6) * N + q_gn0(qd) + lane * 4) =
+              make_float4(csum[0], csum[1], csum[2], csum[3]);
+      } else {
+        epi_pass_side<EPI_DGELU, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
+      }
       return;
     }
+    MLT_DCHECK(epi.q_colpart == nullptr);  // the host guarantees the dGELU side pass for column sums
     if constexpr (sizeof(OutT) == 4) {
       if (sk == EPI_ACC) {
         epi_pass_side<EPI_ACC, OutT, 8, 4>(C, ldc, side, cs, rc, stg);
@@ -1026,9 +1039,10 @@ GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {
 void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
                       const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,
-                      int accumulate, float* ws, unsigned* cnt, hipStream_t st) {
+                      int accumulate, float* ws, unsigned* cnt, hipStream_t st, float* colpart) {
   if (M <= 0 || N <= 0) return;
   GemmEpi e{bias, aux, res, ldaux, ldres, alpha, mode, accumulate};
+  e.q_colpart = colpart;  // dGELU column partials (host: ping-pong plan, interior tiles only)
   if (plan.cfg == 0) {
     launch_gemm_bf16_128(a_mn, b_mn, out_f32, A, B, C, M, N, K, lda, ldb, ldc, e, st);
     return;

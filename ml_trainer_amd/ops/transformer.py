@@ -75,18 +75,30 @@ class Bf16Linear:
     def fwd(x, w, bias=None, gelu_aux=None, res=None):
         return linear_fwd(x, bf16_weight(w), bias, gelu_aux=gelu_aux, res=res)
 
+    fuse_colsum = os.environ.get("MLT_DGELU_COLSUM", "1") != "0"
+
     @staticmethod
-    def dgrad(dy, w, out, aux=None, res=None):
+    def dgrad(dy, w, out, aux=None, res=None, colsum_out=None, colsum_acc=False):
         """out = dy . W  (* gelu'(aux) when aux is given) (+ res). Large token counts take W^T as
         a k-contiguous copy (one transpose per weight per step): the forward-layout tile runs
-        8-11 % faster than the n-contiguous-B one on the BERT dgrad shapes."""
+        8-11 % faster than the n-contiguous-B one on the BERT dgrad shapes. ``colsum_out``: the
+        column sums of the dGELU output (the bias gradient of the layer before the GELU) from the
+        GEMM epilogue (set or accumulated; see dgelu_colsum_ok)."""
         C = require_native()
         mode = 2 if aux is not None else 0
         if dy.shape[0] >= 4096 and os.environ.get("MLT_DGRAD_WT", "1") != "0":
-            C.gemm(dy, bf16_weight_t(w), out, False, False, aux=aux, mode=mode, res=res)
+            C.gemm(dy, bf16_weight_t(w), out, False, False, aux=aux, mode=mode, res=res,
+                   colsum_out=colsum_out, colsum_accumulate=colsum_acc)
         else:
-            C.gemm(dy, bf16_weight(w), out, False, True, aux=aux, mode=mode, res=res)
+            C.gemm(dy, bf16_weight(w), out, False, True, aux=aux, mode=mode, res=res,
+                   colsum_out=colsum_out, colsum_accumulate=colsum_acc)
         return out
+
+    @staticmethod
+    def dgelu_colsum_ok(dy, w) -> bool:
+        """Whether dgrad(dy, w, aux=..., colsum_out=...) can fuse the column sums (ping-pong tiles
+        over the whole output: tokens and W's input width multiples of 256)."""
+        return Bf16Linear.fuse_colsum and dy.shape[0] % 256 == 0 and w.shape[1] % 256 == 0 and dy.shape[1] % 64 == 0
 
 
 BF16 = Bf16Linear()
@@ -231,6 +243,14 @@ def _ffn_bwd(saved, params, dy, G, db2="colsum", impl=BF16):
         d8 = impl.dgrad_gelu_q(dy, w2, pre, w1, db1, gb is not None)
         dw1 = G.wgrad(w1, d8, x, impl)
         dx = impl.dgrad(d8, w1, torch.empty_like(x), res=dy)
+        return dx, dw1, (None if gb is not None else db1), dw2, db2
+    if impl is BF16 and impl.dgelu_colsum_ok(dy, w2):
+        # FFN1's bias gradient from the dGELU epilogue (no separate pass over dpre)
+        gb = G.sink(b1)
+        db1 = gb if gb is not None else torch.empty(w1.shape[0], dtype=torch.float32, device=dy.device)
+        dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre, colsum_out=db1, colsum_acc=gb is not None)
+        dw1 = G.wgrad(w1, dpre, x, impl)
+        dx = impl.dgrad(dpre, w1, torch.empty_like(x), res=dy)
         return dx, dw1, (None if gb is not None else db1), dw2, db2
     dpre = impl.dgrad(dy, w2, torch.empty_like(pre), aux=pre)  # (dy . W2) * gelu'(pre)
     dw1, db1 = G.wgrad_bias(w1, b1, dpre, x, impl)

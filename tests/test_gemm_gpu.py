@@ -264,3 +264,28 @@ def test_persistent_kernel_repeatable_full_chip(dev):
             first = out.clone()
         assert torch.equal(out, first)
     torch.testing.assert_close(first, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("b_mn", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 768)])
+def test_dgelu_colsum_fused(dev, b_mn, M, N, K):
+    """dGELU epilogue with fused column sums (the bias gradient of the layer before the GELU):
+    output and sums vs fp32 torch; set and accumulate modes."""
+    C = require_native()
+    g = torch.Generator().manual_seed(M + N + K + b_mn)
+    A = _mk((M, K), dev, g)
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    aux = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16).to(dev)
+    x = aux.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(torch.ones_like(x))
+    ref = _ref(A, B, 0, b_mn) * x.grad
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    cs = torch.full((N,), 3.0, device=dev)
+    C.gemm(A, B, out, False, bool(b_mn), aux=aux, mode=2, colsum_out=cs)
+    torch.testing.assert_close(out.float(), ref, rtol=3e-2, atol=5e-2)
+    scale = ref.abs().sum(0).max().item()
+    torch.testing.assert_close(cs, ref.sum(0), rtol=1e-3, atol=1e-4 * scale)
+    C.gemm(A, B, out, False, bool(b_mn), aux=aux, mode=2, colsum_out=cs, colsum_accumulate=True)
+    torch.testing.assert_close(cs, 2 * ref.sum(0), rtol=1e-3, atol=2e-4 * scale)
+    with pytest.raises(RuntimeError):  # edge tiles cannot fuse the sums
+        C.gemm(A[:M - 8], B, out[:M - 8], False, bool(b_mn), aux=aux[:M - 8], mode=2, colsum_out=cs)
