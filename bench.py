@@ -440,7 +440,7 @@ def main():
         # update (latency-bound, serial by construction): its cost is the standalone per-call time
         # of the transport the engine chose, measured at set-up on every rank (max over ranks, the
         # same vote that picked the transport)
-        key = {"xgmi-oneshot": "xgmi", "rccl": "rccl"}.get(engine.dp_transport)
+        key = {"xgmi-oneshot": "xgmi", "xgmi-twoshot": "xgmi2", "rccl": "rccl"}.get(engine.dp_transport)
         comm = {"buckets": 1, "bucket_mb": [round(flat.numel * 4 / 2 ** 20, 3)], "comm_dtype": "float32",
                 "in_graph": engine.in_graph_collective, "overlap_pct": 0.0,
                 "allreduce_ms": round(tt[key], 4) if (tt and key in tt) else None}

@@ -845,6 +845,8 @@ class PyXgmi {
   unsigned error() const { return x_.error(); }
   void set_timeout_ms(long long ms) { x_.set_timeout_ms(ms); }
   long long timeout_ms() const { return x_.timeout_ms(); }
+  void set_algo(int a) { x_.set_algo(a); }
+  int algo() const { return x_.algo(); }
   XgmiAllReduce& raw() { return x_; }
 
  private:
@@ -1213,7 +1215,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &PyXgmi::open)
       .def("all_reduce", &PyXgmi::all_reduce, py::arg("tensor"), py::arg("average") = true)
       .def("error", &PyXgmi::error)
-      .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms);
+      .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms)
+      .def_property("algo", &PyXgmi::algo, &PyXgmi::set_algo);
   py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)

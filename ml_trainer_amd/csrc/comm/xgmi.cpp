@@ -1,4 +1,4 @@
-// Host side of the one-shot xGMI all-reduce (kernels/allreduce.hip).
+// Host side of the one-shot / two-shot xGMI all-reduce (kernels/allreduce.hip).
 #include <cstring>
 #include <stdexcept>
 
@@ -11,18 +11,30 @@ static void hcheck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-static size_t region_bytes(int64_t cap, int world, int blocks, size_t* flags_off) {
-  size_t off = ((size_t)2 * cap * sizeof(float) + 255) & ~(size_t)255;
-  *flags_off = off;
-  return off + (size_t)2 * blocks * world * sizeof(uint64_t);
+// region: data [2][cap] | flags [2][G][W] | t1 [2][W][slot] | t2 [2][W][slot] | f1 [2][G][W] | f2 [2][G][W]
+// (the t* / f* parts belong to the two-shot algorithm), every part 256-byte aligned
+struct RegionLayout {
+  size_t flags, t1, t2, f1, f2, bytes;
+};
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
+  RegionLayout L;
+  const size_t fl = (size_t)2 * blocks * world * sizeof(uint64_t), tb = (size_t)2 * world * slot * sizeof(float);
+  L.flags = align256((size_t)2 * cap * sizeof(float));
+  L.t1 = align256(L.flags + fl);
+  L.t2 = align256(L.t1 + tb);
+  L.f1 = align256(L.t2 + tb);
+  L.f2 = align256(L.f1 + fl);
+  L.bytes = L.f2 + fl;
+  return L;
 }
 
 XgmiAllReduce::XgmiAllReduce(int64_t cap_floats, int world, int rank, int device, int blocks)
     : cap_((cap_floats + 3) & ~(int64_t)3), world_(world), rank_(rank), device_(device), blocks_(blocks) {
   if (world < 1 || world > kXgmiMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad world/rank");
   if (blocks < 1 || blocks > 1024) throw std::runtime_error("xgmi: bad block count");
-  size_t foff = 0;
-  bytes_ = region_bytes(cap_, world, blocks, &foff);
+  slot_ = ((cap_ + world - 1) / world + 3) & ~(int64_t)3;
+  bytes_ = region_layout(cap_, world, blocks, slot_).bytes;
   hcheck(hipSetDevice(device), "hipSetDevice");
   hcheck(hipExtMallocWithFlags(&region_, bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
   hcheck(hipMemset(region_, 0, bytes_), "hipMemset(region)");
@@ -58,8 +70,7 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
   if ((int)handles.size() != world_) throw std::runtime_error("xgmi: need one handle per rank");
   hcheck(hipSetDevice(device_), "hipSetDevice");
   XgmiPeers* P = static_cast<XgmiPeers*>(peers_host_);
-  size_t foff = 0;
-  region_bytes(cap_, world_, blocks_, &foff);
+  const RegionLayout L = region_layout(cap_, world_, blocks_, slot_);
   for (int q = 0; q < world_; ++q) {
     void* base = nullptr;
     if (q == rank_) {
@@ -71,8 +82,13 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
       hcheck(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
       peer_base_[q] = base;
     }
+    char* c = static_cast<char*>(base);
     P->data[q] = static_cast<float*>(base);
-    P->flags[q] = reinterpret_cast<uint64_t*>(static_cast<char*>(base) + foff);
+    P->flags[q] = reinterpret_cast<uint64_t*>(c + L.flags);
+    P->t1[q] = reinterpret_cast<float*>(c + L.t1);
+    P->t2[q] = reinterpret_cast<float*>(c + L.t2);
+    P->f1[q] = reinterpret_cast<uint64_t*>(c + L.f1);
+    P->f2[q] = reinterpret_cast<uint64_t*>(c + L.f2);
   }
   opened_ = true;
 }
@@ -80,8 +96,18 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
 void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st, const XgmiPostOpt* post) {
   if (!opened_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (n > cap_) throw std::runtime_error("xgmi: vector larger than the region capacity");
-  launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale, err_,
-                        timeout_ms_ * 100000LL, post, st);  // 100 MHz constant clock: 1e5 ticks per ms
+  const long long ticks = timeout_ms_ * 100000LL;  // 100 MHz constant clock: 1e5 ticks per ms
+  if (algo_ == 1)
+    launch_xgmi_allreduce_2shot(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, slot_, blocks_, seqs_,
+                                scale, err_, ticks, post, st);
+  else
+    launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale,
+                          err_, ticks, post, st);
+}
+
+void XgmiAllReduce::set_algo(int a) {
+  if (a != 0 && a != 1) throw std::runtime_error("xgmi: algo 0 = one-shot, 1 = two-shot");
+  algo_ = a;
 }
 
 unsigned XgmiAllReduce::error() const {

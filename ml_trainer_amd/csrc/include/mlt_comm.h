@@ -66,9 +66,15 @@ class XgmiAllReduce {
   long long timeout_ms() const { return timeout_ms_; }
   int world() const { return world_; }
   int64_t capacity() const { return cap_; }
+  // 0 one-shot (pull everything), 1 two-shot (push reduce-scatter + push all-gather); every rank
+  // must use the same algorithm for a given call. Graphs keep the algorithm they were captured with.
+  void set_algo(int a);
+  int algo() const { return algo_; }
 
  private:
   int64_t cap_;
+  int64_t slot_ = 0;  // two-shot: floats per rank slot of t1 / t2
+  int algo_ = 0;
   int world_, rank_, device_, blocks_;
   void* region_ = nullptr;
   size_t bytes_ = 0;

@@ -173,6 +173,12 @@ constexpr int kXgmiMaxRanks = 8;
 struct XgmiPeers {
   float* data[kXgmiMaxRanks];
   uint64_t* flags[kXgmiMaxRanks];
+  // two-shot (reduce-scatter + all-gather by remote pushes): per-rank [2][W][slot] staging of the
+  // scattered slices (t1) and of the reduced slices (t2), each with its own [2][G][W] flags
+  float* t1[kXgmiMaxRanks];
+  float* t2[kXgmiMaxRanks];
+  uint64_t* f1[kXgmiMaxRanks];
+  uint64_t* f2[kXgmiMaxRanks];
 };
 // optional fused flat-optimizer update of the reduced slice (same semantics as
 // launch_flat_optim with lr / step from device memory)
@@ -186,6 +192,10 @@ struct XgmiPostOpt {
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
                            uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
                            const XgmiPostOpt* post, hipStream_t st);
+// two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
+void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,
+                                 int blocks, uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
+                                 const XgmiPostOpt* post, hipStream_t st);
 
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,

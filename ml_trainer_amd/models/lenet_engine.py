@@ -85,8 +85,8 @@ class LeNetStepEngine:
     # ------------------------------------------------------------------ setup
     def _setup_transport(self, process_group) -> None:
         """Gradient all-reduce transport for the data-parallel step, chosen by measurement:
-        the one-shot xGMI kernel vs RCCL (both enqueued from C++, so both live inside the step's
-        hipGraph); torch.distributed when neither is available."""
+        the one-shot and two-shot xGMI kernels vs RCCL (all enqueued from C++, so all live inside
+        the step's hipGraph); torch.distributed when none is available."""
         import warnings
         import torch.distributed as dist
         from ml_trainer_amd.parallel.comm import create_native_comm, create_xgmi_allreduce
@@ -96,16 +96,22 @@ class LeNetStepEngine:
             warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
             self.comm = None
         self.xgmi = create_xgmi_allreduce(process_group, self.flat.numel, self.device)
-        if self.comm is None:
-            if self.xgmi is not None:  # no RCCL (gloo rehearsal): the one-shot kernel alone
-                self.eng.set_xgmi(self.xgmi)
-                self.dp_transport = "xgmi-oneshot"
+        if self.comm is None and self.xgmi is None:
             return
-        use_xgmi = False
         t = self.flat.grad.clone()
-        cands = [("rccl", lambda: self.comm.all_reduce(t, "avg"))]
-        if self.xgmi is not None:
-            cands.insert(0, ("xgmi", lambda: self.xgmi.all_reduce(t, True)))
+        cands = []
+        x = self.xgmi
+        if x is not None:
+            def one():
+                x.algo = 0
+                x.all_reduce(t, True)
+
+            def two():
+                x.algo = 1
+                x.all_reduce(t, True)
+            cands += [("xgmi", one), ("xgmi2", two)]
+        if self.comm is not None:
+            cands.append(("rccl", lambda: self.comm.all_reduce(t, "avg")))
         times = {}
         for name, fn in cands:
             for _ in range(5):
@@ -118,28 +124,35 @@ class LeNetStepEngine:
             e.synchronize()
             times[name] = s.elapsed_time(e) / 50
         # every rank votes with its own timings and health: the slowest rank decides (MAX), and
-        # an xGMI error word raised on ANY rank during the trial rules the one-shot kernel out
-        bad = 1.0 if (self.xgmi is not None and self.xgmi.error()) else 0.0
-        vote = torch.tensor([bad, times.get("xgmi", float("inf")), times["rccl"]], device=self.device)
+        # an xGMI error word raised on ANY rank during the trial rules the xGMI kernels out
+        names = ("xgmi", "xgmi2", "rccl")
+        bad = 1.0 if (x is not None and x.error()) else 0.0
+        coll_dev = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+        vote = torch.tensor([bad] + [times.get(k, float("inf")) for k in names], device=coll_dev)
         dist.all_reduce(vote, op=dist.ReduceOp.MAX, group=process_group)
-        bad, tx, tr = (float(v) for v in vote.tolist())
-        use_xgmi = self.xgmi is not None and bad == 0.0 and tx < tr
-        self.transport_times_ms = {"rccl": tr, **({"xgmi": tx} if self.xgmi is not None else {})}
-        if self.xgmi is not None and bad != 0.0:
-            warnings.warn("xGMI one-shot all-reduce failed its timing trial on some rank; using RCCL")
-        if use_xgmi:
-            self.eng.set_xgmi(self.xgmi)
-            self.dp_transport = "xgmi-oneshot"
-        else:
+        v = [float(u) for u in vote.tolist()]
+        bad, agreed = v[0], dict(zip(names, v[1:]))
+        if x is not None and bad != 0.0:
+            warnings.warn("xGMI all-reduce failed its timing trial on some rank; using RCCL")
+            agreed["xgmi"] = agreed["xgmi2"] = float("inf")
+        self.transport_times_ms = {k: agreed[k] for k in names if k in times}
+        best = min(names, key=lambda k: agreed[k])
+        if agreed[best] == float("inf"):  # only a failed xGMI and no RCCL: leave torch.distributed
+            return
+        if best == "rccl":
             self.eng.set_comm(self.comm)
             self.dp_transport = "rccl"
+        else:
+            x.algo = 0 if best == "xgmi" else 1
+            self.eng.set_xgmi(x)
+            self.dp_transport = "xgmi-oneshot" if best == "xgmi" else "xgmi-twoshot"
 
     def _poll_transport(self) -> None:
         """Non-blocking health check of the in-graph collective, run after every graph replay:
         the xGMI kernel's sticky error word lives in mapped host memory and RCCL reports through
         ncclCommGetAsyncError, so neither read synchronises the device. A failure aborts the
         communicator (unblocking any stuck collective) and raises TransportError."""
-        if self.dp_transport == "xgmi-oneshot" and self.xgmi is not None:
+        if self.dp_transport.startswith("xgmi") and self.xgmi is not None:
             if self.xgmi.error():
                 raise TransportError("xGMI all-reduce: a peer did not arrive within "
                                      f"{self.xgmi.timeout_ms} ms; the step was not applied")
@@ -229,11 +242,11 @@ class LeNetStepEngine:
         else:
             self.eng.set_comm(None)
             self.eng.set_xgmi(xgmi)
-            self.dp_transport = "xgmi-oneshot"
+            self.dp_transport = "xgmi-twoshot" if getattr(xgmi, "algo", 0) == 1 else "xgmi-oneshot"
 
     @property
     def in_graph_collective(self) -> bool:
-        return self.dp_transport in ("rccl", "xgmi-oneshot")
+        return self.dp_transport in ("rccl", "xgmi-oneshot", "xgmi-twoshot")
 
     def _train_mode(self) -> int:
         C = self.C

@@ -50,7 +50,8 @@ def xgmi_enabled() -> bool:
 
 def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optional[torch.device] = None,
                           allow_gloo: Optional[bool] = None):
-    """One-shot xGMI all-reduce (csrc/kernels/allreduce.hip) for vectors of <= ``capacity`` fp32.
+    """One-shot / two-shot xGMI all-reduce (csrc/kernels/allreduce.hip) for vectors of <=
+    ``capacity`` fp32 (``.algo`` 0 / 1; the LeNet engine picks by a timed vote).
 
     Collective. IPC handles of every rank's uncached region travel through the process group;
     a self-test (sum of rank-dependent vectors, bit-exact, bounded wait) must pass on EVERY rank
@@ -90,16 +91,21 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
     if int(flag.item()) == 0:
         return None
-    # self-test: two launches (both buffer parities), exact small-integer sums
+    # self-test of both algorithms (one-shot, two-shot): two launches each (both buffer
+    # parities), exact small-integer sums, an odd length (tail handling)
     n = max(4, min(int(capacity), 1 << 16))
+    n -= 1 - n % 2
     good = True
-    for it in range(2):
-        t = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97).add_(rank + 1 + it)
-        x.all_reduce(t, average=False)
-        ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
-            world * (world + 1) // 2 + it * world)
-        torch.cuda.synchronize(dev)
-        good = good and bool(torch.equal(t, ref))
+    for algo in (0, 1):
+        x.algo = algo
+        for it in range(2):
+            t = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97).add_(rank + 1 + it)
+            x.all_reduce(t, average=False)
+            ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
+                world * (world + 1) // 2 + it * world)
+            torch.cuda.synchronize(dev)
+            good = good and bool(torch.equal(t, ref))
+    x.algo = 0
     good = good and x.error() == 0
     flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=coll_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)

@@ -313,7 +313,7 @@ class Trainer:
             eng = self._engine
             if self._watchdog is not None and eng.comm is not None and eng.dp_transport == "rccl":
                 self._watchdog.add_probe(eng.comm.async_error, eng.comm.abort)
-            if self._watchdog is not None and eng.xgmi is not None and eng.dp_transport == "xgmi-oneshot":
+            if self._watchdog is not None and eng.xgmi is not None and eng.dp_transport.startswith("xgmi"):
                 x = eng.xgmi
                 self._watchdog.add_probe(lambda: "xGMI all-reduce peer timeout" if x.error() else "")
         return self._engine

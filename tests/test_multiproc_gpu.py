@@ -70,9 +70,9 @@ def _bert_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def _run(fn, world=2):
+def _run(fn, world=2, *extra):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(fn, args=(world, free_port(), d), nprocs=world, join=True)
+        mp.spawn(fn, args=(world, free_port(), d, *extra), nprocs=world, join=True)
         return [torch.load(os.path.join(d, f), weights_only=True) for f in sorted(os.listdir(d))]
 
 
@@ -89,14 +89,15 @@ def test_bert_ddp_direct_grads_two_ranks():
     assert r[0]["g"].abs().sum() > 0
 
 
-def _xgmi_worker(rank, world, port, out_dir):
+def _xgmi_worker(rank, world, port, out_dir, algo=0):
     dist_env(rank, world, port)
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
-    x = create_xgmi_allreduce(None, 70000, dev, allow_gloo=True)  # includes the 2-launch self-test
+    x = create_xgmi_allreduce(None, 70000, dev, allow_gloo=True)  # includes the self-test of both algorithms
     assert x is not None
+    x.algo = algo
     res = []
     g = torch.Generator().manual_seed(100 + rank)
     for it in range(5):  # odd/even parities, sizes with a float4 tail
@@ -119,8 +120,9 @@ def _xgmi_worker(rank, world, port, out_dir):
     opt = build_optimizer("sgd", m.parameters(), lr=1e-2, momentum=0.9, flat=flat)
     eng = LeNetStepEngine(m, flat, max_batch=16, optimizer=opt, world_size=world)
     xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
-    eng.eng.set_xgmi(xe)
-    eng.dp_transport = "xgmi-oneshot"
+    xe.algo = algo
+    eng.use_transport(xgmi=xe)
+    assert eng.dp_transport == ("xgmi-twoshot" if algo else "xgmi-oneshot")
     gd = torch.Generator().manual_seed(3)
     N = 256
     data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
@@ -134,10 +136,12 @@ def _xgmi_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_oneshot_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("algo", [0, 1])
+def test_xgmi_oneshot_allreduce_two_ranks_one_gpu(algo):
     """IPC-shared uncached regions + flag barrier + rank-ordered sums; two processes on the one
-    GPU of the box stand in for two xGMI peers (same code path, the peer is just local)."""
-    r = _run(_xgmi_worker)
+    GPU of the box stand in for two xGMI peers (same code path, the peer is just local).
+    algo 0: one-shot (pull), 1: two-shot (push reduce-scatter + push all-gather)."""
+    r = _run(_xgmi_worker, 2, algo)
     for d in r:
         assert d["ok"].all(), d["ok"]
         assert d["err"].tolist() == [0, 0]
