@@ -115,6 +115,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// LDS hand-off between the lanes of ONE wave (a per-wave LDS region): a compiler fence around a
+// wave barrier orders the wave's earlier LDS accesses before its later ones -- a wave's LDS
+// instructions execute in order, so no s_waitcnt and no workgroup barrier is needed, and the
+// other waves of the block keep running (GEMM epilogues stage through per-wave images).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 // Round-to-nearest-even f32 -> bf16 via the hardware convert (keeps NaN a NaN).

@@ -219,8 +219,10 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
   }
   constexpr int EIT = EPR * WTN / 4 / 64;  // float4 groups per lane per pass
   const EpiSide side = epi_side<OutT>(epi, C, ldc, N, ext);
+  // the image is per wave and the main loop ended with a workgroup barrier (no DMA in flight):
+  // wave-level hand-offs only, so the block's waves run their epilogues independently
   auto stage_pass = [&](int h) __attribute__((always_inline)) {
-    __syncthreads();  // LDS free (main loop / previous pass)
+    wave_lds_sync();  // this wave's reads of the previous pass are done
 #pragma unroll
     for (int ii = 0; ii < RI; ++ii)
 #pragma unroll
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_tile_kernel(const uint8_t* __res
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           cs[(16 * ii + 4 * g + r) * EPS + 16 * j + cl] = acc[RI * h + ii][j][r] * alpha + bv[j];
-    __syncthreads();
+    wave_lds_sync();
   };
   // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
   const int sk = epi_side_kind<OutT>(side, epi, m0 + BM <= M && n0 + BN <= N);
@@ -419,7 +421,7 @@ __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc
     }
     *reinterpret_cast<uint4*>(C + gm * ldc + gn) = make_uint4(o[0], o[1], o[2], o[3]);
   }
-  __syncthreads();
+  wave_lds_sync();  // the image is this wave's own
   const int col = lane & 31, r0 = (lane >> 5) * 32;
   const float* p = cs + r0 * EPS + col;
   uint32_t w[8];
@@ -677,7 +679,8 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
       const int gn = q_gn0(qd) + 16 * j + cl;
       bv[j] = (epi.bias && gn < N && !ext) ? epi.bias[gn] : 0.f;
     }
-    __syncthreads();
+    // per-wave image after the post-loop workgroup barrier: wave-level hand-offs only
+    wave_lds_sync();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -685,7 +688,7 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           cs[(16 * i + 4 * g + r) * EPS + 16 * j + cl] = acc[qd * 8 + i * 2 + j][r] * alpha + bv[j];
-    __syncthreads();
+    wave_lds_sync();
   };
   // side operands (residual / dGELU input / accumulate target) prefetched across the LDS round trip
   const int sk = epi_side_kind<OutT>(side, epi, m0 + 256 <= M && n0 + 256 <= N);
