@@ -14,11 +14,11 @@ __device__ __forceinline__ float fp8_max() {
 // 4 floats -> 4 saturated fp8 bytes (v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32), byte i = value i
 template <int FMT>
 __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
-  const float m = fp8_max<FMT>();
-  a = fminf(fmaxf(a, -m), m);
-  b = fminf(fmaxf(b, -m), m);
-  c = fminf(fmaxf(c, -m), m);
-  d = fminf(fmaxf(d, -m), m);
+  const float m = fp8_max<FMT>();  // saturate: one v_med3_f32 per value
+  a = __builtin_amdgcn_fmed3f(a, -m, m);
+  b = __builtin_amdgcn_fmed3f(b, -m, m);
+  c = __builtin_amdgcn_fmed3f(c, -m, m);
+  d = __builtin_amdgcn_fmed3f(d, -m, m);
   int r;
   if constexpr (FMT == 0) {
     r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);

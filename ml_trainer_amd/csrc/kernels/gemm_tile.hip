@@ -411,36 +411,45 @@ __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc
       }
     }
 #pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      amx = fmaxf(amx, fabsf(v[q]));
+      v[q] *= s;  // the image keeps the SCALED values: the column pass only converts
+    }
+#pragma unroll
     for (int q = 0; q < 4; ++q)
       reinterpret_cast<float4*>(p)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     uint32_t o[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v[4 * q]), fabsf(v[4 * q + 1])), fmaxf(fabsf(v[4 * q + 2]), fabsf(v[4 * q + 3]))));
-      o[q] = pack4_fp8<FMT>(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
-    }
+    for (int q = 0; q < 4; ++q) o[q] = pack4_fp8<FMT>(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     *reinterpret_cast<uint4*>(C + gm * ldc + gn) = make_uint4(o[0], o[1], o[2], o[3]);
   }
   wave_lds_sync();  // the image is this wave's own
   const int col = lane & 31, r0 = (lane >> 5) * 32;
   const float* p = cs + r0 * EPS + col;
-  uint32_t w[8];
-  float sum = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float x[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = p[(4 * k + j) * EPS];
-    sum += (x[0] + x[1]) + (x[2] + x[3]);
-    w[k] = pack4_fp8<FMT>(x[0] * s, x[1] * s, x[2] * s, x[3] * s);
-  }
   uint4* tp = reinterpret_cast<uint4*>(epi.qt + (int64_t)(gn0 + col) * epi.ldqt + gm0 + r0);
-  tp[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  tp[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  if (epi.q_colpart) {
-    sum += __shfl_xor(sum, 32);
-    if (lane < 32) epi.q_colpart[(int64_t)(gm0 >> 6) * N + gn0 + col] = sum;
-  }
+  auto column = [&](auto csc) __attribute__((always_inline)) {
+    constexpr bool CS = decltype(csc)::value;
+    uint32_t w[8];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = p[(4 * k + j) * EPS];
+      if constexpr (CS) sum += (x[0] + x[1]) + (x[2] + x[3]);
+      w[k] = pack4_fp8<FMT>(x[0], x[1], x[2], x[3]);
+    }
+    tp[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    tp[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    if constexpr (CS) {  // column sums of the unscaled output: one multiply by 1/scale
+      sum += __shfl_xor(sum, 32);
+      if (lane < 32) epi.q_colpart[(int64_t)(gm0 >> 6) * N + gn0 + col] = sum * __builtin_amdgcn_rcpf(s);
+    }
+  };
+  if (epi.q_colpart)
+    column(std::true_type{});
+  else
+    column(std::false_type{});
 }
 
 template <bool AM, bool BNL, typename OutT, int F8A = -1, int F8B = -1>
