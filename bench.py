@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch (weak) / global batch (reference); default 32 (LeNet), "
-                         "128 (bert-base / bert-large), 512 (large fp8: 245 GiB of HBM)")
+                         "512 (bert-base: 77 GiB), 256 (bert-large), 512 (large fp8: 245 GiB of HBM)")
     ap.add_argument("--scaling", choices=["weak", "reference"], default="weak")
     ap.add_argument("--model", default="default",
                     choices=["default", "tiny", "bert-base", "bert-tiny", "bert-large", "large"])
@@ -310,9 +310,10 @@ def main():
     if args.batch is None:
         # LeNet: the reference batch (src/trainer.py / main.py: 32). Transformer configs: micro-batches
         # sized for 288 GB of HBM per GPU (per-GPU throughput keeps rising with the micro-batch:
-        # BERT-base 1748 / 2160 / 2232 samples/s at 32 / 128 / 256; the fp8 `large` config, BASELINE
-        # config 5 "sized to fill HBM": 924 / 947 samples/s at 256 / 512 using 126 / 245 GiB)
-        args.batch = {"bert-base": 128, "bert-large": 128, "large": 512, "bert-tiny": 32}.get(args.model, 32)
+        # BERT-base 2,552 / 2,665 / 2,710 samples/s at 128 / 256 / 512 using 21 / 40 / 77 GiB; the fp8
+        # `large` config, BASELINE config 5 "sized to fill HBM": 1,013 / 1,030 samples/s at 256 / 512
+        # using 126 / 245 GiB; profiles/batch_sweep_r2.jsonl)
+        args.batch = {"bert-base": 512, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
 
     if args.device == "cpu" or not torch.cuda.is_available():
         if world > 1:
