@@ -744,7 +744,8 @@ void attn_fwd(Tensor qkv, Tensor out, Tensor lse, c10::optional<Tensor> lens, in
 }
 
 void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10::optional<Tensor> lens, Tensor dqkv,
-              int64_t B, int64_t S, int64_t H, double scale) {
+              int64_t B, int64_t S, int64_t H, double scale, c10::optional<Tensor> colsum_out,
+              bool colsum_accumulate) {
   const int64_t D = H * 64;
   check_bf16_2d(qkv, "qkv", B * S, 3 * D);
   check_bf16_2d(out, "out", B * S, D);
@@ -753,8 +754,33 @@ void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10
   check_dev(lse, "lse", at::kFloat, B * H * S, 4);
   check_dev(delta, "delta", at::kFloat, B * H * S, 4);
   TORCH_CHECK(B > 0 && S > 0 && H > 0 && B <= 65535 && H <= 65535, "attention dims");
-  launch_attn_bwd(bf16_ptr(qkv), bf16_ptr(out), bf16_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
-                  lens_ptr(lens, B), (uint16_t*)dqkv.data_ptr(), (int)B, (int)S, (int)H, (float)scale, cur_stream());
+  Tensor pq, pkv;
+  if (colsum_out.has_value()) {  // QKV bias gradient = column sums of dQKV, from the backward kernels
+    check_dev(*colsum_out, "colsum_out", at::kFloat, 3 * D, 16);
+    const int64_t rows = B * ((S + 63) / 64);
+    pq = at::empty({rows * D}, qkv.options().dtype(at::kFloat));
+    pkv = at::empty({rows * 2 * D}, qkv.options().dtype(at::kFloat));
+  }
+  int rq = 0, rkv = 0;
+  const bool fused = launch_attn_bwd(bf16_ptr(qkv), bf16_ptr(out), bf16_ptr(dout), lse.data_ptr<float>(),
+                                     delta.data_ptr<float>(), lens_ptr(lens, B), (uint16_t*)dqkv.data_ptr(), (int)B,
+                                     (int)S, (int)H, (float)scale, cur_stream(),
+                                     pq.defined() ? pq.data_ptr<float>() : nullptr,
+                                     pkv.defined() ? pkv.data_ptr<float>() : nullptr, &rq, &rkv);
+  if (!colsum_out.has_value()) return;
+  float* cs = colsum_out->data_ptr<float>();
+  const int acc = colsum_accumulate ? 1 : 0;
+  if (fused) {
+    SegOut oq{{cs, nullptr, nullptr}};
+    launch_reduce_rows(pq.data_ptr<float>(), rq, D, (int)D, (int)D, oq, acc, cur_stream());
+    SegOut okv{{cs + D, cs + 2 * D, nullptr}};
+    launch_reduce_rows(pkv.data_ptr<float>(), rkv, 2 * D, (int)(2 * D), (int)D, okv, acc ? 3 : 0, cur_stream());
+  } else {
+    Tensor ws = at::empty({std::max<int64_t>(colsum_ws_floats((int)(B * S), (int)(3 * D)), 4)},
+                          qkv.options().dtype(at::kFloat));
+    launch_colsum_bf16((const uint16_t*)dqkv.data_ptr(), (int)(B * S), (int)(3 * D), dqkv.stride(0), cs, acc,
+                       ws.data_ptr<float>(), cur_stream());
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1194,7 +1220,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("delta"),
+        py::arg("lens"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"),
+        py::arg("colsum_out") = py::none(), py::arg("colsum_accumulate") = false);
   py::class_<PyComm>(m, "Communicator")
       .def(py::init<py::bytes, int, int, int>(), py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
            py::arg("device"))

@@ -226,7 +226,12 @@ void launch_embed_bwd(const int64_t* sid, const int64_t* perm, const int64_t* tt
                       hipStream_t st);
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* lens, int B, int S, int H,
                      float scale, hipStream_t st);
-void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
-                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st);
+// colpart_q [B * ceil(S/64)][D] and colpart_kv [B * ceil(S/64)][2D] (or nullptr): bias-gradient
+// column partials of dQ and dK|dV; returns whether they were written (ring kernels) and the
+// number of partial rows in rows_q / rows_kv
+bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st,
+                     float* colpart_q = nullptr, float* colpart_kv = nullptr, int* rows_q = nullptr,
+                     int* rows_kv = nullptr);
 
 }  // namespace mlt

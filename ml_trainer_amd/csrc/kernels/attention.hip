@@ -701,6 +701,31 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+
+// Column sums over a block's rows of per-lane output fragments v[d][r] (head dims d*16 + 4g + r,
+// one row per lane i of each 16-lane group): xor-shuffles over the 16 rows of a group, then the 4
+// waves through LDS (`red`: 256 floats, free). Threads 0..63 write dims 0..63 to out[0..63].
+// The bias gradient of the QKV projection falls out of the attention backward this way, with no
+// separate pass over dQKV.
+__device__ __forceinline__ void block_colsum64(float (&v)[4][4], float* red, float* __restrict__ out) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) v[d][r] += __shfl_xor(v[d][r], off);
+  if (i == 0) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid * 64 + d * 16 + 4 * g + r] = v[d][r];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64)
+    out[threadIdx.x] = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
+}
+
 template <int NK, int kRing>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                  const uint16_t* __restrict__ dout,
@@ -708,7 +733,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
                                                                  const float* __restrict__ delta,
                                                                  const int* __restrict__ lens,
                                                                  uint16_t* __restrict__ dqkv, int S, int H,
-                                                                 float scale) {
+                                                                 float scale, float* __restrict__ colpart) {
   constexpr int STAGE = 2 * kTile + 2 * AB * 4;  // Q tile, dO tile, lse[64], delta[64]
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
   int kbk, h, b;
@@ -719,6 +744,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
   const int64_t base = (int64_t)b * S;
   const int len = lens ? lens[b] : S;
   const int k0b = kbk * (64 * NK);
+  // column partials [B * key blocks][2 D] (dK | dV) of the bias gradient, or nullptr
+  float* cp = colpart ? colpart + ((int64_t)b * ((S + 64 * NK - 1) / (64 * NK)) + kbk) * 2 * D + h * AH : nullptr;
   if (k0b >= len) {  // fully masked key block: zero gradients
     for (int e = threadIdx.x; e < 64 * NK * AH; e += 256) {
       const int kk = k0b + e / AH, d = e % AH;
@@ -726,6 +753,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
         dqkv[(base + kk) * ld + D + h * AH + d] = 0;
         dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
       }
+    }
+    if (cp && threadIdx.x < 64) {
+      cp[threadIdx.x] = 0.f;
+      cp[D + threadIdx.x] = 0.f;
     }
     return;
   }
@@ -873,6 +904,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
       }
     }
   }
+  if (cp) {  // bias-gradient partials of dK and dV over this block's keys
+    float vk[4][4], vv[4][4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        vk[d][r] = 0.f;
+        vv[d][r] = 0.f;
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          vk[d][r] += key[n] < S ? dk[n][d][r] * scale : 0.f;
+          vv[d][r] += key[n] < S ? dv[n][d][r] : 0.f;
+        }
+      }
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is past its last ring-stage read
+    block_colsum64(vk, red, cp);
+    block_colsum64(vv, red + 256, cp + D);
+  }
 }
 
 template <int NQ, int kRing>
@@ -881,7 +931,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                const int* __restrict__ lens,
-                                                               uint16_t* __restrict__ dqkv, int S, int H, float scale) {
+                                                               uint16_t* __restrict__ dqkv, int S, int H, float scale,
+                                                               float* __restrict__ colpart) {
   constexpr int STAGE = 2 * kTile;  // K tile, V tile
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
   int qb, h, b;
@@ -987,6 +1038,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
       }
     }
   }
+  if (colpart) {  // bias-gradient partials of dQ over this block's queries: [B * query blocks][D]
+    float vq[4][4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        vq[d][r] = 0.f;
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) vq[d][r] += q[n] < S ? acc[n][d][r] * scale : 0.f;
+      }
+    __syncthreads();  // every wave is past its last ring-stage read
+    block_colsum64(vq, reinterpret_cast<float*>(smem),
+                   colpart + ((int64_t)b * ((S + 64 * NQ - 1) / (64 * NQ)) + qb) * D + h * AH);
+  }
 }
 
 // 32 rows per wave (2 x 16-row groups) once the sequence fills a 128-row block.
@@ -1011,9 +1076,10 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* 
     hipLaunchKernelGGL(attn_fwd_lean_kernel<1>, dim3(g1), dim3(256), 0, st, qkv, out, lse, lens, S, H, scale);
 }
 
-void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
-                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st) {
-  if (B <= 0 || S <= 0) return;
+bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                     const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st,
+                     float* colpart_q, float* colpart_kv, int* rows_q, int* rows_kv) {
+  if (B <= 0 || S <= 0) return false;
   const int64_t pairs = (int64_t)B * S * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
                      (int64_t)B * S, H);
@@ -1027,23 +1093,26 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   {                                                                                                                 \
     if (k2)                                                                                                         \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
-                         dqkv, S, H, scale);                                                                        \
+                         dqkv, S, H, scale, colpart_kv);                                                            \
     else                                                                                                            \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
-                         dqkv, S, H, scale);                                                                        \
+                         dqkv, S, H, scale, colpart_kv);                                                            \
     if (q2)                                                                                                         \
       hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
-                         S, H, scale);                                                                              \
+                         S, H, scale, colpart_q);                                                                   \
     else                                                                                                            \
       hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
-                         S, H, scale);                                                                              \
+                         S, H, scale, colpart_q);                                                                   \
   }
     if (ring == 3)
       MLT_RING_LAUNCH(3)
     else
       MLT_RING_LAUNCH(4)
 #undef MLT_RING_LAUNCH
-    return;
+    // partial rows actually written: B x (row blocks of the chosen group count)
+    if (rows_kv) *rows_kv = B * ((S + (k2 ? 127 : 63)) / (k2 ? 128 : 64));
+    if (rows_q) *rows_q = B * ((S + (q2 ? 127 : 63)) / (q2 ? 128 : 64));
+    return colpart_q != nullptr && colpart_kv != nullptr;
   }
   if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
@@ -1053,6 +1122,7 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
   else
     hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
+  return false;  // register-staged kernels: no column partials (the caller reduces dQKV itself)
 }
 
 }  // namespace mlt

@@ -214,8 +214,17 @@ def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
     dattn = impl.dgrad(dy, wo, torch.empty_like(attn))
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
-    C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
-    dwqkv, dbqkv = G.wgrad_bias(wqkv, bqkv, dqkv, x, impl)
+    if impl is BF16 and bqkv is not None and _ATTN_COLSUM:
+        # the QKV bias gradient (column sums of dQKV) from the backward kernels themselves
+        gb = G.sink(bqkv)
+        dbqkv = gb if gb is not None else torch.empty(qkv.shape[1], dtype=torch.float32, device=dy.device)
+        C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE, colsum_out=dbqkv,
+                   colsum_accumulate=gb is not None)
+        dwqkv = G.wgrad(wqkv, dqkv, x, impl)
+        dbqkv = None if gb is not None else dbqkv
+    else:
+        C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE)
+        dwqkv, dbqkv = G.wgrad_bias(wqkv, bqkv, dqkv, x, impl)
     dx = impl.dgrad(dqkv, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
     return dx, dwqkv, dbqkv, dwo, dbo
 
@@ -303,6 +312,7 @@ def _ln_bwd(saved, beta, dy, G, dxsum_param=None):
 
 
 _ATTN_SCALE = 1.0 / 8.0  # 1/sqrt(head_dim = 64)
+_ATTN_COLSUM = os.environ.get("MLT_ATTN_COLSUM", "1") != "0"  # QKV bias grad from the attention backward
 
 
 class _AttentionBlock(torch.autograd.Function):

@@ -352,6 +352,40 @@ def test_attention_bwd_ring_matches_register_staged(dev, B, S, H, use_lens, monk
         assert torch.equal(res["0", grp], res["3", grp]) and torch.equal(res["0", grp], res["4", grp])
 
 
+@pytest.mark.parametrize("B,S,H,use_lens", [(2, 512, 3, False), (3, 200, 2, True), (2, 512, 2, True)])
+def test_attention_bwd_fused_bias_colsum(dev, B, S, H, use_lens, monkeypatch):
+    """QKV bias gradient (column sums of dQKV) from the ring backward kernels' block partials
+    (incl. fully masked key blocks and tails), and the plain fallback for the register-staged
+    kernels: both match the column sums of the dQKV they wrote; set and accumulate."""
+    C = require_native()
+    g = torch.Generator().manual_seed(S * 3 + H)
+    D = H * 64
+    qkv = _bf((B * S, 3 * D), g, 1.0)
+    lens = None
+    if use_lens:
+        lens = torch.tensor([7, S, 130][:B], dtype=torch.int32).to(dev)  # 7: most key blocks fully masked
+    scale = 0.125
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * H * S, device=dev)
+    C.attn_fwd(qkv, out, lse, lens, B, S, H, scale)
+    dout = _bf((B * S, D), g)
+    for ring in ("0", "4"):
+        monkeypatch.setenv("MLT_ATTN_RING", ring)
+        for grp in ("1", "2"):
+            monkeypatch.setenv("MLT_ATTN_DKDV_GROUPS", grp)
+            monkeypatch.setenv("MLT_ATTN_DQ_GROUPS", grp)
+            dqkv = torch.empty_like(qkv)
+            delta = torch.empty(B * S * H, device=dev)
+            cs = torch.full((3 * D,), 2.0, device=dev)
+            C.attn_bwd(qkv, out, dout, lse, delta, lens, dqkv, B, S, H, scale, colsum_out=cs)
+            ref = dqkv.float().sum(0)
+            tol = 1e-2 * dqkv.float().abs().sum(0).max().item()
+            torch.testing.assert_close(cs, ref, rtol=1e-2, atol=tol)
+            C.attn_bwd(qkv, out, dout, lse, delta, lens, dqkv, B, S, H, scale, colsum_out=cs,
+                       colsum_accumulate=True)
+            torch.testing.assert_close(cs, 2 * ref, rtol=1e-2, atol=2 * tol)
+
+
 @pytest.mark.parametrize("jump", [4.0, 300.0])
 @pytest.mark.parametrize("use_lens", [False, True])
 def test_attention_fwd_defer_max_branches(dev, jump, use_lens):
