@@ -1236,7 +1236,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("all_to_all", &PyComm::all_to_all, py::arg("input"), py::arg("output"))
       .def("async_error", &PyComm::async_error)
       .def("abort", &PyComm::abort);
-  py::class_<PyXgmi>(m, "XgmiAllReduce")
+  py::class_<PyXgmi>(m, "XgmiAllReduce", py::dynamic_attr())
       .def(py::init<int64_t, int, int, int, int>(), py::arg("capacity"), py::arg("world"), py::arg("rank"),
            py::arg("device"), py::arg("blocks") = 64)
       .def("handle", &PyXgmi::handle)

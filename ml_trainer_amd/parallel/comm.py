@@ -91,11 +91,13 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
     if int(flag.item()) == 0:
         return None
-    # self-test of both algorithms (one-shot, two-shot): two launches each (both buffer
-    # parities), exact small-integer sums, an odd length (tail handling)
+    # self-test of both algorithms (one-shot, then two-shot): two launches each (both buffer
+    # parities), exact small-integer sums, an odd length (tail handling). A peer timeout (sticky
+    # error word) disqualifies the object; wrong two-shot sums only disqualify the two-shot
+    # algorithm (x.two_shot_ok), every rank agreeing through the MIN vote.
     n = max(4, min(int(capacity), 1 << 16))
     n -= 1 - n % 2
-    good = True
+    good = [True, True]
     for algo in (0, 1):
         x.algo = algo
         for it in range(2):
@@ -104,9 +106,14 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
             ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
                 world * (world + 1) // 2 + it * world)
             torch.cuda.synchronize(dev)
-            good = good and bool(torch.equal(t, ref))
+            good[algo] = good[algo] and bool(torch.equal(t, ref))
     x.algo = 0
-    good = good and x.error() == 0
-    flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=coll_dev)
+    ok = x.error() == 0
+    flag = torch.tensor([1 if (ok and good[0]) else 0, 1 if (ok and good[1]) else 0], dtype=torch.int32,
+                        device=coll_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
-    return x if int(flag.item()) == 1 else None
+    one, two = (int(v) for v in flag.tolist())
+    if one != 1:
+        return None
+    x.two_shot_ok = two == 1
+    return x

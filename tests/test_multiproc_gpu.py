@@ -96,7 +96,7 @@ def _xgmi_worker(rank, world, port, out_dir, algo=0):
     dev = torch.device("cuda", 0)
     from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
     x = create_xgmi_allreduce(None, 70000, dev, allow_gloo=True)  # includes the self-test of both algorithms
-    assert x is not None
+    assert x is not None and x.two_shot_ok  # both algorithms passed the self-test on every rank
     x.algo = algo
     res = []
     g = torch.Generator().manual_seed(100 + rank)
