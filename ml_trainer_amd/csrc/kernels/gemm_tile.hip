@@ -861,6 +861,11 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
   return t;
 }
 
+// grouped tile raster: runs of kGroupM M-tiles walk the N tiles together (MLT_GEMM_GROUP_M
+// overrides). 4 measured >= 8 everywhere on MI355X (profiles/gemm_group_m_r2.txt: BERT-base b512
+// +1.0 %, fp8 large b512 +1.1 %, BERT-base b128 equal); 16 lost 2-3 % at b128 (ab_gemm_group_m.txt)
+constexpr int kGroupM = 4;
+
 GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
                     bool allow_pp = true, bool allow_persist = true) {
   GemmPlan p{0, 1, 0, 0, 0};
@@ -954,7 +959,7 @@ void launch_tile(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C,
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   static const int group_m = [] {
     const char* v = getenv("MLT_GEMM_GROUP_M");
-    return v ? atoi(v) : 8;
+    return v ? atoi(v) : kGroupM;
   }();
   hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), G::SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws,
                      cnt, p.ksteps, group_m);
@@ -973,7 +978,7 @@ void launch_pp(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, i
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   static const int group_m = [] {
     const char* v = getenv("MLT_GEMM_GROUP_M");
-    return v ? atoi(v) : 8;
+    return v ? atoi(v) : kGroupM;
   }();
   hipLaunchKernelGGL(kern, dim3(tiles, p.splits), dim3(T_NT), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt,
                      p.ksteps, group_m);
@@ -994,7 +999,7 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
         if ((K / (F8A >= 0 ? 128 : T_BK)) % 2 == 0 && p.splits == 1) {
           static const int group_m = [] {
             const char* v = getenv("MLT_GEMM_GROUP_M");
-            return v ? atoi(v) : 8;
+            return v ? atoi(v) : kGroupM;
           }();
           launch_gemm_persist<AM, BNL, OutT, F8A, F8B>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, kCUs, st);
           break;
