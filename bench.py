@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dataset-size", type=int, default=50000)
     ap.add_argument("--optimizer", default="sgd")
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
+                    help="LeNet step: bf16 (BASELINE.json configs 2/3 'default config bf16': bf16 MFMA "
+                         "operands, fp32 accumulation / activations / masters / optimizer state; 2 kernels "
+                         "per step) or fp32 (the reference model's dtype; 4 kernels per step)")
     ap.add_argument("--seed", type=int, default=32)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -359,7 +363,8 @@ def main():
         dist.broadcast(flat.data, src=0)  # DDP-style initial parameter broadcast
     opt = build_optimizer(args.optimizer, model.parameters(), lr=1e-3, momentum=0.9, weight_decay=0.0, flat=flat)
     per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
-    engine = LeNetStepEngine(model, flat, max_batch=per_gpu, optimizer=opt, world_size=world, seed=args.seed)
+    engine = LeNetStepEngine(model, flat, max_batch=per_gpu, optimizer=opt, world_size=world, seed=args.seed,
+                             precision=args.precision)
     if os.environ.get("MLT_BENCH_FORCE_RCCL") == "1" and world == 1:
         # W=1 rehearsal of the data-parallel step: real ncclAllReduce inside the captured graph
         C = engine.C
@@ -456,7 +461,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak" if args.scaling == "weak" else "strong",
         "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2),
-        "dtype": "fp32",
+        "dtype": args.precision,
         "data": "synthetic (CIFAR-10-shaped uint8 in HBM, on-GPU RandomCrop+HFlip+Normalize), random-init weights",
         "config": {"model": f"src/model.py MLModel ({args.model} LeNet-5, 62,006 params)" if args.model == "default"
                    else f"src/model.py MLModel ({args.model})",

@@ -14,7 +14,7 @@ CIFAR-shaped dataset and says so in the log.
 
 Extension flags (not in the reference): ``--model`` (default/tiny/bert-base/
 large), ``--synthetic``, ``--per_device_batch``, ``--no_engine``,
-``--no_parallel``, ``--resume``, ``--amp bf16``, ``--metrics_jsonl``, ``--log_jsonl``, ``--zero_stage``.
+``--no_parallel``, ``--resume``, ``--amp bf16``, ``--precision bf16``, ``--metrics_jsonl``, ``--log_jsonl``, ``--zero_stage``.
 """
 from __future__ import annotations
 
@@ -89,6 +89,7 @@ def main(args):
     }
     options = {"per_device_batch": args.per_device_batch, "resume": args.resume,
                "metrics_jsonl": args.metrics_jsonl, "amp": args.amp, "progress": not args.no_progress,
+               "precision": getattr(args, "precision", "fp32"),
                "zero_stage": args.zero_stage}
     if args.no_engine:
         options["use_engine"] = False
@@ -139,6 +140,8 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--zero_stage", type=int, default=0, choices=(0, 1),
                         help="1: ZeRO-1 sharded optimizer state (reduce-scatter / all-gather) under DDP")
     parser.add_argument("--amp", type=str, default=None, choices=[None, "bf16"])
+    parser.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16"],
+                        help="fused LeNet step: fp32 (reference dtype) or bf16 MFMA (fp32 masters)")
     parser.add_argument("--metrics_jsonl", type=str, default=None)
     parser.add_argument("--log_jsonl", type=str, default=None, help="mirror log records into this JSON-lines file")
     parser.add_argument("--no_progress", action="store_true")

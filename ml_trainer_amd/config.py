@@ -47,6 +47,8 @@ class TrainerOptions:
     device_data: Optional[bool] = None    # upload uint8 datasets to HBM + GPU augmentation (auto)
     per_device_batch: bool = False        # True: batch_size is per GPU (weak scaling); reference divides by W
     amp: Optional[str] = None             # None | "bf16": autocast compute dtype for generic models
+    precision: str = "fp32"               # fused LeNet engine: "fp32" (reference dtype) | "bf16" (MFMA step,
+                                          # fp32 masters; BASELINE.json configs 2/3)
     grad_clip: Optional[float] = None     # clip-by-global-norm (fused kernel)
     grad_accum_steps: int = 1             # micro-batches per optimizer step (DDP no_sync between)
     # --- distributed ----------------------------------------------------------------

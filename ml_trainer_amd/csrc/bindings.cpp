@@ -175,6 +175,8 @@ static LeNetAug make_aug(const Tensor& data, const Tensor& perm, c10::optional<T
   for (int c = 0; c < 3; ++c) {
     A.mean[c] = (float)mean[c];
     A.std[c] = (float)stdv[c];
+    A.ascale[c] = (float)(1.0 / (255.0 * stdv[c]));  // (u / 255 - mean) / std = u * ascale + ashift
+    A.ashift[c] = (float)(-mean[c] / stdv[c]);
   }
   return A;
 }
@@ -243,6 +245,7 @@ void head_cls_bwd(Tensor dlogits, Tensor pooled, Tensor wc, Tensor dpre, Tensor 
   check_dev(wc, "W_c", at::kFloat, L * h, 4);
   check_dev(dpre, "dpre", at::kBFloat16, B * h, 2);
   check_dev(dwc, "dW_c", at::kFloat, L * h, 4);
+  TORCH_CHECK(L >= 1 && L <= 1024, "head backward: num_labels must be in [1, 1024]");
   if (dbc.has_value()) check_dev(*dbc, "db_c", at::kFloat, L, 4);
   launch_head_cls_bwd(dlogits.data_ptr<float>(), pooled.data_ptr<float>(), wc.data_ptr<float>(), (int)B, (int)h,
                       (int)L, (uint16_t*)dpre.data_ptr(), dwc.data_ptr<float>(),
@@ -442,9 +445,10 @@ void gemm_f8(Tensor A, Tensor B, Tensor C, int fmt_a, int fmt_b, Tensor inv_scal
     bp = bias->data_ptr<float>();
   }
   TORCH_CHECK(mode >= 0 && mode <= 3, "gemm mode (0 none, 1 gelu, 2 dgelu, 3 tanh)");
-  if (mode != 0) {
+  if (mode == 1 || mode == 2) {  // GELU writes / dGELU reads the pre-activation (tanh needs none)
     TORCH_CHECK(aux.has_value() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
-                    aux->size(1) == N && aux->stride(1) == 1 && aux->is_cuda(), "aux must be bf16 [M,N]");
+                    aux->size(1) == N && aux->stride(1) == 1 && aux->is_cuda(),
+                "gemm_f8 mode 1/2: aux must be bf16 [M,N]");
     ap = bf16_ptr(*aux);
     ldaux = aux->stride(0);
   }
@@ -873,6 +877,8 @@ class PyXgmi {
   long long timeout_ms() const { return x_.timeout_ms(); }
   void set_algo(int a) { x_.set_algo(a); }
   int algo() const { return x_.algo(); }
+  void set_fault(int f) { x_.set_fault(f); }
+  int fault() const { return x_.fault(); }
   XgmiAllReduce& raw() { return x_; }
 
  private:
@@ -972,6 +978,22 @@ class LeNetEngine {
     if (!P_.stage || !P_.stage_meta) P_.stage = nullptr, P_.stage_meta = nullptr;
     P_.cestat = bufs.contains("cestat") ? get("cestat", at::kDouble, B * 2).data_ptr<double>() : nullptr;
     P_.dtargets = nullptr;
+    // bf16 MFMA engine buffers (optional: without them only the fp32 kernels can run)
+    if (bufs.contains("stage2") && bufs.contains("meta2") && bufs.contains("metaN") && bufs.contains("stepinfo") &&
+        bufs.contains("shadow") && bufs.contains("wimg")) {
+      P_.stage2 = get("stage2", at::kByte, B * 3072).data_ptr<uint8_t>();
+      P_.meta2 = get("meta2", at::kLong, B * 4).data_ptr<int64_t>();
+      P_.metaN = get("metaN", at::kLong, B * 4).data_ptr<int64_t>();
+      P_.stepinfo = get("stepinfo", at::kLong, 4).data_ptr<int64_t>();
+      Tensor sh = bufs["shadow"].cast<Tensor>();
+      check_dev(sh, "shadow", at::kShort, 1);
+      keep_.push_back(sh);
+      P_.shadow = reinterpret_cast<uint16_t*>(sh.data_ptr<int16_t>());
+      shadow_n_ = sh.numel();
+      P_.wimg = reinterpret_cast<uint16_t*>(get("wimg", at::kShort, lenet_mfma_wimg_elems()).data_ptr<int16_t>());
+      TORCH_CHECK(P_.slab1 != nullptr && (int64_t)C1 * 640 >= lenet_mfma_slab_floats(cfg), "slab1 too small");
+    }
+    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 32).data_ptr<float>();
     A_ = LeNetAug{};
     O_ = LeNetOpt{};
   }
@@ -1067,8 +1089,23 @@ class LeNetEngine {
     graphs_.clear();
   }
 
+  // 0: fp32 kernels (lenet.hip); 1: bf16 MFMA training step (lenet_mfma.hip; evaluation stays fp32)
+  void set_precision(int p) {
+    TORCH_CHECK(p == 0 || p == 1, "precision: 0 (fp32) or 1 (bf16)");
+    if (p == 1) TORCH_CHECK(P_.shadow && P_.wimg && P_.stage2 && P_.meta2 && P_.metaN && P_.stepinfo,
+                            "bf16 engine buffers missing");
+    prec_ = p;
+    graphs_.clear();
+  }
+  int precision() const { return prec_; }
+
   void check_mode(int mode, int B) const {
     TORCH_CHECK(B > 0 && B <= max_b_, "batch ", B, " outside [1, ", max_b_, "]");
+    if (prec_ == 1 && (mode & LENET_BWD)) {
+      TORCH_CHECK((mode & LENET_FWD) && (mode & LENET_CE), "bf16 engine: training steps are FWD|CE|BWD");
+      TORCH_CHECK(A_.ctrl != nullptr && O_.g != nullptr, "bf16 engine: set_ctrl / set_opt first");
+      TORCH_CHECK(shadow_n_ >= O_.n, "bf16 engine: shadow smaller than the flat parameters");
+    }
     TORCH_CHECK(!((mode & LENET_OPT) && (mode & LENET_REDUCE)),
                 "LENET_OPT (fused local update) and LENET_REDUCE (all-reduce + update) are exclusive");
     if (mode & LENET_REDUCE) TORCH_CHECK(A_.ctrl != nullptr, "ctrl required for the data-parallel update");
@@ -1079,17 +1116,27 @@ class LeNetEngine {
 
   void run(int mode, int B) {
     check_mode(mode, B);
-    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream());
+    const bool mf = prec_ == 1 && (mode & LENET_BWD);
+    if (mf) launch_lenet_mfma_pack(cfg_, P_, O_, cur_stream());  // shadow / fragment image from the masters
+    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream(), mf);
   }
 
   static void launch_step(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
-                          Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s) {
-    launch_lenet(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
+                          Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s, bool mfma = false) {
+    if (mfma) {
+      launch_lenet_mfma(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
+    } else {
+      launch_lenet(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
+    }
     if (mode & LENET_REDUCE) {
       if (xgmi && xgmi->world() > 1) {
-        // one-shot over xGMI (latency-bound bucket) with the optimizer fused into its epilogue
-        XgmiPostOpt post{O.p, O.s1, O.s2, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl};
-        xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s, &post);
+        // xGMI all-reduce of the latency-bound bucket, then the flat update VETOED by the
+        // transport's sticky error word: a step with any timed-out slice is applied on no slice
+        // of this rank (all-or-nothing; the host raises TransportError after the replay)
+        xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s, nullptr);
+        launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
+                          nullptr, nullptr, s, xgmi->error_dev());
+        if (mfma) launch_lenet_mfma_pack(cfg, P, O, s);
         return;
       }
       if (comm)  // (size 1 too: the W=1 RCCL rehearsal captures a real ncclAllReduce)
@@ -1098,6 +1145,9 @@ class LeNetEngine {
       launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
                         nullptr, nullptr, s);
     }
+    // the bf16 step reads its weights from the shadow / fragment image: refresh them after the
+    // data-parallel update (the single-rank step's wgrad kernel writes them itself)
+    if (mfma && (mode & LENET_REDUCE)) launch_lenet_mfma_pack(cfg, P, O, s);
   }
 
   // Capture `nsteps` consecutive steps (the device step counter advances inside)
@@ -1113,8 +1163,10 @@ class LeNetEngine {
     const int cfg = cfg_;
     Communicator* comm = comm_;
     XgmiAllReduce* xgmi = xgmi_;
+    const bool mf = prec_ == 1 && (mode & LENET_BWD);
     g->capture([&](hipStream_t s) {
-      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s);
+      if (mf) launch_lenet_mfma_pack(cfg, P, O, s);  // once per replay: the host may have changed the masters
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf);
     });
     graphs_[key(mode, B, nsteps)] = std::move(g);
   }
@@ -1150,6 +1202,8 @@ class LeNetEngine {
   XgmiAllReduce* xgmi_ = nullptr;
   py::object xgmi_keep_ = py::none();
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
+  int prec_ = 0;
+  int64_t shadow_n_ = 0;
 };
 
 }  // namespace mlt
@@ -1199,6 +1253,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("set_gemm_split_mode", &set_gemm_split_mode, py::arg("mode"));
   m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
+  m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
+  m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));
   m.def("get_lenet_variant", &get_lenet_variant);
   m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("fmt") = 0);
@@ -1244,7 +1300,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("all_reduce", &PyXgmi::all_reduce, py::arg("tensor"), py::arg("average") = true)
       .def("error", &PyXgmi::error)
       .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms)
-      .def_property("algo", &PyXgmi::algo, &PyXgmi::set_algo);
+      .def_property("algo", &PyXgmi::algo, &PyXgmi::set_algo)
+      .def_property("fault", &PyXgmi::fault, &PyXgmi::set_fault);
   py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)
@@ -1261,6 +1318,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("clear_aug", &LeNetEngine::clear_aug)
       .def("set_ctrl", &LeNetEngine::set_ctrl)
       .def("set_opt", &LeNetEngine::set_opt)
+      .def("set_precision", &LeNetEngine::set_precision)
+      .def("precision", &LeNetEngine::precision)
       .def("run", &LeNetEngine::run)
       .def("capture", &LeNetEngine::capture)
       .def("has_graph", &LeNetEngine::has_graph)

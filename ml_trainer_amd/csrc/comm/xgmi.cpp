@@ -99,10 +99,10 @@ void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st, 
   const long long ticks = timeout_ms_ * 100000LL;  // 100 MHz constant clock: 1e5 ticks per ms
   if (algo_ == 1)
     launch_xgmi_allreduce_2shot(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, slot_, blocks_, seqs_,
-                                scale, err_, ticks, post, st);
+                                scale, err_, ticks, post, st, fault_);
   else
     launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale,
-                          err_, ticks, post, st);
+                          err_, ticks, post, st, fault_);
 }
 
 void XgmiAllReduce::set_algo(int a) {

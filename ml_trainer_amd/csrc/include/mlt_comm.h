@@ -66,6 +66,11 @@ class XgmiAllReduce {
   long long timeout_ms() const { return timeout_ms_; }
   int world() const { return world_; }
   int64_t capacity() const { return cap_; }
+  // device alias of the sticky error word (a following launch can veto its work on it)
+  const unsigned* error_dev() const { return err_; }
+  // fault injection for tests: 1 = withhold half of this rank's slice flags (see allreduce.hip)
+  void set_fault(int f) { fault_ = f; }
+  int fault() const { return fault_; }
   // 0 one-shot (pull everything), 1 two-shot (push reduce-scatter + push all-gather); every rank
   // must use the same algorithm for a given call. Graphs keep the algorithm they were captured with.
   void set_algo(int a);
@@ -84,6 +89,7 @@ class XgmiAllReduce {
   long long timeout_ms_ = 2000;
   uint64_t* seqs_ = nullptr;
   bool opened_ = false;
+  int fault_ = 0;
   void* peers_host_ = nullptr;  // XgmiPeers
 };
 

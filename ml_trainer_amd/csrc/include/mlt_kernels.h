@@ -15,7 +15,8 @@ namespace mlt {
 // t  = step_ptr ? *step_ptr : t_host           (1-based step count)
 void launch_flat_optim(float* p, const float* g, float* s1, float* s2, int64_t n, const OptHyper& h,
                        const float* lr_ptr, const int64_t* lr_index_ptr, const int64_t* step_ptr, float t_host,
-                       uint16_t* shadow_bf16, const float* coef_ptr, hipStream_t stream);
+                       uint16_t* shadow_bf16, const float* coef_ptr, hipStream_t stream,
+                       const unsigned* skip = nullptr);  // skip: no update while *skip != 0
 void launch_sq_norm(const float* x, int64_t n, float* out, hipStream_t stream);
 void launch_clip_coef(const float* sq, float max_norm, float* coef, float* total_norm, hipStream_t stream);
 void launch_cast_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
@@ -51,6 +52,14 @@ struct LeNetPtrs {
   uint8_t* stage;            // [B][3072] raw uint8 images of the next step (nullptr: no staging)
   int64_t* stage_meta;       // [B][4] (perm position, dataset row, target, 0) of each staged image; -1 = empty
   double* cestat;            // [B][2] per-sample (loss / B, hit / B) for the fixed-order stats sum (or nullptr)
+  // bf16 MFMA engine (lenet_mfma.hip)
+  uint8_t* stage2;           // [B][3072] raw uint8 images of the next step (staged by the per-sample kernel)
+  int64_t* meta2;            // [B][4] (global step, perm position, dataset row, target) of each; -1 = empty
+  int64_t* metaN;            // [B][4] (global step, perm position, perm entry, 0): lookup one step further
+  int64_t* stepinfo;         // [4] (step, step in epoch, lr bits) of the running step, for the wgrad kernel
+  uint16_t* shadow;          // bf16 copy of the flat fp32 parameters (fc weights are read from it)
+  uint16_t* wimg;            // bf16 conv-weight MFMA fragment image (lenet_mfma_wimg_elems())
+  float* trace;              // LENET_TRACE phase stamps (8-byte slots) or nullptr
 };
 
 struct LeNetAug {
@@ -65,6 +74,7 @@ struct LeNetAug {
   int flip;             // RandomHorizontalFlip(p=0.5)
   int batch_stride;     // samples per step (offset into perm = ctrl[1]*batch_stride)
   float mean[3], std[3];
+  float ascale[3], ashift[3];  // normalisation as one fma (bf16 engine): u * ascale + ashift
 };
 
 struct LeNetOpt {
@@ -84,6 +94,14 @@ void launch_head_cls_fwd(const float* pooled, int B, int h, const float* wc, con
                          hipStream_t st);
 void launch_head_cls_bwd(const float* dlogits, const float* pooled, const float* wc, int B, int h, int L,
                          uint16_t* dpre, float* dwc, float* dbc, bool accumulate, hipStream_t st);
+// bf16 MFMA training step (lenet_mfma.hip): 2 launches per step (per-sample chain + batch
+// reductions / optimizer). Needs stage2 / meta2 / stepinfo / shadow, and slab1 >= B * slab floats.
+void launch_lenet_mfma(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                       hipStream_t stream);
+int lenet_mfma_slab_floats(int cfg);
+int lenet_mfma_wimg_elems();
+// shadow + wimg from the fp32 masters (O.p)
+void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);
 void set_lenet_variant(int v);  // 0 default (4 launches), 1 fully fused per-sample chain, 2 split conv2 / fc
 int get_lenet_variant();
 
@@ -189,13 +207,15 @@ struct XgmiPostOpt {
   const int64_t* lr_index_ptr;
   const int64_t* step_ptr;
 };
+// fault (tests only): 1 = this rank never publishes the slices b with b % (2 W) == rank, so on every
+// rank those slices time out while the others reduce (the "late / partial peer" case)
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
                            uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
-                           const XgmiPostOpt* post, hipStream_t st);
+                           const XgmiPostOpt* post, hipStream_t st, int fault = 0);
 // two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,
                                  int blocks, uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
-                                 const XgmiPostOpt* post, hipStream_t st);
+                                 const XgmiPostOpt* post, hipStream_t st, int fault = 0);
 
 int64_t colsum_ws_floats(int M, int N);
 void launch_colsum_bf16(const uint16_t* X, int M, int N, int64_t ldx, float* out, int accumulate, float* ws,

@@ -17,7 +17,11 @@
 // (monotonic, never reset), so the kernel is replay-safe inside multi-step hipGraphs.
 // Failure: a wait that exceeds the timeout sets the sticky error word (host-mapped, so the
 // host polls it after every graph replay without a device sync) and the block returns WITHOUT
-// reducing or updating -- no step ever runs on partial peer data. Every later launch on this
+// reducing. Blocks whose peers did arrive still reduce their slices, so the training step does
+// not fuse the update into this kernel (POST is for standalone use): the flat optimizer launch
+// that follows reads the error word and applies NOTHING on a rank that saw any timeout -- the
+// step is all-or-nothing per rank (a peer that finished its own wait may have applied it; the
+// failing rank raises TransportError and the job stops). Every later launch on this
 // rank sees the word and returns at once (it stops publishing), so every peer times out too and
 // the whole job fails loudly instead of training divergent replicas; the parity argument
 // above no longer matters because no launch after the error touches gradients or weights.
@@ -38,9 +42,10 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
                                                              int rank, int W, int64_t cap,
                                                              uint64_t* __restrict__ seqs, float scale,
                                                              unsigned* __restrict__ err, long long timeout,
-                                                             XgmiPostOpt O) {
+                                                             XgmiPostOpt O, int fault) {
   static_assert(WT >= 2 && WT <= kXgmiMaxRanks, "rank count");
   const int G = gridDim.x, b = blockIdx.x;
+  const bool withhold = fault == 1 && b % (2 * WT) == rank;  // fault injection (tests only)
   __shared__ int failed;
   if (threadIdx.x == 0) failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   __syncthreads();
@@ -64,7 +69,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
   __threadfence_system();
   __syncthreads();
   // 2. signal every peer
-  if (threadIdx.x < WT) {
+  if (threadIdx.x < WT && !withhold) {
     uint64_t* f = P.flags[threadIdx.x] + ((int64_t)p * G + b) * WT + rank;
     __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -153,11 +158,12 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
 
 template <bool POST>
 static void launch_w(int W, dim3 g, hipStream_t st, float* grad, int64_t n, const XgmiPeers& P, int rank, int64_t cap,
-                     uint64_t* seqs, float scale, unsigned* err, long long timeout, const XgmiPostOpt& post) {
+                     uint64_t* seqs, float scale, unsigned* err, long long timeout, const XgmiPostOpt& post,
+                     int fault) {
 #define MLT_XGMI_W(WV)                                                                                       \
   case WV:                                                                                                   \
     hipLaunchKernelGGL((xgmi_allreduce_kernel<POST, WV>), g, dim3(256), 0, st, grad, n, P, rank, W, cap, seqs, \
-                       scale, err, timeout, post);                                                           \
+                       scale, err, timeout, post, fault);                                                    \
     break;
   switch (W) {
     MLT_XGMI_W(2)
@@ -174,12 +180,13 @@ static void launch_w(int W, dim3 g, hipStream_t st, float* grad, int64_t n, cons
 
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
                            uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
-                           const XgmiPostOpt* post, hipStream_t st) {
+                           const XgmiPostOpt* post, hipStream_t st, int fault) {
   if (n <= 0 || W < 2 || W > kXgmiMaxRanks) return;  // (the host object rejects other world sizes)
   if (post)
-    launch_w<true>(W, dim3(blocks), st, grad, n, P, rank, cap, seqs, scale, err, timeout_ticks, *post);
+    launch_w<true>(W, dim3(blocks), st, grad, n, P, rank, cap, seqs, scale, err, timeout_ticks, *post, fault);
   else
-    launch_w<false>(W, dim3(blocks), st, grad, n, P, rank, cap, seqs, scale, err, timeout_ticks, XgmiPostOpt{});
+    launch_w<false>(W, dim3(blocks), st, grad, n, P, rank, cap, seqs, scale, err, timeout_ticks, XgmiPostOpt{},
+                    fault);
 }
 
 // ---- two-shot: reduce-scatter + all-gather, both by remote PUSHES -----------------------------
@@ -218,9 +225,10 @@ template <bool POST, int WT>
 __global__ __launch_bounds__(256) void xgmi_twoshot_kernel(float* __restrict__ grad, int64_t n, XgmiPeers P, int rank,
                                                            int64_t S, uint64_t* __restrict__ seqs, float scale,
                                                            unsigned* __restrict__ err, long long timeout,
-                                                           XgmiPostOpt O) {
+                                                           XgmiPostOpt O, int fault) {
   static_assert(WT >= 2 && WT <= kXgmiMaxRanks, "rank count");
   const int G = gridDim.x, b = blockIdx.x;
+  const bool withhold = fault == 1 && b % (2 * WT) == rank;  // fault injection (tests only)
   __shared__ int failed;
   if (threadIdx.x == 0) failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   __syncthreads();
@@ -248,7 +256,8 @@ __global__ __launch_bounds__(256) void xgmi_twoshot_kernel(float* __restrict__ g
   }
   __threadfence_system();
   __syncthreads();
-  if (threadIdx.x < WT) __hip_atomic_store(P.f1[threadIdx.x] + fo + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x < WT && !withhold)
+    __hip_atomic_store(P.f1[threadIdx.x] + fo + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (!xgmi_wait<WT>(P.f1[rank] + fo, seq, timeout, err, &failed)) return;
   // 2. reduce my slice's sub-chunk b (local reads, rank order) and gather it to every rank
   const float* mine = P.t1[rank] + (int64_t)p * WT * S;
@@ -312,11 +321,12 @@ __global__ __launch_bounds__(256) void xgmi_twoshot_kernel(float* __restrict__ g
 
 template <bool POST>
 static void launch_w2(int W, dim3 g, hipStream_t st, float* grad, int64_t n, const XgmiPeers& P, int rank, int64_t S,
-                      uint64_t* seqs, float scale, unsigned* err, long long timeout, const XgmiPostOpt& post) {
+                      uint64_t* seqs, float scale, unsigned* err, long long timeout, const XgmiPostOpt& post,
+                      int fault) {
 #define MLT_XGMI_W2(WV)                                                                                         \
   case WV:                                                                                                      \
     hipLaunchKernelGGL((xgmi_twoshot_kernel<POST, WV>), g, dim3(256), 0, st, grad, n, P, rank, S, seqs, scale, \
-                       err, timeout, post);                                                                     \
+                       err, timeout, post, fault);                                                              \
     break;
   switch (W) {
     MLT_XGMI_W2(2)
@@ -333,12 +343,13 @@ static void launch_w2(int W, dim3 g, hipStream_t st, float* grad, int64_t n, con
 
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,
                                  int blocks, uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
-                                 const XgmiPostOpt* post, hipStream_t st) {
+                                 const XgmiPostOpt* post, hipStream_t st, int fault) {
   if (n <= 0 || W < 2 || W > kXgmiMaxRanks) return;
   if (post)
-    launch_w2<true>(W, dim3(blocks), st, grad, n, P, rank, slot, seqs, scale, err, timeout_ticks, *post);
+    launch_w2<true>(W, dim3(blocks), st, grad, n, P, rank, slot, seqs, scale, err, timeout_ticks, *post, fault);
   else
-    launch_w2<false>(W, dim3(blocks), st, grad, n, P, rank, slot, seqs, scale, err, timeout_ticks, XgmiPostOpt{});
+    launch_w2<false>(W, dim3(blocks), st, grad, n, P, rank, slot, seqs, scale, err, timeout_ticks, XgmiPostOpt{},
+                     fault);
 }
 
 }  // namespace mlt

@@ -15,6 +15,7 @@
 namespace mlt {
 
 constexpr int kHeadThreads = 256;
+constexpr int kHeadMaxLabels = 1024;  // num_labels bound of the backward (bindings check it)
 
 __global__ __launch_bounds__(kHeadThreads) void head_cls_fwd_kernel(const float* __restrict__ pooled, int h,
                                                                      const float* __restrict__ wc,
@@ -46,17 +47,15 @@ __global__ __launch_bounds__(kHeadThreads) void head_cls_bwd_x_kernel(const floa
                                                                        const float* __restrict__ pooled, int h,
                                                                        uint16_t* __restrict__ dpre) {
   const int b = blockIdx.x, t = threadIdx.x;
-  __shared__ float dl[64];
+  // the sample's whole dlogits row staged once (L <= kHeadMaxLabels, host-checked): the j loop
+  // below has a thread-dependent trip count, so it must not contain a barrier
+  __shared__ float dl[kHeadMaxLabels];
+  for (int l = t; l < L; l += kHeadThreads) dl[l] = dlogits[(int64_t)b * L + l];
+  __syncthreads();
   const float* x = pooled + (int64_t)b * h;
   for (int j = t; j < h; j += kHeadThreads) {
     float s = 0.f;
-    for (int l0 = 0; l0 < L; l0 += 64) {
-      const int nl = min(64, L - l0);
-      __syncthreads();
-      if (t < nl) dl[t] = dlogits[(int64_t)b * L + l0 + t];
-      __syncthreads();
-      for (int l = 0; l < nl; ++l) s = fmaf(dl[l], wc[(int64_t)(l0 + l) * h + j], s);
-    }
+    for (int l = 0; l < L; ++l) s = fmaf(dl[l], wc[(int64_t)l * h + j], s);
     const float y = x[j];
     dpre[(int64_t)b * h + j] = f32_to_bf16(s * (1.f - y * y));
   }

@@ -1,0 +1,942 @@
+// LeNet-5 CIFAR training step (reference src/model.py:7-24, src/trainer.py:180-197) in bf16 on the
+// CDNA4 matrix cores: TWO launches per step, whatever the batch.
+//
+//   KS  lenet_ms<D>  grid B x 1024 threads, one CU per sample, the whole per-sample chain in LDS:
+//       [staged / augmented input] -> conv1 (MFMA) + bias + ReLU + maxpool -> conv2 (MFMA) + bias +
+//       ReLU + maxpool -> fc1 / fc2 / fc3 (+ReLU) -> softmax-CE -> fc dgrad chain -> unpool2 ->
+//       conv2 dgrad (MFMA) -> pool1 liveness mask -> conv2 wgrad (MFMA) and conv1 wgrad (MFMA) of
+//       the sample -> per-sample weight-gradient slab; + the NEXT step's raw input image gathered
+//       (epoch permutation -> dataset row) and staged by an otherwise idle wave, so the next step
+//       starts with one round trip instead of ctrl -> perm -> image.
+//   KW  lenet_mw<D>  role-split grid: conv slab sums over the batch (sample order), fc weight
+//       gradients over the batch, the fused optimizer update (fp32 masters + bf16 shadow), the
+//       fixed-order loss / accuracy sums, the step-counter advance.
+//
+// Why this shape (measured on the fp32 four-kernel step, profiles/lenet_pmc_r3_base.jsonl): every
+// kernel of that step sat 55-70 % of its wave cycles in s_waitcnt / barriers, and the step took
+// 30.5 us at batch 4 against 32.1 us at batch 32 -- it is a chain of latencies (kernel boundaries,
+// dependent global round trips, LDS-barrier phases), not of FLOPs. A CU per sample removes the
+// cross-CU hand-offs inside the sample's chain; bf16 MFMA (16x the f32 VALU rate) makes the conv
+// phases short enough to run on one CU (an f32 conv1 alone is >= 1.2 us of one CU's FMA issue).
+// Mixed precision as BASELINE.json configs 2/3 ("default config bf16"): bf16 operands for the
+// conv GEMMs and the fc weights, fp32 accumulation, fp32 activations through the fc chain, fp32
+// master weights and optimizer state.
+//
+// GEMM formulations (v_mfma_f32_16x16x32_bf16; lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15],
+// C rows 4(l>>4)+r / column l&15):
+//   conv1 fwd   M = 196 pooled cells x 4 window positions (a lane's 4 accumulators ARE one 2x2
+//               pool window: pooling in registers), N = out channel, K = (kh, kw pair, c4) from the
+//               [Y][X][c4] bf16 image (two 8-byte reads per fragment)
+//   conv2 fwd   M = 25 cells x 4, N = out channel, K = (tap, ic8) from the [y][x][ic8] p1 image
+//   conv2 dgrad M = 196 positions, N = in channel, K = (tap, oc16) from the zero-padded [18][18][oc16]
+//               image of the unpooled conv2-output gradient
+//   conv2 wgrad M = (kw | ic, kh) taps (+ an all-ones row = bias), N = out channel, K = positions;
+//               the A fragment is an 8-wide row window shifted by kw (wave-uniform: v_alignbyte)
+//   conv1 wgrad M = (kw | c, kh) taps (+ ones row), N = out channel, K = the 28x32 positions of the
+//               unpooled conv1 gradient; split over 3 K-ranges, summed in a fixed order
+// All batch reductions (KW) run in sample order: results are bitwise reproducible run to run.
+#include "mlt_common.h"
+#include "mlt_kernels.h"
+#include "mlt_optim.h"
+
+namespace mlt {
+namespace lm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+// Workgroup barrier for LDS hand-offs only: drains this wave's LDS (and scalar) operations and
+// meets the other waves. Unlike __syncthreads() it never waits for outstanding global loads, so
+// prefetches (the fc weights, the next step's image) stay in flight across phases.
+__device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 8 consecutive bf16 starting KW elements into the 16-element window lo ++ hi
+template <int KW>
+__device__ __forceinline__ u32x4 fshift(u32x4 lo, u32x4 hi) {
+  const unsigned d[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  constexpr int k0 = KW >> 1;
+  u32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    r[j] = (KW & 1) ? __builtin_amdgcn_alignbyte(d[k0 + j + 1], d[k0 + j], 2) : d[k0 + j];
+  return r;
+}
+
+// Block-uniform scalar read (s_load through the constant address space: lgkmcnt, not vmcnt, so
+// waiting for it never waits for the vector prefetches in flight). Only for data this kernel does
+// not write before the read; every write in this file is a vector store.
+template <class T>
+__device__ __forceinline__ T sload(const T* p) {
+  typedef const __attribute__((address_space(4))) T* cptr;
+  return *(cptr)(p);
+}
+
+__device__ __forceinline__ unsigned pack2(uint16_t lo, uint16_t hi) { return (unsigned)lo | ((unsigned)hi << 16); }
+
+// conv weight B-fragment image (bf16, 12288 entries = 24 KB): [w1f 4 ksteps][w2f 7][w2d 13], each
+// [kstep][lane][8]. Slot of a parameter element (inverse of the fragment decode in lenet_ms):
+//   conv1 fwd   k = ((kh*3 + kw/2) * 2 + kw%2) * 4 + c, n = oc
+//   conv2 fwd   k = tap * 8 + ic,                       n = oc
+//   conv2 dgrad k = tap * 16 + oc,                      n = ic
+constexpr int kW1F = 0, kW2F = 4 * 512, kW2D = 11 * 512, kWimg = 24 * 512;
+__device__ __forceinline__ int w1f_slot(int oc, int c, int kh, int kw) {
+  const int qq = kh * 3 + (kw >> 1);
+  return kW1F + (((qq >> 2) * 64 + (qq & 3) * 16 + oc) << 3) + ((kw & 1) << 2) + c;
+}
+__device__ __forceinline__ int w2f_slot(int oc, int ic, int tap) {
+  return kW2F + (((tap >> 2) * 64 + (tap & 3) * 16 + oc) << 3) + ic;
+}
+__device__ __forceinline__ int w2d_slot(int oc, int ic, int tap) {
+  return kW2D + (((tap >> 1) * 64 + ((((tap & 1) << 1) | (oc >> 3)) * 16) + ic) << 3) + (oc & 7);
+}
+// parameter element behind image entry e (or -1: padding), given the flat offsets of w1 / w2
+template <int C1, int C2>
+__device__ __forceinline__ int64_t wimg_src(int e, int64_t off_w1, int64_t off_w2) {
+  const int s = (e & 4095) >> 9;
+  if (e < kW2F) {
+    const int l = (e >> 3) & 63, j = e & 7, oc = l & 15, qq = 4 * (e >> 9) + (l >> 4);
+    const int kh = qq / 3, kw = 2 * (qq - 3 * kh) + (j >> 2), c = j & 3;
+    return (qq < 15 && oc < C1 && kw < 5 && c < 3) ? off_w1 + ((oc * 3 + c) * 5 + kh) * 5 + kw : -1;
+  }
+  if (e < kW2D) {
+    const int q = e - kW2F, l = (q >> 3) & 63, j = q & 7, oc = l & 15, tap = 4 * (q >> 9) + (l >> 4);
+    return (tap < 25 && oc < C2 && j < C1) ? off_w2 + (oc * C1 + j) * 25 + tap : -1;
+  }
+  const int q = e - kW2D, l = (q >> 3) & 63, j = q & 7, ic = l & 15, gg = l >> 4;
+  const int tap = 2 * (q >> 9) + (gg >> 1), oc = 8 * (gg & 1) + j;
+  (void)s;
+  return (tap < 25 && ic < C1 && oc < C2) ? off_w2 + (oc * C1 + ic) * 25 + tap : -1;
+}
+
+template <int C1_, int C2_, int F1_, int F2_, int NC_>
+struct Dm {
+  static constexpr int C1 = C1_, C2 = C2_, F1 = F1_, F2 = F2_, NC = NC_, FLAT = C2_ * 25;
+  static_assert(C1_ <= 8 && C2_ <= 16 && C2_ % 4 == 0 && F1_ % 4 == 0 && F2_ % 4 == 0 && NC_ <= 64, "dims");
+  // per-sample weight-gradient slab: [conv1: oc*76 + tap (75 = bias)] [conv2: natural order, then bias]
+  static constexpr int S1 = C1 * 76, S2OFF = (S1 + 3) & ~3, S2 = C2 * C1 * 25 + C2;
+  static constexpr int SLABN = (S2OFF + S2 + 15) & ~15;
+};
+using DmDefault = Dm<6, 16, 120, 84, 10>;
+using DmTiny = Dm<4, 8, 64, 32, 10>;
+
+constexpr int kT = 1024;        // KS threads (16 waves)
+constexpr int XCS = 48;          // [c][Y][X] image row stride (X >= 32 zero: shifted 8-wide windows)
+constexpr int P1CS = 32;         // [ic][y][x] pooled-conv1 image row stride (x >= 14 zero)
+constexpr int kWgT = 256;        // KW threads
+
+// ---------------------------------------------------------------------------
+// fc layer with bf16 weights held in registers (4 columns = 8 bytes per slot) for the whole
+// kernel: forward row dots (G lanes per row, DPP tree) and backward-data (each lane scales its
+// weight fragment by the upstream gradient; row groups summed through LDS in a fixed order).
+// ---------------------------------------------------------------------------
+constexpr int pow2_ge(int v) { return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : v <= 16 ? 16 : v <= 32 ? 32 : 64; }
+
+// (opaque to the optimiser: the packed weights stay the register-resident form -- CSE of the
+// forward's unpacked values into the backward would double their registers)
+__device__ __forceinline__ float4 unpack4(uint2 u) {
+  asm volatile("" : "+v"(u.x), "+v"(u.y));
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <int NCOLS, int NROWS, int NT>
+struct BLinear {
+  static constexpr int NV = NCOLS / 4;
+  static constexpr int G = pow2_ge(NV);
+  static constexpr int PL = (NV + G - 1) / G;
+  static constexpr int R = 64 / G;
+  static constexpr int NW = NT / 64;
+  static constexpr int RPI = NW * R;
+  static constexpr int IT = (NROWS + RPI - 1) / RPI;
+  static constexpr int SCRATCH = RPI * NCOLS;
+  uint2 w[IT][PL];
+
+  __device__ __forceinline__ int row(int it) const {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    return it * RPI + wid * R + lane / G;
+  }
+  // clamped, unconditional loads: padding rows / columns are never used (forward stores only
+  // r < NROWS, v < NV; backward scales padding rows by 0 and stores only v < NV)
+  // 32-bit unsigned element offsets (SGPR base + one VGPR offset per load, not a 64-bit address
+  // pair per load: all IT * PL loads are in flight at once); clamped only where a row / column
+  // group can run past the layer (compile-time per iteration)
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ W) {
+    const unsigned lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gl = lane % G;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const unsigned r0 = it * RPI + wid * R + lane / G;
+      const unsigned r = ((it + 1) * RPI > NROWS) ? min(r0, (unsigned)NROWS - 1) : r0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        const unsigned v = ((i + 1) * G > NV) ? min(gl + i * G, (unsigned)NV - 1) : gl + i * G;
+        w[it][i] = *reinterpret_cast<const uint2*>(W + (r * NCOLS + 4 * v));
+      }
+    }
+  }
+  template <bool RELU>
+  __device__ __forceinline__ void fwd(const float* xin, const float* bias, float* out_lds,
+                                      float* __restrict__ out_g) const {
+    const int gl = (threadIdx.x & 63) % G;
+    const float4* x4 = reinterpret_cast<const float4*>(xin);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        const int v = gl + i * G;
+        if (v < NV) {
+          const float4 xv = x4[v], wq = unpack4(w[it][i]);
+          acc = fmaf(wq.x, xv.x, acc);
+          acc = fmaf(wq.y, xv.y, acc);
+          acc = fmaf(wq.z, xv.z, acc);
+          acc = fmaf(wq.w, xv.w, acc);
+        }
+      }
+      acc = group_reduce_last<G>(acc);
+      const int r = row(it);
+      if (gl == G - 1 && r < NROWS) {
+        float o = acc + bias[r];
+        if (RELU) o = fmaxf(o, 0.f);
+        out_lds[r] = o;
+        out_g[r] = o;
+      }
+    }
+  }
+  // out[k] = mask(k) * sum_r d[r] W[r][k]; scratch >= SCRATCH floats. Ends with a barrier.
+  __device__ __forceinline__ void bwd(const float* d, float* scratch, float* out_lds, float* __restrict__ out_g,
+                                      const float* mask) const {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gl = lane % G, grp = wid * R + lane / G;
+    float dv[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int r = row(it);
+      dv[it] = r < NROWS ? d[r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int v = gl + i * G;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const float4 wq = unpack4(w[it][i]);
+        acc.x = fmaf(dv[it], wq.x, acc.x);
+        acc.y = fmaf(dv[it], wq.y, acc.y);
+        acc.z = fmaf(dv[it], wq.z, acc.z);
+        acc.w = fmaf(dv[it], wq.w, acc.w);
+      }
+      if (v < NV) reinterpret_cast<float4*>(scratch)[grp * NV + v] = acc;
+    }
+    lbar();
+    for (int k = threadIdx.x; k < NCOLS; k += NT) {
+      float sum = 0.f;
+#pragma unroll 8
+      for (int g = 0; g < RPI; ++g) sum += scratch[g * NCOLS + k];
+      if (mask) sum = mask[k] > 0.f ? sum : 0.f;
+      out_lds[k] = sum;
+      out_g[k] = sum;
+    }
+    lbar();
+  }
+};
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <class D>
+struct KsLds {
+  using L1 = BLinear<D::FLAT, D::F1, kT>;
+  using L2 = BLinear<D::F1, D::F2, kT>;
+  using L3 = BLinear<D::F2, D::NC, kT>;
+  static constexpr int SCR = cmax(cmax(L1::SCRATCH, L2::SCRATCH), cmax(L3::SCRATCH, 3 * 5 * 256));
+  // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
+  // MFMA fragment reads
+  alignas(16) uint16_t p1h[196 * 8];                 // pooled conv1 [y][x][ic8]
+  alignas(16) uint16_t p1c[D::C1 * 14 * P1CS];       // pooled conv1 [ic][y][x]
+  alignas(16) uint16_t dch[18 * 18 * 16];            // unpooled conv2-out grad, padded [Y+4][X+4][oc16]
+  alignas(16) uint16_t dcc[16 * 10 * 16];            // unpooled conv2-out grad [oc16][Y][X16]
+  alignas(16) uint16_t d1[D::C1 * 28 * 32];          // unpooled conv1-out grad [oc][Y][X32]
+  // end of the zero span
+  alignas(16) uint16_t xh[32 * 32 * 4];              // input [Y][X][c4] (c = 3 zero)
+  alignas(16) uint16_t xc[3 * 32 * XCS];             // input [c][Y][X48] (X >= 32 zeroed separately)
+  alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
+  alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
+  alignas(16) uint16_t w2d[13 * 64 * 8];             // conv2 dgrad B fragments
+  alignas(16) float f[D::FLAT];                      // flattened pooled conv2 (fc1 input)
+  alignas(16) float df[D::FLAT];                     // its gradient
+  alignas(16) float sh1[D::F1];
+  alignas(16) float sh2[D::F2];
+  alignas(16) float sdh1[D::F1];
+  alignas(16) float sdh2[D::F2];
+  alignas(16) float slog[64];
+  alignas(16) float sdl[64];
+  alignas(16) float scr[SCR];                        // fc bwd row-group partials / conv1 wgrad partials
+  alignas(16) uint8_t raw[3072];                     // this step's raw image (staged or gathered)
+  float b1s[16], b2s[16];
+  alignas(16) float fb[D::F1 + D::F2 + D::NC];       // fc biases
+  uint8_t i1[D::C1 * 196];
+  uint8_t i2[D::FLAT];
+};
+
+// RandomCrop(32, pad) + HFlip + ToTensor + Normalize of pixel (Y, X) from a raw HWC uint8 image
+// in LDS (src/utils/functions.py:5-12): (u / 255 - mean) / std as one fma per channel
+__device__ __forceinline__ void aug_pixel(const uint8_t* img, int Y, int X, int ci, int cj, bool fl, const LeNetAug& A,
+                                          float v[3]) {
+  const int sx = fl ? 31 - X : X;
+  const int r = Y + ci - A.pad, q = sx + cj - A.pad;
+  const bool in = (unsigned)r < 32u && (unsigned)q < 32u;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float u = in ? (float)img[(r * 32 + q) * 3 + c] : 0.f;
+    v[c] = fmaf(u, A.ascale[c], A.ashift[c]);
+  }
+}
+
+__device__ __forceinline__ void aug_params(const LeNetAug& A, int64_t step, int64_t pos, int& ci, int& cj, bool& fl) {
+  const uint64_t h = mix64(mix64(A.seed + (uint64_t)step) ^ (uint64_t)pos);
+  const int span = 2 * A.pad + 1;
+  ci = A.pad ? (int)(h % span) : 0;
+  cj = A.pad ? (int)((h >> 20) % span) : 0;
+  fl = A.flip && ((h >> 40) & 1);
+}
+
+__device__ __forceinline__ void pool4(f32x4 a, float bias, float& pv, uint8_t& code) {
+  float m = a[0];
+  int k = 0;
+  if (a[1] > m) { m = a[1]; k = 1; }
+  if (a[2] > m) { m = a[2]; k = 2; }
+  if (a[3] > m) { m = a[3]; k = 3; }
+  m += bias;
+  pv = m > 0.f ? m : 0.f;
+  code = m > 0.f ? (uint8_t)k : (uint8_t)4;
+}
+
+// ---------------------------------------------------------------------------
+// KS: the per-sample chain
+// ---------------------------------------------------------------------------
+template <class D>
+__global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A, LeNetOpt O, float inv_B) {
+  constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC;
+  using S = KsLds<D>;
+  static_assert(offsetof(S, w2f) == offsetof(S, w1f) + 2 * kW2F && offsetof(S, w2d) == offsetof(S, w1f) + 2 * kW2D,
+                "fragment images must be contiguous");
+  __shared__ S L;
+  // w is wave-uniform: readfirstlane makes the per-wave role branches scalar (uniform) branches,
+  // so a role's pending loads never force waits on the other roles' code paths
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, g = lane >> 4, m = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  // LENET_TRACE: s_memtime stamps of block 0 per phase (P.trace[0..15]; 100 MHz wall stamps at 14, 15)
+  auto stamp = [&](int k) {
+    if (!(mode & LENET_TRACE)) return;
+    lbar();
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long c, wc;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c), "=s"(wc)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (b == 0 && t == 0 && P.trace) {
+      reinterpret_cast<unsigned long long*>(P.trace)[k] = c;
+      if (k == 0) reinterpret_cast<unsigned long long*>(P.trace)[14] = wc;
+      if (k == 13) reinterpret_cast<unsigned long long*>(P.trace)[15] = wc;
+    }
+  };
+  stamp(0);
+
+  // ---- P0: every independent load in flight together ----------------------------------------
+  // straight-line and unconditional (ctrl / meta2 / stage2 are host-checked), ctrl first: the
+  // only values needed before the others arrive (vmcnt retires in issue order)
+  const bool aug = A.data != nullptr;
+  const int64_t step = sload(A.ctrl), sie = sload(A.ctrl + 1);
+  const int64_t mstep = sload(P.meta2 + 4 * b), mpos = sload(P.meta2 + 4 * b + 1), mtgt = sload(P.meta2 + 4 * b + 3);
+  uint4 sraw = reinterpret_cast<const uint4*>(P.stage2 + (int64_t)b * 3072)[min(t, 191)];
+  const bool stage_on = aug && w == 15;  // next-step staging wave (see below)
+  int64_t sN = -1, pN = -1, iN = -1;
+  if (stage_on) {
+    sN = sload(P.metaN + 4 * b);
+    pN = sload(P.metaN + 4 * b + 1);
+    iN = sload(P.metaN + 4 * b + 2);
+  }
+  float xin[3] = {0.f, 0.f, 0.f};
+  if (!aug) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) xin[c] = P.x[(int64_t)b * 3072 + c * 1024 + t];
+  }
+  // conv weight B-fragment images (bf16, packed by the optimizer / lenet_mpack): 24 KB, linear
+  const uint4* wimg4 = reinterpret_cast<const uint4*>(P.wimg);
+  const uint4 wi0 = wimg4[t], wi1 = wimg4[1024 + min(t, 511)];
+  const float b1v = P.b1[min(t, C1 - 1)], b2v = P.b2[min(t, C2 - 1)];
+  constexpr int NFB = F1 + F2 + NC;
+  const float fbv = t < F1 ? P.b3[t] : (t < F1 + F2 ? P.b4[min(t - F1, F2 - 1)] : P.b5[min(max(t - F1 - F2, 0), NC - 1)]);
+  typename S::L1 l1;
+  typename S::L2 l2;
+  typename S::L3 l3;
+  l1.load(P.shadow + O.off[4]);
+  l2.load(P.shadow + O.off[6]);
+  l3.load(P.shadow + O.off[8]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the index math below behind the load issue
+  int64_t pos = sie * A.batch_stride + b;
+  if (aug && pos >= A.perm_len) pos %= A.perm_len;
+  // next-step staging (wave 15, two steps deep so that no load waits on another inside this kernel):
+  // metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1; when it
+  // matches, the raw image of step + 1 is gathered right away (stored to stage2 in P10). The perm
+  // entry for step + 2 is looked up here and published to metaN in P10. A mismatch (epoch start,
+  // new permutation, ...) stages nothing: the next step then gathers its images itself.
+  int64_t pos1 = 0, pos2 = 0, idx1 = 0, ntgt = 0;
+  int nperm2 = 0;
+  bool st1 = false;
+  uint4 nraw0 = make_uint4(0u, 0u, 0u, 0u), nraw1 = nraw0, nraw2 = nraw0;
+  if (stage_on) {
+    pos1 = (sie + 1) * A.batch_stride + b;
+    if (pos1 >= A.perm_len) pos1 %= A.perm_len;
+    pos2 = (sie + 2) * A.batch_stride + b;
+    if (pos2 >= A.perm_len) pos2 %= A.perm_len;
+    nperm2 = sload(A.perm + pos2);
+    st1 = sN == step + 1 && pN == pos1 && iN >= 0 && iN < A.n;
+    if (st1) {
+      idx1 = iN;
+      const uint4* src = reinterpret_cast<const uint4*>(A.data + idx1 * 3072);
+      nraw0 = src[lane];
+      nraw1 = src[lane + 64];
+      nraw2 = src[lane + 128];
+      ntgt = sload(P.dtargets + idx1);
+    }
+  }
+
+  // ---- P1: input images, zero spans, weight fragment images -----------------------------------
+  const bool hit = aug && mstep == step && mpos == pos;  // block-uniform
+  int64_t tgt = 0;
+  {
+    // zero span [p1h .. d1 end) and the X >= 32 columns of xc
+    constexpr int ZB = (int)(offsetof(S, xh) - offsetof(S, p1h));
+    static_assert(ZB % 16 == 0, "zero span");
+    uint4* z = reinterpret_cast<uint4*>(L.p1h);
+    for (int e = t; e < ZB / 16; e += kT) z[e] = make_uint4(0u, 0u, 0u, 0u);
+    if (t < 3 * 32 * 2) reinterpret_cast<uint4*>(L.xc + (t >> 1) * XCS + 32)[t & 1] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* wl = reinterpret_cast<uint4*>(L.w1f);  // w1f | w2f | w2d are contiguous
+    wl[t] = wi0;
+    if (t < 512) wl[1024 + t] = wi1;
+    if (t < NFB) L.fb[t] = fbv;
+    if (t < 16) {
+      L.b1s[t] = t < C1 ? b1v : 0.f;
+      L.b2s[t] = t < C2 ? b2v : 0.f;
+    }
+  }
+  const int Y0 = t >> 5, X0 = t & 31;
+  uint2 px;
+  if (aug) {
+    // hit: the previous step staged this sample's raw image (one round trip, issued in P0);
+    // miss (first step of an epoch, ...): perm -> image. Either way crop / flip / normalise here.
+    // (the LDS write sits inside each branch: a write after the join would wait for the
+    // conservative merge of both paths' pending loads -- i.e. for every prefetch in flight)
+    if (!hit) {
+      int64_t idx = sload(A.perm + pos);
+      idx = idx < 0 ? 0 : (idx >= A.n ? A.n - 1 : idx);
+      const uint4 graw = reinterpret_cast<const uint4*>(A.data + idx * 3072)[min(t, 191)];
+      tgt = sload(P.dtargets + idx);
+      if (t < 192) reinterpret_cast<uint4*>(L.raw)[t] = graw;
+    } else {
+      tgt = mtgt;
+      if (t < 192) reinterpret_cast<uint4*>(L.raw)[t] = sraw;
+    }
+    int ci, cj;
+    bool fl;
+    aug_params(A, step, pos, ci, cj, fl);
+    lbar();
+    float v[3];
+    aug_pixel(L.raw, Y0, X0, ci, cj, fl, A, v);
+    px = make_uint2(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), 0));
+  } else {
+    px = make_uint2(pack2(f32_to_bf16(xin[0]), f32_to_bf16(xin[1])), pack2(f32_to_bf16(xin[2]), 0));
+    tgt = sload(P.targets + b);
+  }
+  reinterpret_cast<uint2*>(L.xh)[t] = px;
+  L.xc[(0 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x & 0xffff);
+  L.xc[(1 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x >> 16);
+  L.xc[(2 * 32 + Y0) * XCS + X0] = (uint16_t)(px.y & 0xffff);
+  lbar();
+  stamp(1);
+
+  // ---- P2: conv1 (MFMA) + bias + ReLU + maxpool in registers -> p1 images, i1 ------------------
+  {
+    const uint16_t* xh = L.xh;
+    for (int T = w; T < 49; T += 16) {
+      const int cell = 4 * T + (m >> 2), q = m & 3;
+      const int py = cell / 14, pxx = cell - 14 * py, Y = 2 * py + (q >> 1), X = 2 * pxx + (q & 1);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int qq = 4 * s + g, kh = qq / 3, kwp = qq - 3 * kh;
+        const int p = qq < 15 ? (Y + kh) * 32 + X + 2 * kwp : 0;
+        const uint2 lo = *reinterpret_cast<const uint2*>(xh + 4 * p), hi = *reinterpret_cast<const uint2*>(xh + 4 * p + 4);
+        u32x4 a = {lo.x, lo.y, hi.x, hi.y};
+        if (qq >= 15) a = u32x4{0u, 0u, 0u, 0u};
+        acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w1f + (s * 64 + lane) * 8), acc);
+      }
+      const int cc = 4 * T + g, oc = m;
+      float pv;
+      uint8_t code;
+      pool4(acc, L.b1s[oc], pv, code);
+      if (oc < C1) {
+        const int cy = cc / 14, cx = cc - 14 * cy;
+        const uint16_t hv = f32_to_bf16(pv);
+        L.p1h[cc * 8 + oc] = hv;
+        L.p1c[(oc * 14 + cy) * P1CS + cx] = hv;
+        L.i1[oc * 196 + cc] = code;
+      }
+    }
+  }
+  lbar();
+  stamp(2);
+
+  // ---- P3: conv2 (MFMA) + bias + ReLU + maxpool -> f (flatten order oc*25 + cell), i2 ----------
+  if (w < 7) {
+    const int r = 16 * w + m, cell = min(r >> 2, 24), q = r & 3;
+    const int py = cell / 5, pxx = cell - 5 * py, y = 2 * py + (q >> 1), x = 2 * pxx + (q & 1);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int tap = 4 * s + g, kh = tap / 5, kw = tap - 5 * kh;
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * 14 + x + kw : 0)) * 8);
+      if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
+      acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2f + (s * 64 + lane) * 8), acc);
+    }
+    const int cc = 4 * w + g, oc = m;
+    float pv;
+    uint8_t code;
+    pool4(acc, L.b2s[oc], pv, code);
+    if (cc < 25 && oc < C2) {
+      const int o = oc * 25 + cc;
+      L.f[o] = pv;
+      L.i2[o] = code;
+      P.p2[(int64_t)b * FLAT + o] = pv;
+    }
+  }
+  lbar();
+  stamp(3);
+
+  // ---- P4-P9: fc1 -> fc2 -> fc3 -> softmax-CE -> fc dgrad chain -------------------------------
+  l1.template fwd<true>(L.f, L.fb, L.sh1, P.h1 + (int64_t)b * F1);
+  lbar();
+  l2.template fwd<true>(L.sh1, L.fb + F1, L.sh2, P.h2 + (int64_t)b * F2);
+  lbar();
+  l3.template fwd<false>(L.sh2, L.fb + F1 + F2, L.slog, P.logits + (int64_t)b * NC);
+  lbar();
+  stamp(4);
+  if (w == 0) {
+    constexpr int GC = pow2_ge(NC);
+    const float z = lane < NC ? L.slog[lane] : -INFINITY;
+    const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC, true>(z)), GC - 1));
+    const float e = lane < NC ? expf(z - mx) : 0.f;
+    const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC>(e)), GC - 1));
+    const float lse = mx + logf(s);
+    const bool valid = tgt >= 0 && tgt < NC;
+    const unsigned long long am_mask = __ballot(lane < NC && z == mx);
+    const int am = __ffsll((long long)am_mask) - 1;
+    const float loss = valid ? lse - L.slog[valid ? tgt : 0] : 0.f;
+    if (lane < NC) {
+      const float dl = valid ? (e / s - (lane == tgt ? 1.f : 0.f)) * inv_B : 0.f;
+      L.sdl[lane] = dl;
+      P.dlogits[(int64_t)b * NC + lane] = dl;
+    }
+    if (lane == 0 && P.cestat) {
+      P.cestat[2 * b] = (double)loss * (double)inv_B;
+      P.cestat[2 * b + 1] = (am == tgt) ? (double)inv_B : 0.0;
+    }
+  }
+  lbar();
+  l3.bwd(L.sdl, L.scr, L.sdh2, P.dh2 + (int64_t)b * F2, L.sh2);
+  l2.bwd(L.sdh2, L.scr, L.sdh1, P.dh1 + (int64_t)b * F1, L.sh1);
+  l1.bwd(L.sdh1, L.scr, L.df, P.dflat + (int64_t)b * FLAT, nullptr);
+  stamp(5);
+
+  // ---- P10: unpool2 -> the conv2-output gradient images (zero except at arg-max cells) ---------
+  for (int e = t; e < FLAT; e += kT) {
+    const int code = L.i2[e];
+    if (code < 4) {
+      const int oc = e / 25, cell = e - 25 * oc, py = cell / 5, pxx = cell - 5 * py;
+      const int Y = 2 * py + (code >> 1), X = 2 * pxx + (code & 1);
+      const uint16_t v = f32_to_bf16(L.df[e]);
+      L.dch[((Y + 4) * 18 + X + 4) * 16 + oc] = v;
+      L.dcc[(oc * 10 + Y) * 16 + X] = v;
+    }
+  }
+  if (stage_on) {  // wave 15 (no unpool work): publish the next step's raw image + tags
+    if (st1) {
+      uint4* dst = reinterpret_cast<uint4*>(P.stage2 + (int64_t)b * 3072);
+      dst[lane] = nraw0;
+      dst[lane + 64] = nraw1;
+      dst[lane + 128] = nraw2;
+    }
+    if (lane == 0) {
+      if (st1) {
+        P.meta2[4 * b] = step + 1;
+        P.meta2[4 * b + 1] = pos1;
+        P.meta2[4 * b + 2] = idx1;
+        P.meta2[4 * b + 3] = ntgt;
+      }
+      P.metaN[4 * b] = step + 2;
+      P.metaN[4 * b + 1] = pos2;
+      P.metaN[4 * b + 2] = nperm2;
+    }
+  }
+  lbar();
+  stamp(6);
+
+  // ---- P11: conv2 dgrad (waves 0-12) -> liveness mask -> unpooled conv1 grad d1 ----------------
+  //           conv2 wgrad of the sample (waves 13-15) -> slab
+  float* slab = P.slab1 + (int64_t)b * D::SLABN;
+  if (w < 13) {
+    const int pos_a = min(16 * w + m, 195), Y = pos_a / 14, X = pos_a - 14 * Y;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      const int tap = 2 * s + (g >> 1), oc0 = 8 * (g & 1), kh = tap / 5, kw = tap - 5 * kh;
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((tap < 25 ? (Y - kh + 4) * 18 + X - kw + 4 : 0)) * 16 + oc0);
+      if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
+      acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2d + (s * 64 + lane) * 8), acc);
+    }
+    const int ic = m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pc = 16 * w + 4 * g + r;
+      if (pc < 196 && ic < C1) {
+        const int code = L.i1[ic * 196 + pc];
+        const float gv = code < 4 ? acc[r] : 0.f;
+        if (P.g1) P.g1[((int64_t)b * C1 + ic) * 196 + pc] = gv;
+        if (code < 4) {
+          const int py = pc / 14, pxx = pc - 14 * py;
+          L.d1[(ic * 28 + 2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(gv);
+        }
+      }
+    }
+  } else if (w < 15) {
+    // 10 M-tiles: tile tt = (kw, half); rows (ic, kh) = 16 * half + m; row 31 of tile 1 = ones (bias)
+    const int t0 = w == 13 ? 0 : 5, t1 = w == 13 ? 5 : 10;
+    for (int tt = t0; tt < t1; ++tt) {
+      const int kw = tt >> 1, h = tt & 1, i = 16 * h + m, ic = i / 5, kh = i - 5 * ic;
+      const bool valid = ic < C1, ones = tt == 1 && m == 15;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const int y = 2 * s + (g >> 1), x0 = 8 * (g & 1);
+        const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * 16 + x0);
+        const uint16_t* rowp = L.p1c + ((valid ? ic : 0) * 14 + y + (valid ? kh : 0)) * P1CS + x0;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp), hi = *reinterpret_cast<const u32x4*>(rowp + 8);
+        u32x4 a;
+        switch (kw) {
+          case 0: a = fshift<0>(lo, hi); break;
+          case 1: a = fshift<1>(lo, hi); break;
+          case 2: a = fshift<2>(lo, hi); break;
+          case 3: a = fshift<3>(lo, hi); break;
+          default: a = fshift<4>(lo, hi); break;
+        }
+        if (!valid) a = ones ? u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u32x4{0u, 0u, 0u, 0u};
+        acc = mfma(a, bq, acc);
+      }
+      const int oc = m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ir = 16 * h + 4 * g + r, icr = ir / 5, khr = ir - 5 * icr;
+        if (oc < C2 && icr < C1) slab[D::S2OFF + (oc * C1 + icr) * 25 + khr * 5 + kw] = acc[r];
+        if (oc < C2 && tt == 1 && ir == 31) slab[D::S2OFF + C2 * C1 * 25 + oc] = acc[r];
+      }
+    }
+  }
+  lbar();
+  stamp(7);
+
+  // ---- P13: conv1 wgrad (waves 0-14: tile kw = w / 3, K range w % 3) ---------------------------
+  //           next-step staging (wave 15)
+  if (w < 15) {
+    const int kw = w / 3, kp = w - 3 * kw, c = m / 5, kh = m - 5 * c;
+    const bool valid = m < 15, ones = m == 15 && kw == 0;
+    const int ya = 10 * kp, yb = min(ya + 10, 28), x0 = 8 * g;
+    const uint16_t* xrow = L.xc + ((valid ? c : 0) * 32 + (valid ? kh : 0)) * XCS + x0;
+    const uint16_t* drow = L.d1 + (min(m, C1 - 1) * 28) * 32 + x0;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int Y = ya; Y < yb; ++Y) {
+      u32x4 bq = *reinterpret_cast<const u32x4*>(drow + Y * 32);
+      if (m >= C1) bq = u32x4{0u, 0u, 0u, 0u};
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(xrow + Y * XCS), hi = *reinterpret_cast<const u32x4*>(xrow + Y * XCS + 8);
+      u32x4 a;
+      switch (kw) {
+        case 0: a = fshift<0>(lo, hi); break;
+        case 1: a = fshift<1>(lo, hi); break;
+        case 2: a = fshift<2>(lo, hi); break;
+        case 3: a = fshift<3>(lo, hi); break;
+        default: a = fshift<4>(lo, hi); break;
+      }
+      if (!valid) a = ones ? u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u32x4{0u, 0u, 0u, 0u};
+      acc = mfma(a, bq, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) L.scr[((kp * 5 + kw) * 16 + 4 * g + r) * 16 + m] = acc[r];
+  }
+  lbar();
+  for (int e = t; e < 5 * 256; e += kT) {
+    const int kw = e >> 8, i = (e >> 4) & 15, oc = e & 15;
+    const float v = (L.scr[e] + L.scr[1280 + e]) + L.scr[2560 + e];
+    if (oc < C1) {
+      if (i < 15) slab[oc * 76 + (i / 5) * 25 + (i % 5) * 5 + kw] = v;
+      else if (kw == 0) slab[oc * 76 + 75] = v;
+    }
+  }
+  if (aug && t == 0 && P.targets) P.targets[b] = tgt;  // (inspection; nothing downstream reads it)
+  // the step's optimizer context for KW (lr from the device table, Adam's t)
+  if (b == 0 && t == 0 && P.stepinfo) {
+    float lr = O.h.lr;
+    if (O.lr_ptr) lr = O.lr_ptr[O.lr_table ? sie : 0];
+    P.stepinfo[0] = step;
+    P.stepinfo[1] = sie;
+    P.stepinfo[2] = (int64_t)__float_as_uint(lr);
+  }
+  stamp(13);
+}
+
+// ---------------------------------------------------------------------------
+// KW: batch reductions + optimizer
+// ---------------------------------------------------------------------------
+struct Ctx {
+  bool on;
+  float lr, t;
+};
+
+__device__ __forceinline__ void upd1(const LeNetOpt& O, const Ctx& c, uint16_t* shadow, int64_t i, float g, float p,
+                                     float a, float s) {
+  O.g[i] = g;
+  if (!c.on) return;
+  opt_update(O.h, c.lr, c.t, p, g, a, s);
+  O.p[i] = p;
+  if (O.s1) O.s1[i] = a;
+  if (O.s2) O.s2[i] = s;
+  if (shadow) shadow[i] = f32_to_bf16(p);
+}
+
+template <class D>
+__host__ __device__ constexpr int mw_conv_blocks() {
+  return (D::S1 + D::S2 + kWgT - 1) / kWgT;
+}
+template <class D>
+__host__ __device__ constexpr int mw_fc_blocks() {
+  return (D::F1 * (D::FLAT / 4) + kWgT - 1) / kWgT + (D::F2 * (D::F1 / 4) + kWgT - 1) / kWgT +
+         (D::NC * (D::F2 / 4) + kWgT - 1) / kWgT;
+}
+
+template <int NCOLS>
+__device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float* __restrict__ dY,
+                                         const float* __restrict__ X, const LeNetOpt& O, const Ctx& c,
+                                         uint16_t* shadow, int64_t offW, int64_t offb) {
+  constexpr int NV = NCOLS / 4;
+  const int item = blk * kWgT + threadIdx.x;
+  if (item >= nrows * NV) return;
+  const int j = item / NV, v = item - j * NV;
+  const int64_t iw = offW + 4 * (int64_t)item, ib = offb + j;
+  float4 pw = make_float4(0.f, 0.f, 0.f, 0.f), aw = pw, sw = pw;
+  float pb = 0.f, ab = 0.f, sb = 0.f;
+  if (c.on) {  // optimizer state in flight together with the batch loads
+    pw = *reinterpret_cast<const float4*>(O.p + iw);
+    if (O.s1) aw = *reinterpret_cast<const float4*>(O.s1 + iw);
+    if (O.s2) sw = *reinterpret_cast<const float4*>(O.s2 + iw);
+    if (v == 0) {
+      pb = O.p[ib];
+      if (O.s1) ab = O.s1[ib];
+      if (O.s2) sb = O.s2[ib];
+    }
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float bacc = 0.f;
+  const float4* x4 = reinterpret_cast<const float4*>(X);
+#pragma unroll 2
+  for (int b0 = 0; b0 < B; b0 += 8) {
+    float d[8];
+    float4 xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int bb = min(b0 + u, B - 1);
+      d[u] = dY[(int64_t)bb * nrows + j];
+      xv[u] = x4[(int64_t)bb * NV + v];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float du = b0 + u < B ? d[u] : 0.f;
+      acc.x = fmaf(du, xv[u].x, acc.x);
+      acc.y = fmaf(du, xv[u].y, acc.y);
+      acc.z = fmaf(du, xv[u].z, acc.z);
+      acc.w = fmaf(du, xv[u].w, acc.w);
+      bacc += du;
+    }
+  }
+  *reinterpret_cast<float4*>(O.g + iw) = acc;
+  if (c.on) {
+    opt_update(O.h, c.lr, c.t, pw.x, acc.x, aw.x, sw.x);
+    opt_update(O.h, c.lr, c.t, pw.y, acc.y, aw.y, sw.y);
+    opt_update(O.h, c.lr, c.t, pw.z, acc.z, aw.z, sw.z);
+    opt_update(O.h, c.lr, c.t, pw.w, acc.w, aw.w, sw.w);
+    *reinterpret_cast<float4*>(O.p + iw) = pw;
+    if (O.s1) *reinterpret_cast<float4*>(O.s1 + iw) = aw;
+    if (O.s2) *reinterpret_cast<float4*>(O.s2 + iw) = sw;
+    if (shadow)
+      *reinterpret_cast<uint2*>(shadow + iw) =
+          make_uint2(pack2(f32_to_bf16(pw.x), f32_to_bf16(pw.y)), pack2(f32_to_bf16(pw.z), f32_to_bf16(pw.w)));
+  }
+  if (v == 0) upd1(O, c, shadow, ib, bacc, pb, ab, sb);
+}
+
+template <class D>
+__global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
+  constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
+  constexpr int NBC = mw_conv_blocks<D>();
+  constexpr int NB3 = (F1 * (FLAT / 4) + kWgT - 1) / kWgT, NB4 = (F2 * (F1 / 4) + kWgT - 1) / kWgT,
+                NB5 = (NC * (F2 / 4) + kWgT - 1) / kWgT;
+  const int t = threadIdx.x;
+  int blk = blockIdx.x;
+  // the step's counters / lr as the per-sample kernel saw them (nothing here reads ctrl, which
+  // block NBC + fc blocks advances)
+  const int64_t step = P.stepinfo[0], sie = P.stepinfo[1];
+  Ctx c;
+  c.on = (mode & LENET_OPT) != 0;
+  c.t = (float)(step + 1);
+  c.lr = __uint_as_float((unsigned)P.stepinfo[2]);
+  uint16_t* shadow = P.shadow;
+  if (blk < NBC) {
+    const int e = blk * kWgT + t;
+    if (e >= D::S1 + D::S2) return;
+    int soff;
+    int64_t dst;
+    if (e < D::S1) {
+      const int oc = e / 76, tap = e - 76 * oc;
+      soff = e;
+      dst = tap < 75 ? O.off[0] + oc * 75 + tap : O.off[1] + oc;
+    } else {
+      const int e2 = e - D::S1;
+      soff = D::S2OFF + e2;
+      dst = e2 < C2 * C1 * 25 ? O.off[2] + e2 : O.off[3] + (e2 - C2 * C1 * 25);
+    }
+    float p = 0.f, a = 0.f, s = 0.f;
+    if (c.on) {
+      p = O.p[dst];
+      if (O.s1) a = O.s1[dst];
+      if (O.s2) s = O.s2[dst];
+    }
+    float gsum = 0.f;  // all loads of a 32-sample chunk in flight, summed in sample order
+    for (int b0 = 0; b0 < B; b0 += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = P.slab1[(int64_t)min(b0 + u, B - 1) * D::SLABN + soff];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) gsum += b0 + u < B ? v[u] : 0.f;
+    }
+    O.g[dst] = gsum;
+    if (c.on) {
+      opt_update(O.h, c.lr, c.t, p, gsum, a, s);
+      O.p[dst] = p;
+      if (O.s1) O.s1[dst] = a;
+      if (O.s2) O.s2[dst] = s;
+      const uint16_t hb = f32_to_bf16(p);
+      if (shadow) shadow[dst] = hb;
+      if (P.wimg) {  // the per-sample kernel's fragment image of the conv weights
+        if (e < D::S1) {
+          const int oc = e / 76, tap = e - 76 * oc;
+          if (tap < 75) P.wimg[w1f_slot(oc, tap / 25, (tap % 25) / 5, tap % 5)] = hb;
+        } else {
+          const int e2 = e - D::S1;
+          if (e2 < C2 * C1 * 25) {
+            const int oc = e2 / (C1 * 25), ic = (e2 / 25) % C1, tap = e2 % 25;
+            P.wimg[w2f_slot(oc, ic, tap)] = hb;
+            P.wimg[w2d_slot(oc, ic, tap)] = hb;
+          }
+        }
+      }
+    }
+    return;
+  }
+  blk -= NBC;
+  if (blk < NB3) {
+    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5]);
+  } else if ((blk -= NB3) < NB4) {
+    fc_wgrad<F1>(blk, F2, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7]);
+  } else if ((blk -= NB4) < NB5) {
+    fc_wgrad<F2>(blk, NC, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9]);
+  } else {
+    // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats
+    __shared__ double red[2][4];
+    const int lane = t & 63, wid = t >> 6;
+    double s0 = 0.0, s1 = 0.0;
+    for (int i = t; i < B; i += kWgT) {
+      s0 += P.cestat[2 * i];
+      s1 += P.cestat[2 * i + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+    }
+    if (lane == 0) {
+      red[0][wid] = s0;
+      red[1][wid] = s1;
+    }
+    __syncthreads();
+    if (t == 0) {
+      P.stats[0] += ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+      P.stats[1] += ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+      if (ctrl) {  // advance the device step counters (next step / lr index / Adam t)
+        ctrl[0] = step + 1;
+        ctrl[1] = sie + 1;
+      }
+    }
+  }
+}
+
+// bf16 shadow of the flat parameters + the conv fragment image, from the fp32 masters (start of
+// every captured step sequence, and after each data-parallel optimizer launch)
+template <class D>
+__global__ __launch_bounds__(256) void lenet_mpack(const float* __restrict__ p, int64_t n, uint16_t* __restrict__ shadow,
+                                                  uint16_t* __restrict__ wimg, int64_t off_w1, int64_t off_w2) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) shadow[i] = f32_to_bf16(p[i]);
+  if (i < kWimg) {
+    const int64_t src = wimg_src<D::C1, D::C2>((int)i, off_w1, off_w2);
+    wimg[i] = src >= 0 ? f32_to_bf16(p[src]) : (uint16_t)0;
+  }
+}
+
+template <class D>
+void pack(const LeNetPtrs& P, const LeNetOpt& O, hipStream_t st) {
+  const int64_t tot = O.n > kWimg ? O.n : kWimg;
+  hipLaunchKernelGGL(lenet_mpack<D>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, O.p, O.n, P.shadow, P.wimg,
+                     O.off[0], O.off[2]);
+}
+
+template <class D>
+void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
+  const float inv_B = 1.f / (float)B;
+  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
+  const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
+  hipLaunchKernelGGL(lenet_mw<D>, dim3(nblk), dim3(kWgT), 0, st, mode, P, O, B, A.ctrl);
+}
+
+}  // namespace lm
+
+int lenet_mfma_slab_floats(int cfg) { return cfg == LENET_TINY ? lm::DmTiny::SLABN : lm::DmDefault::SLABN; }
+int lenet_mfma_wimg_elems() { return lm::kWimg; }
+
+void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream) {
+  if (cfg == LENET_TINY)
+    lm::pack<lm::DmTiny>(P, O, stream);
+  else
+    lm::pack<lm::DmDefault>(P, O, stream);
+}
+
+void launch_lenet_mfma(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                       hipStream_t stream) {
+  if (B <= 0) return;
+  if (cfg == LENET_TINY)
+    lm::run<lm::DmTiny>(mode, B, P, A, O, stream);
+  else
+    lm::run<lm::DmDefault>(mode, B, P, A, O, stream);
+}
+
+}  // namespace mlt

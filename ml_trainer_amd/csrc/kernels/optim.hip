@@ -18,7 +18,11 @@ __global__ __launch_bounds__(256) void flat_optim_kernel(float* __restrict__ p, 
                                                          const int64_t* __restrict__ lr_index_ptr,
                                                          const int64_t* __restrict__ step_ptr, float t_host,
                                                          uint16_t* __restrict__ shadow,
-                                                         const float* __restrict__ coef_ptr) {
+                                                         const float* __restrict__ coef_ptr,
+                                                         const unsigned* __restrict__ skip) {
+  // all-or-nothing data-parallel step: a collective that failed on this rank (sticky error word,
+  // e.g. an xGMI peer timeout that left some slices unreduced) vetoes the whole update
+  if (skip && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
   const float lr = lr_ptr ? lr_ptr[lr_index_ptr ? (*lr_index_ptr - 1) : 0] : h.lr;
   const float t = step_ptr ? (float)(*step_ptr) : t_host;
   if (coef_ptr) h.grad_scale *= *coef_ptr;  // e.g. clip-by-norm coefficient
@@ -93,11 +97,11 @@ static inline int grid_for(int64_t n4) {
 
 void launch_flat_optim(float* p, const float* g, float* s1, float* s2, int64_t n, const OptHyper& h,
                        const float* lr_ptr, const int64_t* lr_index_ptr, const int64_t* step_ptr, float t_host,
-                       uint16_t* shadow, const float* coef_ptr, hipStream_t stream) {
+                       uint16_t* shadow, const float* coef_ptr, hipStream_t stream, const unsigned* skip) {
   const int64_t n4 = n / 4;
   if (n4 == 0) return;
   hipLaunchKernelGGL(flat_optim_kernel, dim3(grid_for(n4)), dim3(256), 0, stream, p, g, s1, s2, n4, h, lr_ptr,
-                     lr_index_ptr, step_ptr, t_host, shadow, coef_ptr);
+                     lr_index_ptr, step_ptr, t_host, shadow, coef_ptr, skip);
 }
 
 void launch_sq_norm(const float* x, int64_t n, float* out, hipStream_t stream) {

@@ -111,6 +111,13 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         "stage_meta": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
         # per-sample (loss / B, hit / B) of a training step, summed in sample order by K4
         "cestat": torch.zeros(B * 2, dtype=torch.float64, device=device),
+        # bf16 MFMA engine (lenet_mfma.hip): raw next-step images staged by the per-sample kernel,
+        # tagged (global step, perm position, dataset row, target); metaN = the perm lookup one step
+        # further; stepinfo = (step, step in epoch, lr bits) handed to the wgrad kernel
+        "stage2": torch.zeros(B * 3072, dtype=torch.uint8, device=device),
+        "meta2": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
+        "metaN": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
+        "stepinfo": torch.zeros(4, dtype=torch.int64, device=device),
     }
     return bufs
 

@@ -42,8 +42,15 @@ class TransportError(RuntimeError):
 
 
 class LeNetStepEngine:
+    """``precision``: "fp32" (default; the reference model's dtype, four fp32 kernels per step) or
+    "bf16" (BASELINE.json configs 2/3: bf16 MFMA operands, fp32 accumulation / activations /
+    master weights / optimizer state; two kernels per step, csrc/kernels/lenet_mfma.hip).
+    Evaluation always runs the fp32 forward on the fp32 masters."""
+
     def __init__(self, model: MLModel, flat: FlatParams, max_batch: int, optimizer=None, process_group=None,
-                 world_size: int = 1, seed: int = 0):
+                 world_size: int = 1, seed: int = 0, precision: str = "fp32"):
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         C = require_native()
         self.C = C
         self.model = model
@@ -62,11 +69,17 @@ class LeNetStepEngine:
             o, n = flat.segment(p)
             bufs[name] = flat.data[o:o + n]
             bufs["g" + name] = flat.grad[o:o + n]
+        # bf16 engine: bf16 copy of the flat parameters + the conv-weight MFMA fragment image
+        bufs["shadow"] = torch.zeros(flat.numel, dtype=torch.int16, device=self.device)
+        bufs["wimg"] = torch.zeros(C.lenet_mfma_wimg_elems(), dtype=torch.int16, device=self.device)
         self.bufs = bufs
         self.stats = bufs["stats"]
         self.ctrl = torch.zeros(2, dtype=torch.int64, device=self.device)
         self.eng = C.LeNetEngine(model.cfg_id, self.max_batch, bufs)
         self.eng.set_ctrl(self.ctrl)
+        self.precision = precision
+        if precision == "bf16":
+            self.eng.set_precision(1)
         self.offsets = [flat.segment(p)[0] for p in params]
         self.comm = None
         self.xgmi = None
@@ -96,11 +109,23 @@ class LeNetStepEngine:
             warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed")
             self.comm = None
         self.xgmi = create_xgmi_allreduce(process_group, self.flat.numel, self.device)
+        # availability is agreed (MIN over ranks) BEFORE any rank times a candidate: every rank
+        # then runs the same trials in the same order and the same MAX vote below (a rank whose
+        # RCCL bring-up failed would otherwise skip the RCCL trial and desynchronise the group)
+        coll_dev = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+        x = self.xgmi
+        avail = torch.tensor([float(self.comm is not None), float(x is not None),
+                              float(x is not None and getattr(x, "two_shot_ok", True))], device=coll_dev)
+        dist.all_reduce(avail, op=dist.ReduceOp.MIN, group=process_group)
+        have_rccl, have_xgmi, have_two = (bool(v) for v in avail.tolist())
+        if not have_rccl:
+            self.comm = None
+        if not have_xgmi:
+            self.xgmi = x = None
         if self.comm is None and self.xgmi is None:
             return
         t = self.flat.grad.clone()
         cands = []
-        x = self.xgmi
         if x is not None:
             def one():
                 x.algo = 0
@@ -110,7 +135,7 @@ class LeNetStepEngine:
                 x.algo = 1
                 x.all_reduce(t, True)
             cands.append(("xgmi", one))
-            if getattr(x, "two_shot_ok", True):  # passed its self-test on every rank
+            if have_two:  # passed its self-test on every rank
                 cands.append(("xgmi2", two))
         if self.comm is not None:
             cands.append(("rccl", lambda: self.comm.all_reduce(t, "avg")))
@@ -157,7 +182,7 @@ class LeNetStepEngine:
         if self.dp_transport.startswith("xgmi") and self.xgmi is not None:
             if self.xgmi.error():
                 raise TransportError("xGMI all-reduce: a peer did not arrive within "
-                                     f"{self.xgmi.timeout_ms} ms; the step was not applied")
+                                     f"{self.xgmi.timeout_ms} ms; this rank applied no part of that step")
         elif self.dp_transport == "rccl" and self.comm is not None:
             err = self.comm.async_error()
             if err:
@@ -197,7 +222,7 @@ class LeNetStepEngine:
         cap = int(perm_capacity or self.data.shape[0])
         self.perm = torch.zeros(max(cap, 1), dtype=torch.int32, device=self.device)
         self.batch_size = int(batch_size)
-        self.bufs["stage_meta"].fill_(-1)  # staged next-step images belong to the old dataset
+        self._reset_staging()  # staged next-step images belong to the old dataset
         self.eng.set_aug(self.data, self.perm, self.ctrl, self.targets, self.seed, pad if augment else 0,
                          1 if (augment and flip) else 0, self.batch_size, list(mean), list(std))
 
@@ -208,7 +233,7 @@ class LeNetStepEngine:
             raise ValueError("epoch permutation larger than perm capacity")
         self.perm[:n].copy_(indices.to(torch.int32), non_blocking=True)
         self.ctrl[1:2].zero_()
-        self.bufs["stage_meta"].fill_(-1)  # images staged by the last step came from the old order
+        self._reset_staging()  # images staged by the last step came from the old order
         if lr_values is not None:
             if not self._use_table:
                 raise RuntimeError("engine not configured with an lr table")
@@ -216,6 +241,10 @@ class LeNetStepEngine:
             self.lr_table[:vals.numel()].copy_(vals, non_blocking=False)
         elif self.optimizer is not None:
             self.optimizer.lr_tensor(0)  # sync group lr -> device scalar
+
+    def _reset_staging(self) -> None:
+        for k in ("stage_meta", "meta2", "metaN"):
+            self.bufs[k].fill_(-1)
 
     def reset_stats(self) -> None:
         self.stats.zero_()

@@ -74,7 +74,10 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     x, ok = None, True
     try:
         x = C.XgmiAllReduce(int(capacity), world, rank, dev.index)
-        x.timeout_ms = int(os.environ.get("MLT_XGMI_TIMEOUT_MS", "2000"))
+        # a timeout is fatal (sticky error word -> TransportError), and ranks are not lined up
+        # before the first replay of a step graph (each builds its dataset / captures its graphs):
+        # generous by default; dead peers are the watchdog's job (600 s)
+        x.timeout_ms = int(os.environ.get("MLT_XGMI_TIMEOUT_MS", "30000"))
         h = x.handle()
     except RuntimeError:
         ok, h = False, b""

@@ -9,9 +9,15 @@ SMDDP backend (``src/trainer.py:97-101``) and its dead manual
   registration order -- the order autograd produces gradients -- so each bucket
   is a contiguous slice that is all-reduced in place (no copy-in/out);
 * a per-bucket countdown driven by ``post_accumulate_grad`` hooks launches the
-  bucket's all-reduce (``async_op=True`` on RCCL's own stream, ordered after the
-  producing kernels) as soon as its last gradient lands, so communication
-  overlaps the rest of backward; the end-of-backward callback only waits;
+  bucket's all-reduce as soon as its last gradient lands, so communication overlaps
+  the rest of backward;
+* GPU jobs on RCCL (``backend="nccl"``, W > 1) reduce through the NATIVE communicator
+  (csrc/comm/comm.cpp, ``ncclAllReduce`` AVG) enqueued on a dedicated high-priority HIP
+  comm stream: a hipEvent recorded on the compute stream when the bucket is ready, the
+  comm stream waits on it, the collective runs there, and the end-of-backward callback
+  makes the compute stream wait on the comm stream -- the host never blocks on a
+  collective and torch.distributed is only the rendezvous (the unique id travels over it);
+  ``comm=False`` keeps ``torch.distributed`` collectives instead (CPU / gloo always do);
 * bucket sizing for xGMI: every MI355X has 7 point-to-point links of ~153 GB/s.
   A ring all-reduce moves 2(W-1)/W * M bytes per GPU; RCCL spreads rings over
   all links, so ~25-64 MB buckets are bandwidth-efficient while still starting
@@ -51,7 +57,10 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_parameters: bool = True,
                  mode: str = "overlap", flat: Optional[FlatParams] = None,
-                 comm_dtype: Optional[torch.dtype] = None, timing: bool = False):
+                 comm_dtype: Optional[torch.dtype] = None, timing: bool = False, comm=None):
+        """``comm``: None = native RCCL communicator when the group is RCCL with W > 1 (else
+        torch.distributed); False = always torch.distributed; a ``_C.Communicator`` = use that
+        one (also at world size 1: the single-GPU rehearsal of the native collective path)."""
         super().__init__()
         if mode not in ("overlap", "manual"):
             raise ValueError("mode must be 'overlap' or 'manual'")
@@ -61,6 +70,14 @@ class DistributedDataParallel(nn.Module):
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self.flat = flat if flat is not None else FlatParams(module.parameters(), reverse=True)
+        self._ncomm = None
+        if comm is not None and comm is not False:
+            self._ncomm = comm
+            self.world_size = int(comm.size)
+        elif comm is None and self.flat.device.type == "cuda" and self.world_size > 1:
+            from ml_trainer_amd.parallel.comm import create_native_comm
+            self._ncomm = create_native_comm(process_group, self.flat.device)
+        self.comm_backend = "native-rccl" if self._ncomm is not None else f"torch.distributed-{self.backend}"
         self._bucket_cap = int((bucket_cap_mb or DEFAULT_BUCKET_MB) * 2 ** 20)
         self._first_cap = int((first_bucket_mb or DEFAULT_FIRST_BUCKET_MB) * 2 ** 20)
         self._build_buckets()
@@ -71,9 +88,11 @@ class DistributedDataParallel(nn.Module):
                       if self.comm_dtype is not None else None)
         self.timing = bool(timing)
         cuda = self.flat.device.type == "cuda"
-        # collectives that need work of their own (casts, timing events) run on a side stream
+        # native collectives, and collectives that need work of their own (casts, timing events),
+        # run on a dedicated high-priority comm stream
         self._comm_stream = (torch.cuda.Stream(device=self.flat.device, priority=-1)
-                             if cuda and (self.timing or self.comm_dtype is not None) else None)
+                             if cuda and (self._ncomm is not None or self.timing or self.comm_dtype is not None)
+                             else None)
         self._step_rec: Optional[Dict] = None
         self._records: List[Dict] = []
         self.require_sync = True
@@ -163,11 +182,14 @@ class DistributedDataParallel(nn.Module):
             if self._cbuf is not None:
                 buf = self._cbuf[s:e]
                 buf.copy_(view)
-            op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
-            w = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
-            w.wait()  # comm stream waits for the collective (no host block on RCCL)
-            if self.backend != "nccl":
-                buf.mul_(1.0 / self.world_size)
+            if self._ncomm is not None:
+                self._ncomm.all_reduce(buf, "avg")  # enqueued on the comm stream by C++
+            else:
+                op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+                w = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
+                w.wait()  # comm stream waits for the collective (no host block on RCCL)
+                if self.backend != "nccl":
+                    buf.mul_(1.0 / self.world_size)
             if buf is not view:
                 view.copy_(buf)
             if rec is not None:
@@ -178,7 +200,7 @@ class DistributedDataParallel(nn.Module):
 
     def _make_hook(self, i: int):
         def hook(p):
-            if not self.require_sync or self.world_size == 1:
+            if not self.require_sync or (self.world_size == 1 and self._ncomm is None):
                 return
             # A fused backward that wrote p's gradient straight into the flat buffer notifies here
             # (FlatParams.notify_grad_ready) AND autograd still runs p's AccumulateGrad node, whose
@@ -241,7 +263,8 @@ class DistributedDataParallel(nn.Module):
         ``exposed_ms`` comm time after backward compute ended (what the step waits for),
         ``overlap_pct`` share of the collective time hidden under forward/backward,
         ``fwd_bwd_ms`` forward start -> backward compute end, plus the bucket layout."""
-        out = {"buckets": len(self._buckets), "bucket_mb": [round(b / 2 ** 20, 3) for b in self.bucket_sizes_bytes],
+        out = {"comm": self.comm_backend, "buckets": len(self._buckets),
+               "bucket_mb": [round(b / 2 ** 20, 3) for b in self.bucket_sizes_bytes],
                "comm_dtype": str(self.comm_dtype or self.flat.grad.dtype).replace("torch.", ""),
                "steps_timed": 0}
         recs = [r for r in self._records if r.get("t0") is not None and r.get("bwd_end") is not None and r["buckets"]]
@@ -269,6 +292,9 @@ class DistributedDataParallel(nn.Module):
 
     def sync_gradients(self) -> None:
         """Manual mode (or after no_sync accumulation): all-reduce the whole flat gradient."""
+        if self._ncomm is not None:
+            self._ncomm.all_reduce(self.flat.grad, "avg")  # on the current stream
+            return
         if self.world_size == 1:
             return
         if self.backend == "nccl":

@@ -45,7 +45,9 @@ def local_rank() -> int:
 def bind_device(prefer_gpu: bool = True) -> torch.device:
     """Select the device for this process (LOCAL_RANK-th GPU) before anything touches it."""
     if prefer_gpu and torch.cuda.is_available():
-        lr = local_rank()
+        # MLT_SAME_DEVICE=1: every rank on GPU 0 -- the rehearsal knob for exercising the multi-rank
+        # paths on a one-GPU box (gloo group + MLT_XGMI_ALLOW_GLOO); never for real runs
+        lr = 0 if os.environ.get("MLT_SAME_DEVICE") == "1" else local_rank()
         n = torch.cuda.device_count()
         if lr >= n:
             raise RuntimeError(f"LOCAL_RANK={lr} but only {n} GPUs are visible")

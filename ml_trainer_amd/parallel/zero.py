@@ -92,6 +92,22 @@ class ShardView:
 
     def gather_into(self, out: torch.Tensor, shard: torch.Tensor, async_op: bool = False):
         """All-gather ``shard`` (this rank's chunks) into the full-layout tensor ``out``."""
+        nc = getattr(self, "ncomm", None)
+        if nc is not None and out.is_cuda:
+            # native RCCL all-gathers: on the comm stream (after a hipEvent edge from the
+            # compute stream) when asynchronous, else on the current stream
+            cs = self.comm_stream if async_op else None
+            if cs is not None:
+                ready = torch.cuda.Event()
+                ready.record()
+                with torch.cuda.stream(cs):
+                    cs.wait_event(ready)
+                    for s, e, so, c in self.chunks:
+                        nc.all_gather(shard[so:so + c], out[s:e])
+                return [_StreamDone(cs)]
+            for s, e, so, c in self.chunks:
+                nc.all_gather(shard[so:so + c], out[s:e])
+            return []
         if out.is_cuda and dist.get_backend(self.process_group) != "nccl":
             # gloo rehearsal of the GPU path (several ranks on one GPU): stage through the host
             host = out.cpu()
@@ -125,6 +141,16 @@ class _Done:
         pass
 
 
+class _StreamDone:
+    """``wait()`` makes the current (compute) stream wait for the comm stream -- no host block."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self) -> None:
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+
 class ZeroDataParallel(DistributedDataParallel):
     """DDP with ZeRO stage-1 optimizer sharding. Usage::
 
@@ -136,14 +162,16 @@ class ZeroDataParallel(DistributedDataParallel):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_parameters: bool = True,
-                 mode: str = "overlap"):
+                 mode: str = "overlap", comm=None):
         world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        if comm is not None and comm is not False:  # an explicit native communicator sets the layout
+            world, rank = int(comm.size), int(comm.rank)
         dev = next((p.device for p in module.parameters()), torch.device("cpu"))
         flat = FlatParams(module.parameters(), device=dev, reverse=True, align=16 * max(world, 1))
         super().__init__(module, process_group=process_group, bucket_cap_mb=bucket_cap_mb,
                          first_bucket_mb=first_bucket_mb, broadcast_parameters=broadcast_parameters,
-                         mode=mode, flat=flat)
+                         mode=mode, flat=flat, comm=comm)
         chunks, so = [], 0
         for s, e in self._buckets:
             assert (e - s) % world == 0, "bucket not divisible by the world size"
@@ -151,6 +179,8 @@ class ZeroDataParallel(DistributedDataParallel):
             chunks.append((s, e, so, c))
             so += c
         self.shard = ShardView(self.flat, chunks, rank, world, process_group)
+        self.shard.ncomm = self._ncomm
+        self.shard.comm_stream = self._comm_stream
         self._gather_works: List = []
 
     # ---- gradients: reduce-scatter instead of all-reduce ------------------------------------
@@ -158,6 +188,14 @@ class ZeroDataParallel(DistributedDataParallel):
         s, e, so, c = self.shard.chunks[bi]
         out = self.shard.grad[so:so + c]
         inp = self.flat.grad[s:e]
+        if self._ncomm is not None:  # native RCCL on the comm stream, after the bucket's producers
+            cs = self._comm_stream
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(cs):
+                cs.wait_event(ready)
+                self._ncomm.reduce_scatter(inp, out, "avg")
+            return None
         if self.backend == "nccl":
             return dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.AVG, group=self.process_group,
                                               async_op=async_op)
@@ -171,9 +209,11 @@ class ZeroDataParallel(DistributedDataParallel):
         return (w, out)
 
     def sync_gradients(self) -> None:
-        if self.world_size == 1:
+        if self.world_size == 1 and self._ncomm is None:
             return  # the shard aliases the full gradient
         self._works.extend(self._reduce_bucket(b) for b in range(len(self._buckets)))
+        if self._ncomm is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._comm_stream)
         self._wait_all()
 
     # ---- parameters: all-gather after the optimizer step --------------------------------------
@@ -186,7 +226,7 @@ class ZeroDataParallel(DistributedDataParallel):
 
     @torch.no_grad()
     def gather_parameters(self, async_op: bool = True) -> None:
-        if self.world_size > 1:
+        if self.world_size > 1 or self._ncomm is not None:
             self._gather_works.extend(self.shard.gather_into(self.flat.data, self.shard.data, async_op=async_op))
         self.flat.generation += 1
         if not async_op:

@@ -299,7 +299,8 @@ class Trainer:
         if self._engine is None:
             n_steps = len(self.train_loader)
             self._engine = LeNetStepEngine(self._core, self.flat, max_batch=self.batch_size,
-                                           world_size=self.world_size, seed=self.seed)
+                                           world_size=self.world_size, seed=self.seed,
+                                           precision=self.opts.precision)
             self._engine.set_optimizer(self.optimizer,
                                        lr_table_len=n_steps if self.scheduler_type == "CosineAnnealingWarmRestarts"
                                        else 0)
@@ -311,6 +312,10 @@ class Trainer:
                                      perm_capacity=n_idx)
             self._engine.ctrl[0:1].fill_(self.global_step)
             eng = self._engine
+            if mdist.is_dist():
+                # line the ranks up after each built its device dataset (the first in-graph
+                # collective of the step graphs then starts within a small skew on every rank)
+                dist.barrier()
             if self._watchdog is not None and eng.comm is not None and eng.dp_transport == "rccl":
                 self._watchdog.add_probe(eng.comm.async_error, eng.comm.abort)
             if self._watchdog is not None and eng.xgmi is not None and eng.dp_transport.startswith("xgmi"):

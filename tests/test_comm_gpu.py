@@ -145,6 +145,51 @@ def test_xgmi_late_peer_fails_within_one_step():
     assert r["sticky_raised"] and r["sticky_secs"] < 1.0, r
 
 
+def _partial_peer_worker(rank, world, port, out_dir, algo):
+    """Rank r withholds the flags of slices b % 4 == r (fault injection): on each rank half of the
+    blocks see their peers and reduce, the other half time out. The step must be applied NOWHERE --
+    neither on the slices that reduced nor on the ones that did not (all-or-nothing)."""
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    os.environ["MLT_XGMI_TIMEOUT_MS"] = "300"
+    from ml_trainer_amd.models.lenet_engine import TransportError
+    from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
+    eng, flat = _lenet_engine(dev)
+    xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
+    assert xe is not None
+    xe.algo = algo
+    eng.use_transport(xgmi=xe)
+    eng.train_steps(32, 2, use_graph=True, steps_per_graph=1)  # healthy steps
+    eng.check_transport()
+    dist.barrier()
+    before = flat.data.clone()
+    xe.fault = 1  # graphs are captured afresh below (use_transport clears them): the fault is live
+    eng.use_transport(xgmi=xe)
+    raised = False
+    try:
+        eng.train_steps(32, 1, use_graph=True, steps_per_graph=1)
+        eng.check_transport()
+    except TransportError:
+        raised = True
+    torch.cuda.synchronize()
+    torch.save({"raised": raised, "unchanged": bool(torch.equal(flat.data, before))},
+               os.path.join(out_dir, f"p{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_xgmi_partial_peer_step_all_or_nothing(algo):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_partial_peer_worker, args=(2, free_port(), d, algo), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"p{i}.pt"), weights_only=True) for i in range(2)]
+    for i in range(2):
+        assert r[i]["raised"], (i, r)
+        assert r[i]["unchanged"], (i, r)
+
+
 def _ddp_avg_worker(rank, world, port, out_dir):
     """Native DDP on the GPU must AVERAGE: the synced gradient equals the mean of the ranks'
     local gradients (no_sync backward of the same batch), not their sum."""
@@ -180,3 +225,39 @@ def test_ddp_gpu_averages_not_sums():
     assert not torch.equal(r[0]["local"], r[1]["local"])
     for i in range(2):
         torch.testing.assert_close(r[i]["synced"], mean, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("zero", [False, True])
+def test_ddp_native_comm_single_rank_bit_equal(dev, zero):
+    """BERT-tiny DDP (and ZeRO-1) with its buckets reduced by the native RCCL communicator (size-1
+    rehearsal of the W > 1 path: dedicated high-priority comm stream, hipEvent edges, AVG) gives
+    gradients / weights bit-equal to the same model without any communication."""
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops._ext import require_native
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    from ml_trainer_amd.parallel.zero import ZeroDataParallel
+    C = require_native()
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(5, 1000, (2, 128), generator=g).to(dev)
+    y = torch.randint(0, 2, (2,), generator=g).to(dev)
+    out = []
+    for native in (False, True):
+        torch.manual_seed(0)
+        m = BertClassifier(bert_config("bert-tiny")).to(dev)
+        comm = C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index) if native else False
+        cls = ZeroDataParallel if zero else DistributedDataParallel
+        ddp = cls(m, bucket_cap_mb=1.0, first_bucket_mb=0.5, comm=comm)
+        assert ddp.comm_backend == ("native-rccl" if native else "torch.distributed-none")
+        opt = ddp.make_optimizer(FusedAdamW, lr=1e-3) if zero else FusedAdamW(m.parameters(), lr=1e-3, flat=ddp.flat)
+        for _ in range(3):
+            opt.zero_grad(set_to_none=False)
+            F.cross_entropy(ddp(ids), y).backward()
+            opt.step()
+        if zero:
+            ddp.wait_parameters()
+        torch.cuda.synchronize()
+        out.append((ddp.flat.data.clone(), ddp.flat.grad.clone()))
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][0], out[1][0])
