@@ -1,0 +1,59 @@
+"""Per-phase timing of the bf16 per-sample LeNet kernel (lenet_mfma.hip, LENET_TRACE): block 0
+stores s_memtime stamps at every phase boundary (each stamp adds a barrier, so the sum runs a
+little over the untraced kernel). Usage: python benchmarks/lenet_bf16_phases.py [batch] [--jsonl F]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ml_trainer_amd.models.lenet import MLModel  # noqa: E402
+from ml_trainer_amd.models.lenet_engine import LeNetStepEngine  # noqa: E402
+from ml_trainer_amd.ops.optim import build_optimizer  # noqa: E402
+from ml_trainer_amd.utils.flat import FlatParams  # noqa: E402
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+B = int(args[0]) if args else 32
+out = sys.argv[sys.argv.index("--jsonl") + 1] if "--jsonl" in sys.argv else None
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+m = MLModel().to(dev)
+flat = FlatParams(m.parameters())
+opt = build_optimizer("sgd", m.parameters(), lr=1e-3, momentum=0.9, flat=flat)
+eng = LeNetStepEngine(m, flat, max_batch=B, optimizer=opt, precision="bf16")
+trace = torch.zeros(32, dtype=torch.float32, device=dev)
+eng.bufs["trace"] = trace
+eng.eng = eng.C.LeNetEngine(m.cfg_id, B, eng.bufs)  # rebuild with the trace buffer bound
+eng.eng.set_ctrl(eng.ctrl)
+eng.eng.set_precision(1)
+eng.set_optimizer(opt)
+N = 4096
+data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8)
+targets = torch.randint(0, 10, (N,))
+eng.set_dataset(data, targets, batch_size=B)
+eng.start_epoch(torch.randperm(N))
+eng.train_steps(B, 20, use_graph=False)
+C = eng.C
+names = ["P0 loads + P1 input/zero", "P2 conv1", "P3 conv2", "P4 fc fwd", "P5-9 CE + fc bwd", "P10 unpool",
+         "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad + slabs"]
+idx = [0, 1, 2, 3, 4, 5, 6, 7, 13]
+rows = []
+for rep in range(9):
+    eng.eng.run(C.LENET_FWD | C.LENET_CE | C.LENET_BWD | C.LENET_TRACE, B)
+    torch.cuda.synchronize()
+    rows.append(trace.view(torch.int64).cpu().tolist())
+st = rows[-1]
+cyc = st[13] - st[0]
+us = (st[15] - st[14]) / 100.0
+ghz = cyc / (us * 1e3) if us > 0 else float("nan")
+print(f"block 0 total: {cyc} cycles = {us:.2f} us ({ghz:.2f} GHz), batch {B}")
+rec = {"batch": B, "total_cycles": cyc, "total_us": us, "ghz": round(ghz, 3), "phases_us": {}}
+for k, n in enumerate(names):
+    d = sorted(r[idx[k + 1]] - r[idx[k]] for r in rows)
+    dm = d[len(d) // 2]
+    rec["phases_us"][n] = round(dm / ghz / 1e3, 3)
+    print(f"  {n:28s} {dm:8d} cycles  {dm / ghz / 1e3:7.2f} us")
+if out:
+    with open(out, "a") as f:
+        f.write(json.dumps(rec) + "\n")

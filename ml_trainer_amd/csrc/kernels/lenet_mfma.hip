@@ -12,7 +12,7 @@
 //       gradients over the batch, the fused optimizer update (fp32 masters + bf16 shadow), the
 //       fixed-order loss / accuracy sums, the step-counter advance.
 //
-// Why this shape (measured on the fp32 four-kernel step, profiles/lenet_pmc_r3_base.jsonl): every
+// Why this shape (measured on the fp32 four-kernel step, profiles/pmc/lenet_fp32_b{4,32}_r3.jsonl): every
 // kernel of that step sat 55-70 % of its wave cycles in s_waitcnt / barriers, and the step took
 // 30.5 us at batch 4 against 32.1 us at batch 32 -- it is a chain of latencies (kernel boundaries,
 // dependent global round trips, LDS-barrier phases), not of FLOPs. A CU per sample removes the
@@ -719,24 +719,33 @@ template <class D>
 __host__ __device__ constexpr int mw_conv_blocks() {
   return (D::S1 + D::S2 + kWgT - 1) / kWgT;
 }
+// fc weight gradients: a block holds kFcItems (row, 4-column) items x kFcQ batch quarters; each
+// thread sums its quarter of the batch (all its loads in flight at once: one round trip at batch
+// 32), the quarters are combined in a fixed order through LDS
+constexpr int kFcQ = 4, kFcItems = kWgT / kFcQ;
+template <int NCOLS>
+__host__ __device__ constexpr int fc_items(int nrows) {
+  return nrows * (NCOLS / 4);
+}
 template <class D>
 __host__ __device__ constexpr int mw_fc_blocks() {
-  return (D::F1 * (D::FLAT / 4) + kWgT - 1) / kWgT + (D::F2 * (D::F1 / 4) + kWgT - 1) / kWgT +
-         (D::NC * (D::F2 / 4) + kWgT - 1) / kWgT;
+  return (fc_items<D::FLAT>(D::F1) + kFcItems - 1) / kFcItems + (fc_items<D::F1>(D::F2) + kFcItems - 1) / kFcItems +
+         (fc_items<D::F2>(D::NC) + kFcItems - 1) / kFcItems;
 }
 
 template <int NCOLS>
 __device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float* __restrict__ dY,
                                          const float* __restrict__ X, const LeNetOpt& O, const Ctx& c,
-                                         uint16_t* shadow, int64_t offW, int64_t offb) {
+                                         uint16_t* shadow, int64_t offW, int64_t offb, float* red) {
   constexpr int NV = NCOLS / 4;
-  const int item = blk * kWgT + threadIdx.x;
-  if (item >= nrows * NV) return;
-  const int j = item / NV, v = item - j * NV;
-  const int64_t iw = offW + 4 * (int64_t)item, ib = offb + j;
+  const int t = threadIdx.x, q = t & (kFcQ - 1);
+  const int item = blk * kFcItems + (t >> 2);
+  const bool ok = item < nrows * NV;
+  const int it = ok ? item : 0, j = it / NV, v = it - j * NV;
+  const int64_t iw = offW + 4 * (int64_t)it, ib = offb + j;
   float4 pw = make_float4(0.f, 0.f, 0.f, 0.f), aw = pw, sw = pw;
   float pb = 0.f, ab = 0.f, sb = 0.f;
-  if (c.on) {  // optimizer state in flight together with the batch loads
+  if (c.on && q == 0 && ok) {  // optimizer state in flight together with the batch loads
     pw = *reinterpret_cast<const float4*>(O.p + iw);
     if (O.s1) aw = *reinterpret_cast<const float4*>(O.s1 + iw);
     if (O.s2) sw = *reinterpret_cast<const float4*>(O.s2 + iw);
@@ -749,25 +758,40 @@ __device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float*
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float bacc = 0.f;
   const float4* x4 = reinterpret_cast<const float4*>(X);
-#pragma unroll 2
-  for (int b0 = 0; b0 < B; b0 += 8) {
+  for (int b0 = 0; b0 < B; b0 += 8 * kFcQ) {  // this thread: samples b0 + 8q .. b0 + 8q + 7
     float d[8];
     float4 xv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int bb = min(b0 + u, B - 1);
+      const int bb = min(b0 + 8 * q + u, B - 1);
       d[u] = dY[(int64_t)bb * nrows + j];
       xv[u] = x4[(int64_t)bb * NV + v];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const float du = b0 + u < B ? d[u] : 0.f;
+      const float du = b0 + 8 * q + u < B ? d[u] : 0.f;
       acc.x = fmaf(du, xv[u].x, acc.x);
       acc.y = fmaf(du, xv[u].y, acc.y);
       acc.z = fmaf(du, xv[u].z, acc.z);
       acc.w = fmaf(du, xv[u].w, acc.w);
       bacc += du;
     }
+  }
+  float* r = red + 5 * t;
+  r[0] = acc.x;
+  r[1] = acc.y;
+  r[2] = acc.z;
+  r[3] = acc.w;
+  r[4] = bacc;
+  __syncthreads();
+  if (q != 0 || !ok) return;
+#pragma unroll
+  for (int k = 1; k < kFcQ; ++k) {  // fixed order: quarter 0 + 1 + 2 + 3
+    acc.x += r[5 * k];
+    acc.y += r[5 * k + 1];
+    acc.z += r[5 * k + 2];
+    acc.w += r[5 * k + 3];
+    bacc += r[5 * k + 4];
   }
   *reinterpret_cast<float4*>(O.g + iw) = acc;
   if (c.on) {
@@ -789,8 +813,9 @@ template <class D>
 __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
   constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
   constexpr int NBC = mw_conv_blocks<D>();
-  constexpr int NB3 = (F1 * (FLAT / 4) + kWgT - 1) / kWgT, NB4 = (F2 * (F1 / 4) + kWgT - 1) / kWgT,
-                NB5 = (NC * (F2 / 4) + kWgT - 1) / kWgT;
+  constexpr int NB3 = (fc_items<FLAT>(F1) + kFcItems - 1) / kFcItems,
+                NB4 = (fc_items<F1>(F2) + kFcItems - 1) / kFcItems, NB5 = (fc_items<F2>(NC) + kFcItems - 1) / kFcItems;
+  __shared__ float red[5 * kWgT];
   const int t = threadIdx.x;
   int blk = blockIdx.x;
   // the step's counters / lr as the per-sample kernel saw them (nothing here reads ctrl, which
@@ -855,14 +880,14 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
   }
   blk -= NBC;
   if (blk < NB3) {
-    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5]);
+    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], red);
   } else if ((blk -= NB3) < NB4) {
-    fc_wgrad<F1>(blk, F2, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7]);
+    fc_wgrad<F1>(blk, F2, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], red);
   } else if ((blk -= NB4) < NB5) {
-    fc_wgrad<F2>(blk, NC, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9]);
+    fc_wgrad<F2>(blk, NC, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9], red);
   } else {
     // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats
-    __shared__ double red[2][4];
+    double* red2 = reinterpret_cast<double*>(red);
     const int lane = t & 63, wid = t >> 6;
     double s0 = 0.0, s1 = 0.0;
     for (int i = t; i < B; i += kWgT) {
@@ -875,13 +900,13 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
       s1 += __shfl_xor(s1, o, 64);
     }
     if (lane == 0) {
-      red[0][wid] = s0;
-      red[1][wid] = s1;
+      red2[wid] = s0;
+      red2[4 + wid] = s1;
     }
     __syncthreads();
     if (t == 0) {
-      P.stats[0] += ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-      P.stats[1] += ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+      P.stats[0] += ((red2[0] + red2[1]) + red2[2]) + red2[3];
+      P.stats[1] += ((red2[4] + red2[5]) + red2[6]) + red2[7];
       if (ctrl) {  // advance the device step counters (next step / lr index / Adam t)
         ctrl[0] = step + 1;
         ctrl[1] = sie + 1;

@@ -55,8 +55,6 @@ class ShardView:
         else:
             self.data = torch.empty(self.numel, dtype=full.data.dtype, device=self.device)
             self.grad = torch.zeros(self.numel, dtype=full.grad.dtype, device=self.device)
-        self.shadow = None  # the replicated buffer's shadow is refreshed after the all-gather
-        self._shadow_ver = -1
         self.generation = 0
         self.grad_ready_hooks: List = []
         self.load_from_full()
@@ -73,8 +71,21 @@ class ShardView:
         if self.world > 1:
             self.grad.zero_()
 
+    # bf16 shadow: with world > 1 the replicated buffer's shadow is re-cast after the all-gather;
+    # with world 1 the shard IS the replicated buffer, so the fused optimizer rewrites its shadow
+    # directly (a native kernel does not bump data._version, so a lazily refreshed shadow would
+    # otherwise go stale)
+    @property
+    def shadow(self):
+        return self.full.shadow if self.world == 1 else None
+
+    @property
+    def _shadow_ver(self) -> int:
+        return self.full._shadow_ver if self.world == 1 else -1
+
     def mark_shadow_fresh(self) -> None:
-        pass
+        if self.world == 1:
+            self.full.mark_shadow_fresh()
 
     # ---- shard <-> full -------------------------------------------------------------------
     def local_slices(self):

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One-command scaling curve for an 8-GPU MI355X node (BASELINE.json metric: samples/sec/node +
+# step time, src/model.py default, DDP 1/2/4/8): bench.py at N = 1, 2, 4, 8 in both batch
+# semantics -- weak (32 per GPU) and the reference's (global batch 32 split over the ranks,
+# src/trainer.py:62-64) -- for the bf16 and the fp32 LeNet step, then the BERT-base DDP bucket
+# sweep. Every bench run appends its JSON line (plus the mode) to gpurun_out/scale_curve.jsonl;
+# efficiency = value(N) / (N * value(1)) is left to the reader / driver.
+#   usage: scripts/scale_curve.sh [STEPS=2000] [WARMUP=200]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+STEPS=${1:-2000}
+WARMUP=${2:-200}
+export TMPDIR=/tmp PYTHONUNBUFFERED=1 HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+out=gpurun_out/scale_curve.jsonl
+: > "$out"
+ngpu=$(python3 -c "import torch; print(torch.cuda.device_count())")
+for prec in bf16 fp32; do
+  for scaling in weak reference; do
+    for n in 1 2 4 8; do
+      if [ "$n" -gt "$ngpu" ]; then echo "=== skip N=$n ($ngpu GPUs visible)"; continue; fi
+      echo "=== LeNet $prec, $scaling, N=$n"
+      timeout -k 10 300 python3 -u bench.py --gpus "$n" --steps "$STEPS" --warmup "$WARMUP" --precision "$prec" \
+        --scaling "$scaling" --json-out gpurun_out/_scale_last.json > "gpurun_out/scale_${prec}_${scaling}_${n}.log" 2>&1
+      rc=$?
+      if [ "$rc" -ne 0 ]; then echo "=== stopping: rc=$rc (gpurun_out/scale_${prec}_${scaling}_${n}.log)"; exit "$rc"; fi
+      python3 -c "import json,sys; d=json.load(open('gpurun_out/_scale_last.json')); d['mode']='$scaling'; print(json.dumps(d))" >> "$out"
+      tail -n 1 "$out"
+    done
+  done
+done
+if [ "$ngpu" -ge 8 ]; then
+  bash scripts/bucket_sweep.sh 8 10 && cat gpurun_out/bucket_sweep.jsonl >> "$out"
+fi
+echo "=== $(wc -l < "$out") records in $out"
