@@ -22,7 +22,7 @@ m = MLModel().to(dev)
 flat = FlatParams(m.parameters())
 opt = build_optimizer("sgd", m.parameters(), lr=1e-3, momentum=0.9, flat=flat)
 eng = LeNetStepEngine(m, flat, max_batch=B, optimizer=opt, precision="bf16")
-trace = torch.zeros(32, dtype=torch.float32, device=dev)
+trace = torch.zeros(64, dtype=torch.float32, device=dev)
 eng.bufs["trace"] = trace
 eng.eng = eng.C.LeNetEngine(m.cfg_id, B, eng.bufs)  # rebuild with the trace buffer bound
 eng.eng.set_ctrl(eng.ctrl)
@@ -35,9 +35,12 @@ eng.set_dataset(data, targets, batch_size=B)
 eng.start_epoch(torch.randperm(N))
 eng.train_steps(B, 20, use_graph=False)
 C = eng.C
-names = ["P0 loads + P1 input/zero", "P2 conv1", "P3 conv2", "P4 fc fwd", "P5-9 CE + fc bwd", "P10 unpool",
-         "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad + slabs"]
-idx = [0, 1, 2, 3, 4, 5, 6, 7, 13]
+# stamp slots in kernel order (lenet_mfma.hip stamp(k)); a name per interval
+idx = [0, 16, 17, 1, 2, 3, 18, 19, 4, 20, 21, 22, 5, 6, 7, 13]
+names = ["P0 loads issued (+ctrl/meta scalar wait)", "P1 zero fill + raw image to LDS", "P1 augment -> xh/xc",
+         "P2 conv1", "P3 conv2", "P4 fc1 fwd (MFMA)", "P4 fc2 fwd", "P4 fc3 fwd", "P5 softmax-CE",
+         "P6 fc3 dgrad", "P7 fc2 dgrad", "P8 fc1 dgrad (MFMA)", "P10 unpool", "P11 conv2 dgrad/wgrad",
+         "P13 conv1 wgrad + slabs"]
 rows = []
 for rep in range(9):
     eng.eng.run(C.LENET_FWD | C.LENET_CE | C.LENET_BWD | C.LENET_TRACE, B)

@@ -993,7 +993,7 @@ class LeNetEngine {
       P_.wimg = reinterpret_cast<uint16_t*>(get("wimg", at::kShort, lenet_mfma_wimg_elems()).data_ptr<int16_t>());
       TORCH_CHECK(P_.slab1 != nullptr && (int64_t)C1 * 640 >= lenet_mfma_slab_floats(cfg), "slab1 too small");
     }
-    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 32).data_ptr<float>();
+    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 64).data_ptr<float>();
     A_ = LeNetAug{};
     O_ = LeNetOpt{};
   }

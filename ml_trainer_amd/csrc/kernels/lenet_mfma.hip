@@ -24,9 +24,9 @@
 //
 // GEMM formulations (v_mfma_f32_16x16x32_bf16; lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15],
 // C rows 4(l>>4)+r / column l&15):
-//   conv1 fwd   M = 196 pooled cells x 4 window positions (a lane's 4 accumulators ARE one 2x2
-//               pool window: pooling in registers), N = out channel, K = (kh, kw pair, c4) from the
-//               [Y][X][c4] bf16 image (two 8-byte reads per fragment)
+//   conv1 fwd   M = 196 pooled cells x 2 window rows, N = (out channel, window column), K = (kh, x
+//               pair, c4) from the [Y][X][c4] bf16 image (one 16-byte read per fragment); the 2x2
+//               pool is in registers (own rows + the partner lane's column, one DPP swap)
 //   conv2 fwd   M = 25 cells x 4, N = out channel, K = (tap, ic8) from the [y][x][ic8] p1 image
 //   conv2 dgrad M = 196 positions, N = in channel, K = (tap, oc16) from the zero-padded [18][18][oc16]
 //               image of the unpooled conv2-output gradient
@@ -81,13 +81,17 @@ __device__ __forceinline__ unsigned pack2(uint16_t lo, uint16_t hi) { return (un
 
 // conv weight B-fragment image (bf16, 12288 entries = 24 KB): [w1f 4 ksteps][w2f 7][w2d 13], each
 // [kstep][lane][8]. Slot of a parameter element (inverse of the fragment decode in lenet_ms):
-//   conv1 fwd   k = ((kh*3 + kw/2) * 2 + kw%2) * 4 + c, n = oc
+//   conv1 fwd   k = ((kh*3 + i) * 2 + p) * 4 + c, n = 2 oc + dx, with kw = 2 i + p - dx: every
+//               weight sits in two columns (output x parity dx = 0 / 1, the pool window's x)
 //   conv2 fwd   k = tap * 8 + ic,                       n = oc
 //   conv2 dgrad k = tap * 16 + oc,                      n = ic
 constexpr int kW1F = 0, kW2F = 4 * 512, kW2D = 11 * 512, kWimg = 24 * 512;
-__device__ __forceinline__ int w1f_slot(int oc, int c, int kh, int kw) {
-  const int qq = kh * 3 + (kw >> 1);
-  return kW1F + (((qq >> 2) * 64 + (qq & 3) * 16 + oc) << 3) + ((kw & 1) << 2) + c;
+// followed by fc1's weight TRANSPOSED ([in][out] bf16, the backward-data B operand: 16 contiguous
+// bytes per lane), sized for the largest config
+constexpr int kFc1T = kWimg, kWimgTot = kWimg + 400 * 120;
+__device__ __forceinline__ int w1f_slot(int oc, int c, int kh, int kw, int dx) {
+  const int u = kw + dx, qq = kh * 3 + (u >> 1);
+  return kW1F + (((qq >> 2) * 64 + (qq & 3) * 16 + 2 * oc + dx) << 3) + ((u & 1) << 2) + c;
 }
 __device__ __forceinline__ int w2f_slot(int oc, int ic, int tap) {
   return kW2F + (((tap >> 2) * 64 + (tap & 3) * 16 + oc) << 3) + ic;
@@ -100,9 +104,9 @@ template <int C1, int C2>
 __device__ __forceinline__ int64_t wimg_src(int e, int64_t off_w1, int64_t off_w2) {
   const int s = (e & 4095) >> 9;
   if (e < kW2F) {
-    const int l = (e >> 3) & 63, j = e & 7, oc = l & 15, qq = 4 * (e >> 9) + (l >> 4);
-    const int kh = qq / 3, kw = 2 * (qq - 3 * kh) + (j >> 2), c = j & 3;
-    return (qq < 15 && oc < C1 && kw < 5 && c < 3) ? off_w1 + ((oc * 3 + c) * 5 + kh) * 5 + kw : -1;
+    const int l = (e >> 3) & 63, j = e & 7, n = l & 15, qq = 4 * (e >> 9) + (l >> 4);
+    const int kh = qq / 3, oc = n >> 1, kw = 2 * (qq - 3 * kh) + (j >> 2) - (n & 1), c = j & 3;
+    return (qq < 15 && oc < C1 && kw >= 0 && kw < 5 && c < 3) ? off_w1 + ((oc * 3 + c) * 5 + kh) * 5 + kw : -1;
   }
   if (e < kW2D) {
     const int q = e - kW2F, l = (q >> 3) & 63, j = q & 7, oc = l & 15, tap = 4 * (q >> 9) + (l >> 4);
@@ -128,6 +132,13 @@ using DmTiny = Dm<4, 8, 64, 32, 10>;
 constexpr int kT = 1024;        // KS threads (16 waves)
 constexpr int XCS = 48;          // [c][Y][X] image row stride (X >= 32 zero: shifted 8-wide windows)
 constexpr int P1CS = 32;         // [ic][y][x] pooled-conv1 image row stride (x >= 14 zero)
+// LDS row strides chosen against bank conflicts of the MFMA operand reads (64 banks x 4 B; the
+// strides of the natural layouts map the rows a fragment gathers onto the same banks):
+constexpr int XHS = 48;          // [Y][X][c4] input image: pixels per row (conv1 A, 1.7-way vs 2.4 at 32)
+constexpr int P1HS = 24;         // [y][x][ic8] pooled conv1: pixels per row (conv2 A, 1.5-way vs 1.9)
+constexpr int DCHS = 22;         // [Y+4][X+4][oc16] padded conv2-output grad: pixels per row (dgrad A, 1-way)
+constexpr int DCCS = 24;         // [oc][Y][X] conv2-output grad: row stride (conv2 wgrad B, 1-way)
+constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel stride (conv1 wgrad B, 1-way vs 5)
 constexpr int kWgT = 256;        // KW threads
 
 // ---------------------------------------------------------------------------
@@ -210,7 +221,7 @@ struct BLinear {
   }
   // out[k] = mask(k) * sum_r d[r] W[r][k]; scratch >= SCRATCH floats. Ends with a barrier.
   __device__ __forceinline__ void bwd(const float* d, float* scratch, float* out_lds, float* __restrict__ out_g,
-                                      const float* mask) const {
+                                      const float* mask, uint16_t* out_b16 = nullptr) const {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gl = lane % G, grp = wid * R + lane / G;
     float dv[IT];
 #pragma unroll
@@ -240,33 +251,49 @@ struct BLinear {
       if (mask) sum = mask[k] > 0.f ? sum : 0.f;
       out_lds[k] = sum;
       out_g[k] = sum;
+      if (out_b16) out_b16[k] = f32_to_bf16(sum);
     }
     lbar();
   }
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+
+// fc1 (FLAT -> F1, 62 % of the model's weights) on the matrix cores, the sample's input row
+// broadcast over the 16 A rows. Forward: N tiles of 16 outputs x K steps of 32 inputs, K split
+// FS ways over the waves (fixed-order partial sum); backward-data: N tiles of 16 inputs x K
+// steps over the outputs, from the transposed bf16 image. B fragments live in registers.
+template <class D>
+struct Fc1 {
+  static constexpr int FNT = (D::F1 + 15) / 16, FKS = (D::FLAT + 31) / 32;
+  static constexpr int FS = cmax(1, cmin(16 / FNT, FKS)), FKP = (FKS + FS - 1) / FS;
+  static constexpr int BNT = (D::FLAT + 15) / 16, BKS = (D::F1 + 31) / 32, BTP = (BNT + 15) / 16;
+  static_assert(D::FLAT % 8 == 0 && D::F1 % 8 == 0 && D::F1 * D::FLAT <= 400 * 120, "fc1 fragments");
+};
 
 template <class D>
 struct KsLds {
-  using L1 = BLinear<D::FLAT, D::F1, kT>;
   using L2 = BLinear<D::F1, D::F2, kT>;
   using L3 = BLinear<D::F2, D::NC, kT>;
-  static constexpr int SCR = cmax(cmax(L1::SCRATCH, L2::SCRATCH), cmax(L3::SCRATCH, 3 * 5 * 256));
+  using F = Fc1<D>;
+  static constexpr int SCR = cmax(cmax(L2::SCRATCH, L3::SCRATCH), 3 * 5 * 256);
   // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
   // MFMA fragment reads
-  alignas(16) uint16_t p1h[196 * 8];                 // pooled conv1 [y][x][ic8]
+  alignas(16) uint16_t p1h[14 * P1HS * 8];           // pooled conv1 [y][x][ic8]
   alignas(16) uint16_t p1c[D::C1 * 14 * P1CS];       // pooled conv1 [ic][y][x]
-  alignas(16) uint16_t dch[18 * 18 * 16];            // unpooled conv2-out grad, padded [Y+4][X+4][oc16]
-  alignas(16) uint16_t dcc[16 * 10 * 16];            // unpooled conv2-out grad [oc16][Y][X16]
-  alignas(16) uint16_t d1[D::C1 * 28 * 32];          // unpooled conv1-out grad [oc][Y][X32]
+  alignas(16) uint16_t dch[18 * DCHS * 16];          // unpooled conv2-out grad, padded [Y+4][X+4][oc16]
+  alignas(16) uint16_t dcc[16 * 10 * DCCS];          // unpooled conv2-out grad [oc16][Y][X]
+  alignas(16) uint16_t d1[D::C1 * D1S];              // unpooled conv1-out grad [oc][Y][X32]
   // end of the zero span
-  alignas(16) uint16_t xh[32 * 32 * 4];              // input [Y][X][c4] (c = 3 zero)
+  alignas(16) uint16_t xh[32 * XHS * 4];             // input [Y][X][c4] (c = 3 zero; X >= 32 never read)
   alignas(16) uint16_t xc[3 * 32 * XCS];             // input [c][Y][X48] (X >= 32 zeroed separately)
   alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
   alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
   alignas(16) uint16_t w2d[13 * 64 * 8];             // conv2 dgrad B fragments
-  alignas(16) float f[D::FLAT];                      // flattened pooled conv2 (fc1 input)
+  alignas(16) uint16_t fb16[32 * F::FKS];           // flattened pooled conv2, bf16 (fc1 A row; tail zero)
+  alignas(16) uint16_t dh1b[32 * F::BKS];            // fc1 output gradient, bf16 (fc1 dgrad A row; tail zero)
+  alignas(16) float part[F::FS * F::FNT * 16];       // fc1 forward K-split partials
   alignas(16) float df[D::FLAT];                     // its gradient
   alignas(16) float sh1[D::F1];
   alignas(16) float sh2[D::F2];
@@ -296,11 +323,21 @@ __device__ __forceinline__ void aug_pixel(const uint8_t* img, int Y, int X, int 
   }
 }
 
+// h % span of the other kernels' hash (lenet.hip), exactly: the default RandomCrop padding 4 as a
+// constant divisor (multiply-high), anything else through two 32-bit remainders -- not the
+// generic 64-bit division (~250 instructions on the step's critical path)
+__device__ __forceinline__ int hmod(uint64_t h, unsigned span) {
+  if (span == 9u) return (int)(h % 9u);
+  const unsigned hi = (unsigned)(h >> 32) % span, lo = (unsigned)h % span;
+  const unsigned r32 = (0xffffffffu % span + 1u) % span;  // 2^32 mod span
+  return (int)((hi * r32 + lo) % span);                    // < span^2 + span: 32 bits (pad < 2^14)
+}
+
 __device__ __forceinline__ void aug_params(const LeNetAug& A, int64_t step, int64_t pos, int& ci, int& cj, bool& fl) {
   const uint64_t h = mix64(mix64(A.seed + (uint64_t)step) ^ (uint64_t)pos);
-  const int span = 2 * A.pad + 1;
-  ci = A.pad ? (int)(h % span) : 0;
-  cj = A.pad ? (int)((h >> 20) % span) : 0;
+  const unsigned span = 2 * A.pad + 1;
+  ci = A.pad ? hmod(h, span) : 0;
+  cj = A.pad ? hmod(h >> 20, span) : 0;
   fl = A.flip && ((h >> 40) & 1);
 }
 
@@ -329,7 +366,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   // so a role's pending loads never force waits on the other roles' code paths
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, g = lane >> 4, m = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  // LENET_TRACE: s_memtime stamps of block 0 per phase (P.trace[0..15]; 100 MHz wall stamps at 14, 15)
+  // LENET_TRACE: s_memtime stamps of block 0 per phase (P.trace: 32 8-byte slots; 100 MHz wall
+  // stamps at 14, 15; sub-phase stamps at 16..)
   auto stamp = [&](int k) {
     if (!(mode & LENET_TRACE)) return;
     lbar();
@@ -370,10 +408,19 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   const float b1v = P.b1[min(t, C1 - 1)], b2v = P.b2[min(t, C2 - 1)];
   constexpr int NFB = F1 + F2 + NC;
   const float fbv = t < F1 ? P.b3[t] : (t < F1 + F2 ? P.b4[min(t - F1, F2 - 1)] : P.b5[min(max(t - F1 - F2, 0), NC - 1)]);
-  typename S::L1 l1;
+  using F1M = typename S::F;
+  u32x4 f1w[F1M::FKP];  // fc1 forward B fragments (row-major W rows of the shadow: 16 B per lane)
+  {
+    const unsigned tn = w % F1M::FNT, sp = w / F1M::FNT, row = 16 * tn + m;
+#pragma unroll
+    for (int q = 0; q < F1M::FKP; ++q) {
+      const unsigned col = 32 * (sp * F1M::FKP + q) + 8 * g;
+      const bool ok = w < F1M::FNT * F1M::FS && row < (unsigned)F1 && col < (unsigned)FLAT;
+      f1w[q] = *reinterpret_cast<const u32x4*>(P.shadow + O.off[4] + (ok ? row * FLAT + col : 0u));
+    }
+  }
   typename S::L2 l2;
   typename S::L3 l3;
-  l1.load(P.shadow + O.off[4]);
   l2.load(P.shadow + O.off[6]);
   l3.load(P.shadow + O.off[8]);
   __builtin_amdgcn_sched_barrier(0);  // keep the index math below behind the load issue
@@ -406,6 +453,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   }
 
   // ---- P1: input images, zero spans, weight fragment images -----------------------------------
+  stamp(16);
   const bool hit = aug && mstep == step && mpos == pos;  // block-uniform
   int64_t tgt = 0;
   {
@@ -415,6 +463,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     uint4* z = reinterpret_cast<uint4*>(L.p1h);
     for (int e = t; e < ZB / 16; e += kT) z[e] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 3 * 32 * 2) reinterpret_cast<uint4*>(L.xc + (t >> 1) * XCS + 32)[t & 1] = make_uint4(0u, 0u, 0u, 0u);
+    if (t < 32 * S::F::FKS - FLAT) L.fb16[FLAT + t] = 0;
+    if (t < 32 * S::F::BKS - F1) L.dh1b[F1 + t] = 0;
     uint4* wl = reinterpret_cast<uint4*>(L.w1f);  // w1f | w2f | w2d are contiguous
     wl[t] = wi0;
     if (t < 512) wl[1024 + t] = wi1;
@@ -445,6 +495,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     bool fl;
     aug_params(A, step, pos, ci, cj, fl);
     lbar();
+    stamp(17);
     float v[3];
     aug_pixel(L.raw, Y0, X0, ci, cj, fl, A, v);
     px = make_uint2(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), 0));
@@ -452,7 +503,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     px = make_uint2(pack2(f32_to_bf16(xin[0]), f32_to_bf16(xin[1])), pack2(f32_to_bf16(xin[2]), 0));
     tgt = sload(P.targets + b);
   }
-  reinterpret_cast<uint2*>(L.xh)[t] = px;
+  reinterpret_cast<uint2*>(L.xh)[Y0 * XHS + X0] = px;
   L.xc[(0 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x & 0xffff);
   L.xc[(1 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x >> 16);
   L.xc[(2 * 32 + Y0) * XCS + X0] = (uint16_t)(px.y & 0xffff);
@@ -460,29 +511,41 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   stamp(1);
 
   // ---- P2: conv1 (MFMA) + bias + ReLU + maxpool in registers -> p1 images, i1 ------------------
+  // M = (pooled cell, window y) rows, N = (out channel, window x) columns, K = (kh, x pair, c4): a
+  // lane's accumulators are the window rows of two cells, the partner lane (n ^ 1) holds the other
+  // window column. 25 tiles x 4 k-steps; B fragments (4 x 16 B per lane) read once per wave.
   {
-    const uint16_t* xh = L.xh;
-    for (int T = w; T < 49; T += 16) {
-      const int cell = 4 * T + (m >> 2), q = m & 3;
-      const int py = cell / 14, pxx = cell - 14 * py, Y = 2 * py + (q >> 1), X = 2 * pxx + (q & 1);
+    u32x4 bw[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bw[s] = *reinterpret_cast<const u32x4*>(L.w1f + (s * 64 + lane) * 8);
+    const int a = m >> 2, r = m & 3, dx = m & 1, oc = m >> 1;
+    const float bias = L.b1s[min(oc, 15)];
+    for (int T = w; T < 25; T += 16) {
+      const int cell = min(8 * T + 2 * a + (r >> 1), 195);
+      const int py = cell / 14, pxx = cell - 14 * py, Y = 2 * py + (r & 1);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int qq = 4 * s + g, kh = qq / 3, kwp = qq - 3 * kh;
-        const int p = qq < 15 ? (Y + kh) * 32 + X + 2 * kwp : 0;
-        const uint2 lo = *reinterpret_cast<const uint2*>(xh + 4 * p), hi = *reinterpret_cast<const uint2*>(xh + 4 * p + 4);
-        u32x4 a = {lo.x, lo.y, hi.x, hi.y};
-        if (qq >= 15) a = u32x4{0u, 0u, 0u, 0u};
-        acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w1f + (s * 64 + lane) * 8), acc);
+        const int qq = 4 * s + g, kh = qq / 3, i = qq - 3 * kh;
+        u32x4 av = *reinterpret_cast<const u32x4*>(L.xh + ((qq < 15 ? (Y + kh) * XHS + 2 * pxx + 2 * i : 0)) * 4);
+        if (qq >= 15) av = u32x4{0u, 0u, 0u, 0u};
+        acc = mfma(av, bw[s], acc);
       }
-      const int cc = 4 * T + g, oc = m;
+      // rows 4g + r: cell 8T + 2g (r = 0, 1: window y) and 8T + 2g + 1 (r = 2, 3); column (oc, dx)
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[k]), 0xB1, 0xf, 0xf, false));  // lane ^ 1
+      // the dx = 0 lane pools the first cell, the dx = 1 lane the second; window order (y, x)
+      const f32x4 win = dx == 0 ? f32x4{acc[0], o[0], acc[1], o[1]} : f32x4{o[2], acc[2], o[3], acc[3]};
+      const int cc = 8 * T + 2 * g + dx;
       float pv;
       uint8_t code;
-      pool4(acc, L.b1s[oc], pv, code);
-      if (oc < C1) {
+      pool4(win, bias, pv, code);
+      if (oc < C1 && cc < 196) {
         const int cy = cc / 14, cx = cc - 14 * cy;
         const uint16_t hv = f32_to_bf16(pv);
-        L.p1h[cc * 8 + oc] = hv;
+        L.p1h[(cy * P1HS + cx) * 8 + oc] = hv;
         L.p1c[(oc * 14 + cy) * P1CS + cx] = hv;
         L.i1[oc * 196 + cc] = code;
       }
@@ -499,7 +562,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
       const int tap = 4 * s + g, kh = tap / 5, kw = tap - 5 * kh;
-      u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * 14 + x + kw : 0)) * 8);
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * P1HS + x + kw : 0)) * 8);
       if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
       acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2f + (s * 64 + lane) * 8), acc);
     }
@@ -509,7 +572,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     pool4(acc, L.b2s[oc], pv, code);
     if (cc < 25 && oc < C2) {
       const int o = oc * 25 + cc;
-      L.f[o] = pv;
+      L.fb16[o] = f32_to_bf16(pv);
       L.i2[o] = code;
       P.p2[(int64_t)b * FLAT + o] = pv;
     }
@@ -518,10 +581,48 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   stamp(3);
 
   // ---- P4-P9: fc1 -> fc2 -> fc3 -> softmax-CE -> fc dgrad chain -------------------------------
-  l1.template fwd<true>(L.f, L.fb, L.sh1, P.h1 + (int64_t)b * F1);
+  u32x4 f1t[F1M::BTP][F1M::BKS];  // fc1 backward-data B fragments, loaded once the forward ones are dead
+  {
+    const int tn = w % F1M::FNT, sp = w / F1M::FNT;
+    if (w < F1M::FNT * F1M::FS) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < F1M::FKP; ++q) {
+        const int ks = sp * F1M::FKP + q, col = 32 * ks + 8 * g;
+        if (ks < F1M::FKS) {
+          const u32x4 av = *reinterpret_cast<const u32x4*>(L.fb16 + min(col, 32 * F1M::FKS - 8));
+          const bool ok = 16 * tn + m < F1 && col < FLAT;
+          acc = mfma(av, ok ? f1w[q] : u32x4{0u, 0u, 0u, 0u}, acc);
+        }
+      }
+      if (g == 0) L.part[(sp * F1M::FNT + tn) * 16 + m] = acc[0];  // C row 0 (all rows are equal)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tp = 0; tp < F1M::BTP; ++tp) {
+      const unsigned c = 16 * (w + 16 * tp) + m;
+#pragma unroll
+      for (int ks = 0; ks < F1M::BKS; ++ks) {
+        const unsigned r0 = 32 * ks + 8 * g;
+        const bool ok = c < (unsigned)FLAT && r0 < (unsigned)F1;
+        f1t[tp][ks] = *reinterpret_cast<const u32x4*>(P.wimg + kFc1T + (ok ? c * F1 + r0 : 0u));
+      }
+    }
+  }
   lbar();
+  if (t < F1) {
+    float h = L.part[t];
+#pragma unroll
+    for (int sp = 1; sp < F1M::FS; ++sp) h += L.part[sp * F1M::FNT * 16 + t];
+    h = fmaxf(h + L.fb[t], 0.f);
+    L.sh1[t] = h;
+    P.h1[(int64_t)b * F1 + t] = h;
+  }
+  lbar();
+  stamp(18);
   l2.template fwd<true>(L.sh1, L.fb + F1, L.sh2, P.h2 + (int64_t)b * F2);
   lbar();
+  stamp(19);
   l3.template fwd<false>(L.sh2, L.fb + F1 + F2, L.slog, P.logits + (int64_t)b * NC);
   lbar();
   stamp(4);
@@ -547,9 +648,31 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     }
   }
   lbar();
+  stamp(20);
   l3.bwd(L.sdl, L.scr, L.sdh2, P.dh2 + (int64_t)b * F2, L.sh2);
-  l2.bwd(L.sdh2, L.scr, L.sdh1, P.dh1 + (int64_t)b * F1, L.sh1);
-  l1.bwd(L.sdh1, L.scr, L.df, P.dflat + (int64_t)b * FLAT, nullptr);
+  stamp(21);
+  l2.bwd(L.sdh2, L.scr, L.sdh1, P.dh1 + (int64_t)b * F1, L.sh1, L.dh1b);
+  stamp(22);
+  // (l2.bwd also wrote the bf16 copy dh1b: fc1's dgrad A row)
+#pragma unroll
+  for (int tp = 0; tp < F1M::BTP; ++tp) {
+    const int tile = w + 16 * tp;
+    if (tile < F1M::BNT) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < F1M::BKS; ++ks) {
+        const u32x4 av = *reinterpret_cast<const u32x4*>(L.dh1b + 32 * ks + 8 * g);
+        const bool ok = 16 * tile + m < FLAT && 32 * ks + 8 * g < F1;
+        acc = mfma(av, ok ? f1t[tp][ks] : u32x4{0u, 0u, 0u, 0u}, acc);
+      }
+      const int c = 16 * tile + m;
+      if (g == 0 && c < FLAT) {
+        L.df[c] = acc[0];
+        P.dflat[(int64_t)b * FLAT + c] = acc[0];
+      }
+    }
+  }
+  lbar();
   stamp(5);
 
   // ---- P10: unpool2 -> the conv2-output gradient images (zero except at arg-max cells) ---------
@@ -559,8 +682,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
       const int oc = e / 25, cell = e - 25 * oc, py = cell / 5, pxx = cell - 5 * py;
       const int Y = 2 * py + (code >> 1), X = 2 * pxx + (code & 1);
       const uint16_t v = f32_to_bf16(L.df[e]);
-      L.dch[((Y + 4) * 18 + X + 4) * 16 + oc] = v;
-      L.dcc[(oc * 10 + Y) * 16 + X] = v;
+      L.dch[((Y + 4) * DCHS + X + 4) * 16 + oc] = v;
+      L.dcc[(oc * 10 + Y) * DCCS + X] = v;
     }
   }
   if (stage_on) {  // wave 15 (no unpool work): publish the next step's raw image + tags
@@ -594,7 +717,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
     for (int s = 0; s < 13; ++s) {
       const int tap = 2 * s + (g >> 1), oc0 = 8 * (g & 1), kh = tap / 5, kw = tap - 5 * kh;
-      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((tap < 25 ? (Y - kh + 4) * 18 + X - kw + 4 : 0)) * 16 + oc0);
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((tap < 25 ? (Y - kh + 4) * DCHS + X - kw + 4 : 0)) * 16 + oc0);
       if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
       acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2d + (s * 64 + lane) * 8), acc);
     }
@@ -608,13 +731,14 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         if (P.g1) P.g1[((int64_t)b * C1 + ic) * 196 + pc] = gv;
         if (code < 4) {
           const int py = pc / 14, pxx = pc - 14 * py;
-          L.d1[(ic * 28 + 2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(gv);
+          L.d1[ic * D1S + (2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(gv);
         }
       }
     }
-  } else if (w < 15) {
-    // 10 M-tiles: tile tt = (kw, half); rows (ic, kh) = 16 * half + m; row 31 of tile 1 = ones (bias)
-    const int t0 = w == 13 ? 0 : 5, t1 = w == 13 ? 5 : 10;
+  } else {
+    // 10 M-tiles over waves 13-15 (4 / 3 / 3): tile tt = (kw, half); rows (ic, kh) = 16 * half + m;
+    // row 31 of tile 1 = ones (bias). Wave 15's staging stores were issued in P10.
+    const int t0 = w == 13 ? 0 : (w == 14 ? 4 : 7), t1 = w == 13 ? 4 : (w == 14 ? 7 : 10);
     for (int tt = t0; tt < t1; ++tt) {
       const int kw = tt >> 1, h = tt & 1, i = 16 * h + m, ic = i / 5, kh = i - 5 * ic;
       const bool valid = ic < C1, ones = tt == 1 && m == 15;
@@ -622,7 +746,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
       for (int s = 0; s < 5; ++s) {
         const int y = 2 * s + (g >> 1), x0 = 8 * (g & 1);
-        const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * 16 + x0);
+        const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * DCCS + x0);
         const uint16_t* rowp = L.p1c + ((valid ? ic : 0) * 14 + y + (valid ? kh : 0)) * P1CS + x0;
         const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp), hi = *reinterpret_cast<const u32x4*>(rowp + 8);
         u32x4 a;
@@ -655,7 +779,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     const bool valid = m < 15, ones = m == 15 && kw == 0;
     const int ya = 10 * kp, yb = min(ya + 10, 28), x0 = 8 * g;
     const uint16_t* xrow = L.xc + ((valid ? c : 0) * 32 + (valid ? kh : 0)) * XCS + x0;
-    const uint16_t* drow = L.d1 + (min(m, C1 - 1) * 28) * 32 + x0;
+    const uint16_t* drow = L.d1 + min(m, C1 - 1) * D1S + x0;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int Y = ya; Y < yb; ++Y) {
       u32x4 bq = *reinterpret_cast<const u32x4*>(drow + Y * 32);
@@ -736,7 +860,8 @@ __host__ __device__ constexpr int mw_fc_blocks() {
 template <int NCOLS>
 __device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float* __restrict__ dY,
                                          const float* __restrict__ X, const LeNetOpt& O, const Ctx& c,
-                                         uint16_t* shadow, int64_t offW, int64_t offb, float* red) {
+                                         uint16_t* shadow, int64_t offW, int64_t offb, float* red,
+                                         uint16_t* __restrict__ timg = nullptr) {
   constexpr int NV = NCOLS / 4;
   const int t = threadIdx.x, q = t & (kFcQ - 1);
   const int item = blk * kFcItems + (t >> 2);
@@ -802,9 +927,14 @@ __device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float*
     *reinterpret_cast<float4*>(O.p + iw) = pw;
     if (O.s1) *reinterpret_cast<float4*>(O.s1 + iw) = aw;
     if (O.s2) *reinterpret_cast<float4*>(O.s2 + iw) = sw;
-    if (shadow)
-      *reinterpret_cast<uint2*>(shadow + iw) =
-          make_uint2(pack2(f32_to_bf16(pw.x), f32_to_bf16(pw.y)), pack2(f32_to_bf16(pw.z), f32_to_bf16(pw.w)));
+    const uint16_t h0 = f32_to_bf16(pw.x), h1 = f32_to_bf16(pw.y), h2 = f32_to_bf16(pw.z), h3 = f32_to_bf16(pw.w);
+    if (shadow) *reinterpret_cast<uint2*>(shadow + iw) = make_uint2(pack2(h0, h1), pack2(h2, h3));
+    if (timg) {  // transposed bf16 image [in][out] (the per-sample kernel's fc1 dgrad operand)
+      timg[(4 * v + 0) * nrows + j] = h0;
+      timg[(4 * v + 1) * nrows + j] = h1;
+      timg[(4 * v + 2) * nrows + j] = h2;
+      timg[(4 * v + 3) * nrows + j] = h3;
+    }
   }
   if (v == 0) upd1(O, c, shadow, ib, bacc, pb, ab, sb);
 }
@@ -865,7 +995,11 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
       if (P.wimg) {  // the per-sample kernel's fragment image of the conv weights
         if (e < D::S1) {
           const int oc = e / 76, tap = e - 76 * oc;
-          if (tap < 75) P.wimg[w1f_slot(oc, tap / 25, (tap % 25) / 5, tap % 5)] = hb;
+          if (tap < 75) {
+            const int c = tap / 25, kh = (tap % 25) / 5, kw = tap % 5;
+            P.wimg[w1f_slot(oc, c, kh, kw, 0)] = hb;
+            P.wimg[w1f_slot(oc, c, kh, kw, 1)] = hb;
+          }
         } else {
           const int e2 = e - D::S1;
           if (e2 < C2 * C1 * 25) {
@@ -880,7 +1014,7 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
   }
   blk -= NBC;
   if (blk < NB3) {
-    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], red);
+    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], red, P.wimg ? P.wimg + kFc1T : nullptr);
   } else if ((blk -= NB3) < NB4) {
     fc_wgrad<F1>(blk, F2, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], red);
   } else if ((blk -= NB4) < NB5) {
@@ -919,20 +1053,24 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
 // every captured step sequence, and after each data-parallel optimizer launch)
 template <class D>
 __global__ __launch_bounds__(256) void lenet_mpack(const float* __restrict__ p, int64_t n, uint16_t* __restrict__ shadow,
-                                                  uint16_t* __restrict__ wimg, int64_t off_w1, int64_t off_w2) {
+                                                  uint16_t* __restrict__ wimg, int64_t off_w1, int64_t off_w2,
+                                                  int64_t off_w3) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) shadow[i] = f32_to_bf16(p[i]);
   if (i < kWimg) {
     const int64_t src = wimg_src<D::C1, D::C2>((int)i, off_w1, off_w2);
     wimg[i] = src >= 0 ? f32_to_bf16(p[src]) : (uint16_t)0;
+  } else if (i < kWimgTot) {  // fc1 transposed: [c][r] = W3[r][c]
+    const int e = (int)(i - kFc1T), cc = e / D::F1, r = e - cc * D::F1;
+    wimg[i] = cc < D::FLAT ? f32_to_bf16(p[off_w3 + (int64_t)r * D::FLAT + cc]) : (uint16_t)0;
   }
 }
 
 template <class D>
 void pack(const LeNetPtrs& P, const LeNetOpt& O, hipStream_t st) {
-  const int64_t tot = O.n > kWimg ? O.n : kWimg;
+  const int64_t tot = O.n > kWimgTot ? O.n : kWimgTot;
   hipLaunchKernelGGL(lenet_mpack<D>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, O.p, O.n, P.shadow, P.wimg,
-                     O.off[0], O.off[2]);
+                     O.off[0], O.off[2], O.off[4]);
 }
 
 template <class D>
@@ -946,7 +1084,7 @@ void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt&
 }  // namespace lm
 
 int lenet_mfma_slab_floats(int cfg) { return cfg == LENET_TINY ? lm::DmTiny::SLABN : lm::DmDefault::SLABN; }
-int lenet_mfma_wimg_elems() { return lm::kWimg; }
+int lenet_mfma_wimg_elems() { return lm::kWimgTot; }
 
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream) {
   if (cfg == LENET_TINY)
