@@ -79,13 +79,14 @@ __device__ __forceinline__ T sload(const T* p) {
 
 __device__ __forceinline__ unsigned pack2(uint16_t lo, uint16_t hi) { return (unsigned)lo | ((unsigned)hi << 16); }
 
-// conv weight B-fragment image (bf16, 12288 entries = 24 KB): [w1f 4 ksteps][w2f 7][w2d 13], each
+// conv weight B-fragment image (bf16, 13312 entries = 26 KB): [w1f 4 ksteps][w2f 7][w2d 15], each
 // [kstep][lane][8]. Slot of a parameter element (inverse of the fragment decode in lenet_ms):
 //   conv1 fwd   k = ((kh*3 + i) * 2 + p) * 4 + c, n = 2 oc + dx, with kw = 2 i + p - dx: every
 //               weight sits in two columns (output x parity dx = 0 / 1, the pool window's x)
 //   conv2 fwd   k = tap * 8 + ic,                       n = oc
-//   conv2 dgrad k = tap * 16 + oc,                      n = ic
-constexpr int kW1F = 0, kW2F = 4 * 512, kW2D = 11 * 512, kWimg = 24 * 512;
+//   conv2 dgrad k = ((kh*6 + u) * 16 + oc, n = 2 ic + dx, with kw = u - 1 + dx (two columns per
+//               weight, as conv1: the dgrad output's x parity dx is in N)
+constexpr int kW1F = 0, kW2F = 4 * 512, kW2D = 11 * 512, kWimg = 26 * 512;
 // followed by fc1's weight TRANSPOSED ([in][out] bf16, the backward-data B operand: 16 contiguous
 // bytes per lane), sized for the largest config
 constexpr int kFc1T = kWimg, kWimgTot = kWimg + 400 * 120;
@@ -96,8 +97,9 @@ __device__ __forceinline__ int w1f_slot(int oc, int c, int kh, int kw, int dx) {
 __device__ __forceinline__ int w2f_slot(int oc, int ic, int tap) {
   return kW2F + (((tap >> 2) * 64 + (tap & 3) * 16 + oc) << 3) + ic;
 }
-__device__ __forceinline__ int w2d_slot(int oc, int ic, int tap) {
-  return kW2D + (((tap >> 1) * 64 + ((((tap & 1) << 1) | (oc >> 3)) * 16) + ic) << 3) + (oc & 7);
+__device__ __forceinline__ int w2d_slot(int oc, int ic, int tap, int dx) {
+  const int kh = tap / 5, u = tap - 5 * kh + 1 - dx, pp = kh * 6 + u;
+  return kW2D + (((pp >> 1) * 64 + ((((pp & 1) << 1) | (oc >> 3)) * 16) + 2 * ic + dx) << 3) + (oc & 7);
 }
 // parameter element behind image entry e (or -1: padding), given the flat offsets of w1 / w2
 template <int C1, int C2>
@@ -112,10 +114,11 @@ __device__ __forceinline__ int64_t wimg_src(int e, int64_t off_w1, int64_t off_w
     const int q = e - kW2F, l = (q >> 3) & 63, j = q & 7, oc = l & 15, tap = 4 * (q >> 9) + (l >> 4);
     return (tap < 25 && oc < C2 && j < C1) ? off_w2 + (oc * C1 + j) * 25 + tap : -1;
   }
-  const int q = e - kW2D, l = (q >> 3) & 63, j = q & 7, ic = l & 15, gg = l >> 4;
-  const int tap = 2 * (q >> 9) + (gg >> 1), oc = 8 * (gg & 1) + j;
+  const int q = e - kW2D, l = (q >> 3) & 63, j = q & 7, n = l & 15, gg = l >> 4;
+  const int pp = 2 * (q >> 9) + (gg >> 1), oc = 8 * (gg & 1) + j, ic = n >> 1, kh = pp / 6;
+  const int kw = pp - 6 * kh - 1 + (n & 1);
   (void)s;
-  return (tap < 25 && ic < C1 && oc < C2) ? off_w2 + (oc * C1 + ic) * 25 + tap : -1;
+  return (pp < 30 && ic < C1 && oc < C2 && kw >= 0 && kw < 5) ? off_w2 + (oc * C1 + ic) * 25 + kh * 5 + kw : -1;
 }
 
 template <int C1_, int C2_, int F1_, int F2_, int NC_>
@@ -136,7 +139,7 @@ constexpr int P1CS = 32;         // [ic][y][x] pooled-conv1 image row stride (x 
 // strides of the natural layouts map the rows a fragment gathers onto the same banks):
 constexpr int XHS = 48;          // [Y][X][c4] input image: pixels per row (conv1 A, 1.7-way vs 2.4 at 32)
 constexpr int P1HS = 24;         // [y][x][ic8] pooled conv1: pixels per row (conv2 A, 1.5-way vs 1.9)
-constexpr int DCHS = 22;         // [Y+4][X+4][oc16] padded conv2-output grad: pixels per row (dgrad A, 1-way)
+constexpr int DCHS = 19;         // [Y+4][X+4][oc16] padded conv2-output grad: pixels per row (dgrad A, 1-way)
 constexpr int DCCS = 24;         // [oc][Y][X] conv2-output grad: row stride (conv2 wgrad B, 1-way)
 constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel stride (conv1 wgrad B, 1-way vs 5)
 constexpr int kWgT = 256;        // KW threads
@@ -215,7 +218,7 @@ struct BLinear {
         float o = acc + bias[r];
         if (RELU) o = fmaxf(o, 0.f);
         out_lds[r] = o;
-        out_g[r] = o;
+        if (out_g) out_g[r] = o;
       }
     }
   }
@@ -250,7 +253,7 @@ struct BLinear {
       for (int g = 0; g < RPI; ++g) sum += scratch[g * NCOLS + k];
       if (mask) sum = mask[k] > 0.f ? sum : 0.f;
       out_lds[k] = sum;
-      out_g[k] = sum;
+      if (out_g) out_g[k] = sum;
       if (out_b16) out_b16[k] = f32_to_bf16(sum);
     }
     lbar();
@@ -261,15 +264,18 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
 // fc1 (FLAT -> F1, 62 % of the model's weights) on the matrix cores, the sample's input row
-// broadcast over the 16 A rows. Forward: N tiles of 16 outputs x K steps of 32 inputs, K split
-// FS ways over the waves (fixed-order partial sum); backward-data: N tiles of 16 inputs x K
-// steps over the outputs, from the transposed bf16 image. B fragments live in registers.
+// broadcast over the 16 A rows. Forward: FNT tiles of 16 outputs, one per wave of the LAST FNT
+// waves, all K steps of 32 inputs in that wave; backward-data: BNT tiles of 16 inputs over waves
+// 1-15 (wave 0 runs the softmax-CE meanwhile), K steps over the outputs, from the transposed bf16
+// image. B fragments live in registers; their ~100 KB per direction are fetched where the
+// issuing waves are otherwise idle or light (the vector memory path of a CU moves them at
+// ~35 B/clk and a wave stalls while its loads queue): forward at P2 (waves 8-15 carry one conv1
+// tile, the others two), backward during the softmax-CE.
 template <class D>
 struct Fc1 {
-  static constexpr int FNT = (D::F1 + 15) / 16, FKS = (D::FLAT + 31) / 32;
-  static constexpr int FS = cmax(1, cmin(16 / FNT, FKS)), FKP = (FKS + FS - 1) / FS;
-  static constexpr int BNT = (D::FLAT + 15) / 16, BKS = (D::F1 + 31) / 32, BTP = (BNT + 15) / 16;
-  static_assert(D::FLAT % 8 == 0 && D::F1 % 8 == 0 && D::F1 * D::FLAT <= 400 * 120, "fc1 fragments");
+  static constexpr int FNT = (D::F1 + 15) / 16, FKS = (D::FLAT + 31) / 32, FW0 = 16 - FNT;
+  static constexpr int BNT = (D::FLAT + 15) / 16, BKS = (D::F1 + 31) / 32, BTP = (BNT + 14) / 15;
+  static_assert(D::FLAT % 8 == 0 && D::F1 % 8 == 0 && D::F1 * D::FLAT <= 400 * 120 && FNT <= 16, "fc1 fragments");
 };
 
 template <class D>
@@ -290,10 +296,9 @@ struct KsLds {
   alignas(16) uint16_t xc[3 * 32 * XCS];             // input [c][Y][X48] (X >= 32 zeroed separately)
   alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
   alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
-  alignas(16) uint16_t w2d[13 * 64 * 8];             // conv2 dgrad B fragments
+  alignas(16) uint16_t w2d[15 * 64 * 8];             // conv2 dgrad B fragments
   alignas(16) uint16_t fb16[32 * F::FKS];           // flattened pooled conv2, bf16 (fc1 A row; tail zero)
   alignas(16) uint16_t dh1b[32 * F::BKS];            // fc1 output gradient, bf16 (fc1 dgrad A row; tail zero)
-  alignas(16) float part[F::FS * F::FNT * 16];       // fc1 forward K-split partials
   alignas(16) float df[D::FLAT];                     // its gradient
   alignas(16) float sh1[D::F1];
   alignas(16) float sh2[D::F2];
@@ -302,6 +307,9 @@ struct KsLds {
   alignas(16) float slog[64];
   alignas(16) float sdl[64];
   alignas(16) float scr[SCR];                        // fc bwd row-group partials / conv1 wgrad partials
+  alignas(16) float f32[D::FLAT];                    // flattened pooled conv2, fp32 (stored for the fc1 wgrad)
+  unsigned long long tr[32];                         // LENET_TRACE stamps
+  double ce[2];                                      // this sample's (loss / B, hit / B)
   alignas(16) uint8_t raw[3072];                     // this step's raw image (staged or gathered)
   float b1s[16], b2s[16];
   alignas(16) float fb[D::F1 + D::F2 + D::NC];       // fc biases
@@ -368,6 +376,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   // LENET_TRACE: s_memtime stamps of block 0 per phase (P.trace: 32 8-byte slots; 100 MHz wall
   // stamps at 14, 15; sub-phase stamps at 16..)
+  // (kept in LDS and stored at the end: a global store mid-kernel would make later vmcnt waits
+  // wait for its completion too)
   auto stamp = [&](int k) {
     if (!(mode & LENET_TRACE)) return;
     lbar();
@@ -375,10 +385,10 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     unsigned long long c, wc;
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c), "=s"(wc)::"memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (b == 0 && t == 0 && P.trace) {
-      reinterpret_cast<unsigned long long*>(P.trace)[k] = c;
-      if (k == 0) reinterpret_cast<unsigned long long*>(P.trace)[14] = wc;
-      if (k == 13) reinterpret_cast<unsigned long long*>(P.trace)[15] = wc;
+    if (t == 0) {
+      L.tr[k] = c;
+      if (k == 0) L.tr[14] = wc;
+      if (k == 13) L.tr[15] = wc;
     }
   };
   stamp(0);
@@ -390,12 +400,14 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   const int64_t step = sload(A.ctrl), sie = sload(A.ctrl + 1);
   const int64_t mstep = sload(P.meta2 + 4 * b), mpos = sload(P.meta2 + 4 * b + 1), mtgt = sload(P.meta2 + 4 * b + 3);
   uint4 sraw = reinterpret_cast<const uint4*>(P.stage2 + (int64_t)b * 3072)[min(t, 191)];
-  const bool stage_on = aug && w == 15;  // next-step staging wave (see below)
-  int64_t sN = -1, pN = -1, iN = -1;
+  const bool stage_on = aug && w == 15;  // next-step staging wave (see P2)
+  // (vector loads, issued before the bulk: scalar ones would be waited for by every LDS barrier's
+  // lgkmcnt(0), and the staging decision they feed is taken in P2, off the critical path)
+  longlong2 mN01 = make_longlong2(-1, -1);
+  long long mN2 = -1;
   if (stage_on) {
-    sN = sload(P.metaN + 4 * b);
-    pN = sload(P.metaN + 4 * b + 1);
-    iN = sload(P.metaN + 4 * b + 2);
+    mN01 = *reinterpret_cast<const longlong2*>(P.metaN + 4 * b);
+    mN2 = P.metaN[4 * b + 2];
   }
   float xin[3] = {0.f, 0.f, 0.f};
   if (!aug) {
@@ -404,53 +416,31 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   }
   // conv weight B-fragment images (bf16, packed by the optimizer / lenet_mpack): 24 KB, linear
   const uint4* wimg4 = reinterpret_cast<const uint4*>(P.wimg);
-  const uint4 wi0 = wimg4[t], wi1 = wimg4[1024 + min(t, 511)];
+  constexpr int WI1 = kWimg / 8 - 1024;  // uint4s of the image past the first 1024
+  const uint4 wi0 = wimg4[t], wi1 = wimg4[1024 + min(t, WI1 - 1)];
   const float b1v = P.b1[min(t, C1 - 1)], b2v = P.b2[min(t, C2 - 1)];
   constexpr int NFB = F1 + F2 + NC;
   const float fbv = t < F1 ? P.b3[t] : (t < F1 + F2 ? P.b4[min(t - F1, F2 - 1)] : P.b5[min(max(t - F1 - F2, 0), NC - 1)]);
   using F1M = typename S::F;
-  u32x4 f1w[F1M::FKP];  // fc1 forward B fragments (row-major W rows of the shadow: 16 B per lane)
-  {
-    const unsigned tn = w % F1M::FNT, sp = w / F1M::FNT, row = 16 * tn + m;
-#pragma unroll
-    for (int q = 0; q < F1M::FKP; ++q) {
-      const unsigned col = 32 * (sp * F1M::FKP + q) + 8 * g;
-      const bool ok = w < F1M::FNT * F1M::FS && row < (unsigned)F1 && col < (unsigned)FLAT;
-      f1w[q] = *reinterpret_cast<const u32x4*>(P.shadow + O.off[4] + (ok ? row * FLAT + col : 0u));
-    }
-  }
+  u32x4 f1w[F1M::FKS];  // fc1 forward B fragments (row-major W rows of the shadow: 16 B per lane)
   typename S::L2 l2;
   typename S::L3 l3;
-  l2.load(P.shadow + O.off[6]);
-  l3.load(P.shadow + O.off[8]);
+  // fc weights: issued once this step's image and conv fragments are in LDS (fc1: start of P2; fc2 /
+  // fc3: start of P3, where conv1's registers are free), so that their transfer does not delay
+  // those. Padding lanes re-read a valid lane's line (coalesced).
+  auto load_fc = [&]() {
+    if (w >= F1M::FW0) {
+      const unsigned row = min(16u * (w - F1M::FW0) + m, (unsigned)F1 - 1);
+#pragma unroll
+      for (int q = 0; q < F1M::FKS; ++q) {
+        const unsigned col = min(32u * q + 8 * g, (unsigned)FLAT - 8);
+        f1w[q] = *reinterpret_cast<const u32x4*>(P.shadow + O.off[4] + row * FLAT + col);
+      }
+    }
+  };
   __builtin_amdgcn_sched_barrier(0);  // keep the index math below behind the load issue
   int64_t pos = sie * A.batch_stride + b;
   if (aug && pos >= A.perm_len) pos %= A.perm_len;
-  // next-step staging (wave 15, two steps deep so that no load waits on another inside this kernel):
-  // metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1; when it
-  // matches, the raw image of step + 1 is gathered right away (stored to stage2 in P10). The perm
-  // entry for step + 2 is looked up here and published to metaN in P10. A mismatch (epoch start,
-  // new permutation, ...) stages nothing: the next step then gathers its images itself.
-  int64_t pos1 = 0, pos2 = 0, idx1 = 0, ntgt = 0;
-  int nperm2 = 0;
-  bool st1 = false;
-  uint4 nraw0 = make_uint4(0u, 0u, 0u, 0u), nraw1 = nraw0, nraw2 = nraw0;
-  if (stage_on) {
-    pos1 = (sie + 1) * A.batch_stride + b;
-    if (pos1 >= A.perm_len) pos1 %= A.perm_len;
-    pos2 = (sie + 2) * A.batch_stride + b;
-    if (pos2 >= A.perm_len) pos2 %= A.perm_len;
-    nperm2 = sload(A.perm + pos2);
-    st1 = sN == step + 1 && pN == pos1 && iN >= 0 && iN < A.n;
-    if (st1) {
-      idx1 = iN;
-      const uint4* src = reinterpret_cast<const uint4*>(A.data + idx1 * 3072);
-      nraw0 = src[lane];
-      nraw1 = src[lane + 64];
-      nraw2 = src[lane + 128];
-      ntgt = sload(P.dtargets + idx1);
-    }
-  }
 
   // ---- P1: input images, zero spans, weight fragment images -----------------------------------
   stamp(16);
@@ -467,7 +457,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     if (t < 32 * S::F::BKS - F1) L.dh1b[F1 + t] = 0;
     uint4* wl = reinterpret_cast<uint4*>(L.w1f);  // w1f | w2f | w2d are contiguous
     wl[t] = wi0;
-    if (t < 512) wl[1024 + t] = wi1;
+    if (t < WI1) wl[1024 + t] = wi1;
     if (t < NFB) L.fb[t] = fbv;
     if (t < 16) {
       L.b1s[t] = t < C1 ? b1v : 0.f;
@@ -510,6 +500,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   lbar();
   stamp(1);
 
+  load_fc();
   // ---- P2: conv1 (MFMA) + bias + ReLU + maxpool in registers -> p1 images, i1 ------------------
   // M = (pooled cell, window y) rows, N = (out channel, window x) columns, K = (kh, x pair, c4): a
   // lane's accumulators are the window rows of two cells, the partner lane (n ^ 1) holds the other
@@ -554,6 +545,41 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   lbar();
   stamp(2);
 
+  l2.load(P.shadow + O.off[6]);
+  l3.load(P.shadow + O.off[8]);
+  // next-step staging (wave 15, two steps deep so that no load waits on another inside this kernel):
+  // metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1; when it
+  // matches, the raw image of step + 1 is gathered now (stored to stage2 in P10). The perm entry
+  // for step + 2 is looked up here and published to metaN in P10. A mismatch (epoch start, new
+  // permutation, ...) stages nothing: the next step then gathers its images itself. All vector
+  // loads, first waited for in P10.
+  int64_t pos1 = 0, pos2 = 0, idx1 = 0;
+  bool st1 = false;
+  int nperm2v = 0;
+  long long ntgtv = 0;
+  uint4 nraw0 = make_uint4(0u, 0u, 0u, 0u), nraw1 = nraw0, nraw2 = nraw0;
+  if (stage_on) {
+    pos1 = (sie + 1) * A.batch_stride + b;
+    if (pos1 >= A.perm_len) pos1 %= A.perm_len;
+    pos2 = (sie + 2) * A.batch_stride + b;
+    if (pos2 >= A.perm_len) pos2 %= A.perm_len;
+    nperm2v = A.perm[pos2];
+    auto rfl64 = [](long long v) {
+      return (int64_t)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)((uint64_t)v >> 32)) << 32) |
+                       (unsigned)__builtin_amdgcn_readfirstlane((int)v));
+    };
+    const int64_t sN = rfl64(mN01.x), pN = rfl64(mN01.y), iN = rfl64(mN2);
+    st1 = sN == step + 1 && pN == pos1 && iN >= 0 && iN < A.n;
+    if (st1) {
+      idx1 = iN;
+      const uint4* src = reinterpret_cast<const uint4*>(A.data + idx1 * 3072);
+      nraw0 = src[lane];
+      nraw1 = src[lane + 64];
+      nraw2 = src[lane + 128];
+      ntgtv = P.dtargets[idx1];
+    }
+  }
+
   // ---- P3: conv2 (MFMA) + bias + ReLU + maxpool -> f (flatten order oc*25 + cell), i2 ----------
   if (w < 7) {
     const int r = 16 * w + m, cell = min(r >> 2, 24), q = r & 3;
@@ -573,59 +599,47 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     if (cc < 25 && oc < C2) {
       const int o = oc * 25 + cc;
       L.fb16[o] = f32_to_bf16(pv);
+      L.f32[o] = pv;
       L.i2[o] = code;
-      P.p2[(int64_t)b * FLAT + o] = pv;
     }
   }
   lbar();
   stamp(3);
 
   // ---- P4-P9: fc1 -> fc2 -> fc3 -> softmax-CE -> fc dgrad chain -------------------------------
-  u32x4 f1t[F1M::BTP][F1M::BKS];  // fc1 backward-data B fragments, loaded once the forward ones are dead
-  {
-    const int tn = w % F1M::FNT, sp = w / F1M::FNT;
-    if (w < F1M::FNT * F1M::FS) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (w >= F1M::FW0) {
+    const int tn = w - F1M::FW0;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < F1M::FKP; ++q) {
-        const int ks = sp * F1M::FKP + q, col = 32 * ks + 8 * g;
-        if (ks < F1M::FKS) {
-          const u32x4 av = *reinterpret_cast<const u32x4*>(L.fb16 + min(col, 32 * F1M::FKS - 8));
-          const bool ok = 16 * tn + m < F1 && col < FLAT;
-          acc = mfma(av, ok ? f1w[q] : u32x4{0u, 0u, 0u, 0u}, acc);
-        }
-      }
-      if (g == 0) L.part[(sp * F1M::FNT + tn) * 16 + m] = acc[0];  // C row 0 (all rows are equal)
+    for (int q = 0; q < F1M::FKS; ++q) {
+      const int col = 32 * q + 8 * g;
+      const u32x4 av = *reinterpret_cast<const u32x4*>(L.fb16 + col);
+      const bool ok = 16 * tn + m < F1 && col < FLAT;
+      acc = mfma(av, ok ? f1w[q] : u32x4{0u, 0u, 0u, 0u}, acc);
     }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int tp = 0; tp < F1M::BTP; ++tp) {
-      const unsigned c = 16 * (w + 16 * tp) + m;
-#pragma unroll
-      for (int ks = 0; ks < F1M::BKS; ++ks) {
-        const unsigned r0 = 32 * ks + 8 * g;
-        const bool ok = c < (unsigned)FLAT && r0 < (unsigned)F1;
-        f1t[tp][ks] = *reinterpret_cast<const u32x4*>(P.wimg + kFc1T + (ok ? c * F1 + r0 : 0u));
-      }
-    }
-  }
-  lbar();
-  if (t < F1) {
-    float h = L.part[t];
-#pragma unroll
-    for (int sp = 1; sp < F1M::FS; ++sp) h += L.part[sp * F1M::FNT * 16 + t];
-    h = fmaxf(h + L.fb[t], 0.f);
-    L.sh1[t] = h;
-    P.h1[(int64_t)b * F1 + t] = h;
+    const int r = 16 * tn + m;
+    if (g == 0 && r < F1) L.sh1[r] = fmaxf(acc[0] + L.fb[r], 0.f);  // C row 0 (all rows are equal)
   }
   lbar();
   stamp(18);
-  l2.template fwd<true>(L.sh1, L.fb + F1, L.sh2, P.h2 + (int64_t)b * F2);
+  l2.template fwd<true>(L.sh1, L.fb + F1, L.sh2, nullptr);
   lbar();
   stamp(19);
-  l3.template fwd<false>(L.sh2, L.fb + F1 + F2, L.slog, P.logits + (int64_t)b * NC);
+  l3.template fwd<false>(L.sh2, L.fb + F1 + F2, L.slog, nullptr);
   lbar();
   stamp(4);
+  u32x4 f1t[F1M::BTP][F1M::BKS];  // fc1 backward-data B fragments (waves 1-15), fetched during the CE
+  if (w > 0) {
+#pragma unroll
+    for (int tp = 0; tp < F1M::BTP; ++tp) {
+      const unsigned c = min(16u * (w - 1 + 15 * tp) + m, (unsigned)FLAT - 1);
+#pragma unroll
+      for (int ks = 0; ks < F1M::BKS; ++ks) {
+        const unsigned r0 = min(32u * ks + 8 * g, (unsigned)F1 - 8);
+        f1t[tp][ks] = *reinterpret_cast<const u32x4*>(P.wimg + kFc1T + c * F1 + r0);
+      }
+    }
+  }
   if (w == 0) {
     constexpr int GC = pow2_ge(NC);
     const float z = lane < NC ? L.slog[lane] : -INFINITY;
@@ -640,24 +654,23 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     if (lane < NC) {
       const float dl = valid ? (e / s - (lane == tgt ? 1.f : 0.f)) * inv_B : 0.f;
       L.sdl[lane] = dl;
-      P.dlogits[(int64_t)b * NC + lane] = dl;
     }
-    if (lane == 0 && P.cestat) {
-      P.cestat[2 * b] = (double)loss * (double)inv_B;
-      P.cestat[2 * b + 1] = (am == tgt) ? (double)inv_B : 0.0;
+    if (lane == 0) {
+      L.ce[0] = (double)loss * (double)inv_B;
+      L.ce[1] = (am == tgt) ? (double)inv_B : 0.0;
     }
   }
   lbar();
   stamp(20);
-  l3.bwd(L.sdl, L.scr, L.sdh2, P.dh2 + (int64_t)b * F2, L.sh2);
+  l3.bwd(L.sdl, L.scr, L.sdh2, nullptr, L.sh2);
   stamp(21);
-  l2.bwd(L.sdh2, L.scr, L.sdh1, P.dh1 + (int64_t)b * F1, L.sh1, L.dh1b);
+  l2.bwd(L.sdh2, L.scr, L.sdh1, nullptr, L.sh1, L.dh1b);
   stamp(22);
   // (l2.bwd also wrote the bf16 copy dh1b: fc1's dgrad A row)
 #pragma unroll
   for (int tp = 0; tp < F1M::BTP; ++tp) {
-    const int tile = w + 16 * tp;
-    if (tile < F1M::BNT) {
+    const int tile = w - 1 + 15 * tp;
+    if (w > 0 && tile < F1M::BNT) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < F1M::BKS; ++ks) {
@@ -666,10 +679,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         acc = mfma(av, ok ? f1t[tp][ks] : u32x4{0u, 0u, 0u, 0u}, acc);
       }
       const int c = 16 * tile + m;
-      if (g == 0 && c < FLAT) {
-        L.df[c] = acc[0];
-        P.dflat[(int64_t)b * FLAT + c] = acc[0];
-      }
+      if (g == 0 && c < FLAT) L.df[c] = acc[0];
     }
   }
   lbar();
@@ -698,48 +708,50 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         P.meta2[4 * b] = step + 1;
         P.meta2[4 * b + 1] = pos1;
         P.meta2[4 * b + 2] = idx1;
-        P.meta2[4 * b + 3] = ntgt;
+        P.meta2[4 * b + 3] = ntgtv;
       }
       P.metaN[4 * b] = step + 2;
       P.metaN[4 * b + 1] = pos2;
-      P.metaN[4 * b + 2] = nperm2;
+      P.metaN[4 * b + 2] = nperm2v;
     }
   }
   lbar();
   stamp(6);
 
-  // ---- P11: conv2 dgrad (waves 0-12) -> liveness mask -> unpooled conv1 grad d1 ----------------
-  //           conv2 wgrad of the sample (waves 13-15) -> slab
+  // ---- P11: conv2 dgrad (waves 0-6) -> liveness mask -> unpooled conv1 grad d1 -----------------
+  //           conv2 wgrad of the sample (waves 7-15) -> slab
+  // dgrad: M = 98 (y, x pair) positions (column-major: conflict-free A reads at DCHS = 19), N =
+  // (in channel, x parity), K = (kh, u, oc16) with kw = u - 1 + dx: 7 tiles x 15 k-steps
   float* slab = P.slab1 + (int64_t)b * D::SLABN;
-  if (w < 13) {
-    const int pos_a = min(16 * w + m, 195), Y = pos_a / 14, X = pos_a - 14 * Y;
+  if (w < 7) {
+    const int pidx = min(16 * w + m, 97), Y = pidx % 14, xp = pidx / 14;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 13; ++s) {
-      const int tap = 2 * s + (g >> 1), oc0 = 8 * (g & 1), kh = tap / 5, kw = tap - 5 * kh;
-      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((tap < 25 ? (Y - kh + 4) * DCHS + X - kw + 4 : 0)) * 16 + oc0);
-      if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
+    for (int s = 0; s < 15; ++s) {
+      const int pp = 2 * s + (g >> 1), oc0 = 8 * (g & 1), kh = pp / 6, u = pp - 6 * kh;
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((pp < 30 ? (Y - kh + 4) * DCHS + 2 * xp + 5 - u : 0)) * 16 + oc0);
+      if (pp >= 30) a = u32x4{0u, 0u, 0u, 0u};
       acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2d + (s * 64 + lane) * 8), acc);
     }
-    const int ic = m;
+    const int ic = m >> 1, dx = m & 1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int pc = 16 * w + 4 * g + r;
-      if (pc < 196 && ic < C1) {
+      const int pr = 16 * w + 4 * g + r;
+      if (pr < 98 && ic < C1) {
+        const int pc = (pr % 14) * 14 + 2 * (pr / 14) + dx;
         const int code = L.i1[ic * 196 + pc];
-        const float gv = code < 4 ? acc[r] : 0.f;
-        if (P.g1) P.g1[((int64_t)b * C1 + ic) * 196 + pc] = gv;
         if (code < 4) {
           const int py = pc / 14, pxx = pc - 14 * py;
-          L.d1[ic * D1S + (2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(gv);
+          L.d1[ic * D1S + (2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(acc[r]);
         }
       }
     }
   } else {
-    // 10 M-tiles over waves 13-15 (4 / 3 / 3): tile tt = (kw, half); rows (ic, kh) = 16 * half + m;
+    // 10 M-tiles over waves 7-15 (wave 7: two): tile tt = (kw, half); rows (ic, kh) = 16 * half + m;
     // row 31 of tile 1 = ones (bias). Wave 15's staging stores were issued in P10.
-    const int t0 = w == 13 ? 0 : (w == 14 ? 4 : 7), t1 = w == 13 ? 4 : (w == 14 ? 7 : 10);
-    for (int tt = t0; tt < t1; ++tt) {
+    const int t0 = w - 7, t1 = w == 7 ? 2 : w - 6;
+    for (int tt0 = t0; tt0 < t1; ++tt0) {
+      const int tt = w == 7 && tt0 == 1 ? 9 : tt0;
       const int kw = tt >> 1, h = tt & 1, i = 16 * h + m, ic = i / 5, kh = i - 5 * ic;
       const bool valid = ic < C1, ones = tt == 1 && m == 15;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -808,6 +820,26 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
       else if (kw == 0) slab[oc * 76 + 75] = v;
     }
   }
+  static_assert(F1 <= 128 && F2 <= 128 && NC <= 64, "end-of-kernel store mapping");
+  // activations / gradients for the batch reductions of KW (and inspection), all stored here: no
+  // load of this kernel is waited for after this point
+  for (int e = t; e < FLAT; e += kT) {
+    P.p2[(int64_t)b * FLAT + e] = L.f32[e];
+    P.dflat[(int64_t)b * FLAT + e] = L.df[e];
+  }
+  if (t < F1) {
+    P.h1[(int64_t)b * F1 + t] = L.sh1[t];
+    P.dh1[(int64_t)b * F1 + t] = L.sdh1[t];
+  } else if (t >= 128 && t < 128 + F2) {
+    P.h2[(int64_t)b * F2 + t - 128] = L.sh2[t - 128];
+    P.dh2[(int64_t)b * F2 + t - 128] = L.sdh2[t - 128];
+  } else if (t >= 256 && t < 256 + NC) {
+    P.logits[(int64_t)b * NC + t - 256] = L.slog[t - 256];
+    P.dlogits[(int64_t)b * NC + t - 256] = L.sdl[t - 256];
+  } else if (t == 320 && P.cestat) {
+    P.cestat[2 * b] = L.ce[0];
+    P.cestat[2 * b + 1] = L.ce[1];
+  }
   if (aug && t == 0 && P.targets) P.targets[b] = tgt;  // (inspection; nothing downstream reads it)
   // the step's optimizer context for KW (lr from the device table, Adam's t)
   if (b == 0 && t == 0 && P.stepinfo) {
@@ -818,6 +850,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     P.stepinfo[2] = (int64_t)__float_as_uint(lr);
   }
   stamp(13);
+  if ((mode & LENET_TRACE) && b == 0 && t < 32 && P.trace) reinterpret_cast<unsigned long long*>(P.trace)[t] = L.tr[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1005,7 +1038,8 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
           if (e2 < C2 * C1 * 25) {
             const int oc = e2 / (C1 * 25), ic = (e2 / 25) % C1, tap = e2 % 25;
             P.wimg[w2f_slot(oc, ic, tap)] = hb;
-            P.wimg[w2d_slot(oc, ic, tap)] = hb;
+            P.wimg[w2d_slot(oc, ic, tap, 0)] = hb;
+            P.wimg[w2d_slot(oc, ic, tap, 1)] = hb;
           }
         }
       }
