@@ -377,7 +377,13 @@ def main():
     targets = torch.randint(0, 10, (N,), dtype=torch.int64, device=dev, generator=g)
     engine.set_dataset(data, targets, batch_size=per_gpu, augment=True)
     # graphs of up to 64 steps: one replay covers a short timed run, long runs amortise launches
-    spg = args.steps_per_graph or max(1, min(64, args.steps))
+    # steps per graph: the largest d <= 64 dividing both K and W, so that the warmup replays the very
+    # graph the timed steps replay (a freshly uploaded graph's first replay costs ~40 us more, measured
+    # by scripts/debug/replay_cold.py); min(64, K) when they share no useful divisor
+    spg = args.steps_per_graph
+    if not spg:
+        common = [d for d in range(1, 65) if args.steps % d == 0 and args.warmup > 0 and args.warmup % d == 0]
+        spg = max(common) if common and max(common) >= 4 else max(1, min(64, args.steps))
     use_graph = not args.no_graph
 
     state = {"epoch": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}

@@ -22,7 +22,7 @@ m = MLModel().to(dev)
 flat = FlatParams(m.parameters())
 opt = build_optimizer("sgd", m.parameters(), lr=1e-3, momentum=0.9, flat=flat)
 eng = LeNetStepEngine(m, flat, max_batch=B, optimizer=opt, precision="bf16")
-trace = torch.zeros(64, dtype=torch.float32, device=dev)
+trace = torch.zeros(2048, dtype=torch.float32, device=dev)
 eng.bufs["trace"] = trace
 eng.eng = eng.C.LeNetEngine(m.cfg_id, B, eng.bufs)  # rebuild with the trace buffer bound
 eng.eng.set_ctrl(eng.ctrl)
@@ -38,9 +38,8 @@ C = eng.C
 # stamp slots in kernel order (lenet_mfma.hip stamp(k)); a name per interval
 idx = [0, 16, 17, 1, 2, 3, 18, 19, 4, 20, 21, 22, 5, 6, 7, 13]
 names = ["P0 loads issued (+ctrl/meta scalar wait)", "P1 zero fill + raw image to LDS", "P1 augment -> xh/xc",
-         "P2 conv1", "P3 conv2", "P4 fc1 fwd (MFMA)", "P4 fc2 fwd", "P4 fc3 fwd", "P5 softmax-CE",
-         "P6 fc3 dgrad", "P7 fc2 dgrad", "P8 fc1 dgrad (MFMA)", "P10 unpool", "P11 conv2 dgrad/wgrad",
-         "P13 conv1 wgrad + slabs"]
+         "P2 conv1", "P3 conv2", "P4 fc1 fwd", "P4 fc2 fwd", "P4 fc3 fwd + softmax-CE", "P6 fc3 dgrad",
+         "P7 fc2 dgrad", "-", "P8 fc1 dgrad", "P10 unpool", "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad + slabs"]
 rows = []
 for rep in range(9):
     eng.eng.run(C.LENET_FWD | C.LENET_CE | C.LENET_BWD | C.LENET_TRACE, B)
@@ -57,6 +56,24 @@ for k, n in enumerate(names):
     dm = d[len(d) // 2]
     rec["phases_us"][n] = round(dm / ghz / 1e3, 3)
     print(f"  {n:28s} {dm:8d} cycles  {dm / ghz / 1e3:7.2f} us")
+# per-block wall clock (100 MHz): KS blocks (slots 600 + 2b), KW blocks (64 + 5 blk: start, 4 wave ends)
+tr = rows[-1]
+ks = [(tr[600 + 2 * i], tr[601 + 2 * i]) for i in range(min(B, 200))]
+C = eng.C
+nkw = C.lenet_mfma_kw_blocks(m.cfg_id)
+kw = [(tr[64 + 5 * i], max(tr[65 + 5 * i:69 + 5 * i])) for i in range(min(nkw, 100))]
+t0 = min(a for a, _ in ks)
+ks_end = max(e for _, e in ks)
+print(f"KS blocks: start spread {(max(a for a, _ in ks) - t0) * 10} ns, block time "
+      f"{min(e - a for a, e in ks) * 10}..{max(e - a for a, e in ks) * 10} ns, last end at {(ks_end - t0) * 10} ns")
+rec["ks_block_ns"] = [[(a - t0) * 10, (e - t0) * 10] for a, e in ks]
+if kw:
+    k0 = min(a for a, _ in kw)
+    print(f"KW blocks ({nkw}): first start {(k0 - ks_end) * 10} ns after the last KS end; start spread "
+          f"{(max(a for a, _ in kw) - k0) * 10} ns; last end {(max(e for _, e in kw) - k0) * 10} ns after its first start")
+    slow = sorted(range(len(kw)), key=lambda i: kw[i][1])[-5:]
+    print("  latest-ending KW blocks:", [(i, (kw[i][0] - k0) * 10, (kw[i][1] - k0) * 10) for i in slow])
+    rec["kw_block_ns"] = [[(a - k0) * 10, (e - k0) * 10] for a, e in kw]
 if out:
     with open(out, "a") as f:
         f.write(json.dumps(rec) + "\n")

@@ -993,7 +993,7 @@ class LeNetEngine {
       P_.wimg = reinterpret_cast<uint16_t*>(get("wimg", at::kShort, lenet_mfma_wimg_elems()).data_ptr<int16_t>());
       TORCH_CHECK(P_.slab1 != nullptr && (int64_t)C1 * 640 >= lenet_mfma_slab_floats(cfg), "slab1 too small");
     }
-    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 64).data_ptr<float>();
+    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 2048).data_ptr<float>();
     A_ = LeNetAug{};
     O_ = LeNetOpt{};
   }
@@ -1029,6 +1029,8 @@ class LeNetEngine {
     check_dev(p, "p", at::kFloat, n);
     check_dev(g, "g", at::kFloat, n);
     O_ = LeNetOpt{};
+    master_ = p;
+    pack_ver_ = -1;
     O_.p = p.data_ptr<float>();
     O_.g = g.data_ptr<float>();
     O_.n = n;
@@ -1095,6 +1097,7 @@ class LeNetEngine {
     if (p == 1) TORCH_CHECK(P_.shadow && P_.wimg && P_.stage2 && P_.meta2 && P_.metaN && P_.stepinfo,
                             "bf16 engine buffers missing");
     prec_ = p;
+    pack_ver_ = -1;
     graphs_.clear();
   }
   int precision() const { return prec_; }
@@ -1165,7 +1168,7 @@ class LeNetEngine {
     XgmiAllReduce* xgmi = xgmi_;
     const bool mf = prec_ == 1 && (mode & LENET_BWD);
     g->capture([&](hipStream_t s) {
-      if (mf) launch_lenet_mfma_pack(cfg, P, O, s);  // once per replay: the host may have changed the masters
+      // (no pack here: replay() re-packs when the host changed the masters since the last pack)
       for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf);
     });
     graphs_[key(mode, B, nsteps)] = std::move(g);
@@ -1173,9 +1176,23 @@ class LeNetEngine {
 
   bool has_graph(int mode, int B, int nsteps) const { return graphs_.count(key(mode, B, nsteps)) != 0; }
 
+  // bf16 engine: the step kernels read the bf16 shadow / fragment images, which they keep in step
+  // with the fp32 masters themselves. A host-side change of the masters (any torch in-place op:
+  // the flat buffer's version counter moves; invalidate_shadow() for native writers) is folded in
+  // by one pack launch ahead of the next replay.
+  void sync_shadow() {
+    if (prec_ != 1 || !master_.defined()) return;
+    const int64_t v = master_._version();
+    if (v == pack_ver_) return;
+    launch_lenet_mfma_pack(cfg_, P_, O_, cur_stream());
+    pack_ver_ = v;
+  }
+  void invalidate_shadow() { pack_ver_ = -1; }
+
   void replay(int mode, int B, int nsteps) {
     auto it = graphs_.find(key(mode, B, nsteps));
     TORCH_CHECK(it != graphs_.end(), "no captured graph for this (mode, B, nsteps)");
+    if (mode & LENET_BWD) sync_shadow();
     it->second->launch(cur_stream());
   }
 
@@ -1204,6 +1221,8 @@ class LeNetEngine {
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
   int prec_ = 0;
   int64_t shadow_n_ = 0;
+  Tensor master_;          // the fp32 masters (version counter: host-side changes)
+  int64_t pack_ver_ = -1;  // master_._version() at the last pack
 };
 
 }  // namespace mlt
@@ -1255,6 +1274,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
   m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
   m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));
+  m.def("lenet_mfma_kw_blocks", &lenet_mfma_kw_blocks, py::arg("cfg"));
   m.def("get_lenet_variant", &get_lenet_variant);
   m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("fmt") = 0);
@@ -1324,6 +1344,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("capture", &LeNetEngine::capture)
       .def("has_graph", &LeNetEngine::has_graph)
       .def("replay", &LeNetEngine::replay)
+      .def("invalidate_shadow", &LeNetEngine::invalidate_shadow)
       .def("graph_nodes", &LeNetEngine::graph_nodes)
       .def("reset_graphs", &LeNetEngine::reset_graphs);
   m.attr("LENET_FWD") = (int)LENET_FWD;

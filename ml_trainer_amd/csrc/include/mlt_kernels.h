@@ -99,6 +99,7 @@ void launch_head_cls_bwd(const float* dlogits, const float* pooled, const float*
 void launch_lenet_mfma(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                        hipStream_t stream);
 int lenet_mfma_slab_floats(int cfg);
+int lenet_mfma_kw_blocks(int cfg);  // grid of the batch-reduction / optimizer kernel
 int lenet_mfma_wimg_elems();
 // shadow + wimg from the fp32 masters (O.p)
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);

@@ -9,8 +9,9 @@
 //       (epoch permutation -> dataset row) and staged by an otherwise idle wave, so the next step
 //       starts with one round trip instead of ctrl -> perm -> image.
 //   KW  lenet_mw<D>  role-split grid: conv slab sums over the batch (sample order), fc weight
-//       gradients over the batch, the fused optimizer update (fp32 masters + bf16 shadow), the
-//       fixed-order loss / accuracy sums, the step-counter advance.
+//       gradients over the batch (exact-f32 MFMA tiles, sample-ordered), the fused optimizer update
+//       (fp32 masters + bf16 shadow + the per-sample kernel's fragment images), the fixed-order loss
+//       / accuracy sums, the step-counter advance.
 //
 // Why this shape (measured on the fp32 four-kernel step, profiles/pmc/lenet_fp32_b{4,32}_r3.jsonl): every
 // kernel of that step sat 55-70 % of its wave cycles in s_waitcnt / barriers, and the step took
@@ -87,9 +88,17 @@ __device__ __forceinline__ unsigned pack2(uint16_t lo, uint16_t hi) { return (un
 //   conv2 dgrad k = ((kh*6 + u) * 16 + oc, n = 2 ic + dx, with kw = u - 1 + dx (two columns per
 //               weight, as conv1: the dgrad output's x parity dx is in N)
 constexpr int kW1F = 0, kW2F = 4 * 512, kW2D = 11 * 512, kWimg = 26 * 512;
-// followed by fc1's weight TRANSPOSED ([in][out] bf16, the backward-data B operand: 16 contiguous
-// bytes per lane), sized for the largest config
-constexpr int kFc1T = kWimg, kWimgTot = kWimg + 400 * 120;
+// followed by the fc weights the per-sample kernel cannot read from the row-major shadow with 16-byte
+// lanes: every layer TRANSPOSED ([in][out], the backward-data B operand) and fc3 with its rows padded
+// to 8 elements; row pitches padded to 8 elements, padding zero. Sized for the largest config.
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+constexpr int kFc1T = kWimg;               // [FLAT][F1]
+constexpr int kFc2T = kFc1T + 400 * 120;   // [F1][round8(F2)]
+constexpr int kFc3F = kFc2T + 120 * 88;    // [NC][round8(F2)]
+constexpr int kFc3T = kFc3F + 10 * 88;     // [F2][round8(NC)]
+constexpr int kWimgTot = kFc3T + 84 * 16;
+constexpr int round8(int v) { return (v + 7) / 8 * 8; }
 __device__ __forceinline__ int w1f_slot(int oc, int c, int kh, int kw, int dx) {
   const int u = kw + dx, qq = kh * 3 + (u >> 1);
   return kW1F + (((qq >> 2) * 64 + (qq & 3) * 16 + 2 * oc + dx) << 3) + ((u & 1) << 2) + c;
@@ -145,145 +154,61 @@ constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel 
 constexpr int kWgT = 256;        // KW threads
 
 // ---------------------------------------------------------------------------
-// fc layer with bf16 weights held in registers (4 columns = 8 bytes per slot) for the whole
-// kernel: forward row dots (G lanes per row, DPP tree) and backward-data (each lane scales its
-// weight fragment by the upstream gradient; row groups summed through LDS in a fixed order).
+// fc layers on the matrix cores: y = W x for ONE sample, its input row x (bf16 in LDS, zero past K
+// up to the k-step multiple) broadcast over the 16 A rows; a wave owns a tile of 16 outputs and all
+// K steps, its B fragments (W rows, 16 contiguous bytes per lane) in registers. Rows / chunks past
+// the matrix re-read its last ones: their products meet zero A columns or land in unstored outputs.
 // ---------------------------------------------------------------------------
 constexpr int pow2_ge(int v) { return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : v <= 16 ? 16 : v <= 32 ? 32 : 64; }
 
-// (opaque to the optimiser: the packed weights stay the register-resident form -- CSE of the
-// forward's unpacked values into the backward would double their registers)
-__device__ __forceinline__ float4 unpack4(uint2 u) {
-  asm volatile("" : "+v"(u.x), "+v"(u.y));
-  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-                     __uint_as_float(u.y & 0xffff0000u));
+template <int KS, int LD, int N, int K>
+__device__ __forceinline__ void frag_rows(u32x4 (&f)[KS], const uint16_t* __restrict__ W, int tn) {
+  const unsigned lane = threadIdx.x & 63;
+  const unsigned row = min(16u * tn + (lane & 15), (unsigned)N - 1);
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    const unsigned col = min(32u * q + 8 * (lane >> 4), (unsigned)((K - 1) / 8 * 8));
+    f[q] = *reinterpret_cast<const u32x4*>(W + row * LD + col);
+  }
+}
+// output 16 tn + lane of the tile, valid in lanes 0-15 (all 16 C rows are equal)
+template <int KS>
+__device__ __forceinline__ float row_dot(const u32x4 (&f)[KS], const uint16_t* x) {
+  const int g = (threadIdx.x & 63) >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < KS; ++q) acc = mfma(*reinterpret_cast<const u32x4*>(x + 32 * q + 8 * g), f[q], acc);
+  return acc[0];
 }
 
-template <int NCOLS, int NROWS, int NT>
-struct BLinear {
-  static constexpr int NV = NCOLS / 4;
-  static constexpr int G = pow2_ge(NV);
-  static constexpr int PL = (NV + G - 1) / G;
-  static constexpr int R = 64 / G;
-  static constexpr int NW = NT / 64;
-  static constexpr int RPI = NW * R;
-  static constexpr int IT = (NROWS + RPI - 1) / RPI;
-  static constexpr int SCRATCH = RPI * NCOLS;
-  uint2 w[IT][PL];
 
-  __device__ __forceinline__ int row(int it) const {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    return it * RPI + wid * R + lane / G;
-  }
-  // clamped, unconditional loads: padding rows / columns are never used (forward stores only
-  // r < NROWS, v < NV; backward scales padding rows by 0 and stores only v < NV)
-  // 32-bit unsigned element offsets (SGPR base + one VGPR offset per load, not a 64-bit address
-  // pair per load: all IT * PL loads are in flight at once); clamped only where a row / column
-  // group can run past the layer (compile-time per iteration)
-  __device__ __forceinline__ void load(const uint16_t* __restrict__ W) {
-    const unsigned lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gl = lane % G;
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const unsigned r0 = it * RPI + wid * R + lane / G;
-      const unsigned r = ((it + 1) * RPI > NROWS) ? min(r0, (unsigned)NROWS - 1) : r0;
-#pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const unsigned v = ((i + 1) * G > NV) ? min(gl + i * G, (unsigned)NV - 1) : gl + i * G;
-        w[it][i] = *reinterpret_cast<const uint2*>(W + (r * NCOLS + 4 * v));
-      }
-    }
-  }
-  template <bool RELU>
-  __device__ __forceinline__ void fwd(const float* xin, const float* bias, float* out_lds,
-                                      float* __restrict__ out_g) const {
-    const int gl = (threadIdx.x & 63) % G;
-    const float4* x4 = reinterpret_cast<const float4*>(xin);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const int v = gl + i * G;
-        if (v < NV) {
-          const float4 xv = x4[v], wq = unpack4(w[it][i]);
-          acc = fmaf(wq.x, xv.x, acc);
-          acc = fmaf(wq.y, xv.y, acc);
-          acc = fmaf(wq.z, xv.z, acc);
-          acc = fmaf(wq.w, xv.w, acc);
-        }
-      }
-      acc = group_reduce_last<G>(acc);
-      const int r = row(it);
-      if (gl == G - 1 && r < NROWS) {
-        float o = acc + bias[r];
-        if (RELU) o = fmaxf(o, 0.f);
-        out_lds[r] = o;
-        if (out_g) out_g[r] = o;
-      }
-    }
-  }
-  // out[k] = mask(k) * sum_r d[r] W[r][k]; scratch >= SCRATCH floats. Ends with a barrier.
-  __device__ __forceinline__ void bwd(const float* d, float* scratch, float* out_lds, float* __restrict__ out_g,
-                                      const float* mask, uint16_t* out_b16 = nullptr) const {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gl = lane % G, grp = wid * R + lane / G;
-    float dv[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int r = row(it);
-      dv[it] = r < NROWS ? d[r] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const int v = gl + i * G;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const float4 wq = unpack4(w[it][i]);
-        acc.x = fmaf(dv[it], wq.x, acc.x);
-        acc.y = fmaf(dv[it], wq.y, acc.y);
-        acc.z = fmaf(dv[it], wq.z, acc.z);
-        acc.w = fmaf(dv[it], wq.w, acc.w);
-      }
-      if (v < NV) reinterpret_cast<float4*>(scratch)[grp * NV + v] = acc;
-    }
-    lbar();
-    for (int k = threadIdx.x; k < NCOLS; k += NT) {
-      float sum = 0.f;
-#pragma unroll 8
-      for (int g = 0; g < RPI; ++g) sum += scratch[g * NCOLS + k];
-      if (mask) sum = mask[k] > 0.f ? sum : 0.f;
-      out_lds[k] = sum;
-      if (out_g) out_g[k] = sum;
-      if (out_b16) out_b16[k] = f32_to_bf16(sum);
-    }
-    lbar();
-  }
-};
-
-constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int cmin(int a, int b) { return a < b ? a : b; }
-
-// fc1 (FLAT -> F1, 62 % of the model's weights) on the matrix cores, the sample's input row
-// broadcast over the 16 A rows. Forward: FNT tiles of 16 outputs, one per wave of the LAST FNT
-// waves, all K steps of 32 inputs in that wave; backward-data: BNT tiles of 16 inputs over waves
-// 1-15 (wave 0 runs the softmax-CE meanwhile), K steps over the outputs, from the transposed bf16
-// image. B fragments live in registers; their ~100 KB per direction are fetched where the
-// issuing waves are otherwise idle or light (the vector memory path of a CU moves them at
-// ~35 B/clk and a wave stalls while its loads queue): forward at P2 (waves 8-15 carry one conv1
-// tile, the others two), backward during the softmax-CE.
+// The fc chain's wave schedule. Fragments (~150 KB per CU and step) are fetched where the issuing
+// waves are otherwise idle or light -- the vector memory path of a CU moves them at ~35 B/clk and a
+// wave stalls while its loads queue:
+//   fc1 fwd  tiles on waves 8-15, fetched at P2 (these waves carry one conv1 tile, the others two)
+//   fc2 fwd  tiles on waves 8-13, fetched at P3 (conv2 runs on 0-6); fc3 fwd + softmax-CE on wave 14,
+//            fetched during fc2
+//   fc3 / fc2 / fc1 dgrad on waves 0-7 (fc1: 3 tiles each, the 25th on wave 15): fetched by those
+//   waves while waves 8-15 run the forward
 template <class D>
-struct Fc1 {
-  static constexpr int FNT = (D::F1 + 15) / 16, FKS = (D::FLAT + 31) / 32, FW0 = 16 - FNT;
-  static constexpr int BNT = (D::FLAT + 15) / 16, BKS = (D::F1 + 31) / 32, BTP = (BNT + 14) / 15;
-  static_assert(D::FLAT % 8 == 0 && D::F1 % 8 == 0 && D::F1 * D::FLAT <= 400 * 120 && FNT <= 16, "fc1 fragments");
+struct Fc {
+  static constexpr int T1 = (D::F1 + 15) / 16, K1 = (D::FLAT + 31) / 32, W1F = 16 - T1;  // fc1 fwd
+  static constexpr int T2 = (D::F2 + 15) / 16, K2 = (D::F1 + 31) / 32, W2F = 8;           // fc2 fwd
+  static constexpr int K3 = (D::F2 + 31) / 32, W3F = 14;                                  // fc3 fwd
+  static constexpr int B3T = (D::F2 + 15) / 16, B3K = (D::NC + 31) / 32;                  // fc3 dgrad
+  static constexpr int B2T = (D::F1 + 15) / 16, B2K = (D::F2 + 31) / 32;                  // fc2 dgrad
+  static constexpr int B1T = (D::FLAT + 15) / 16, B1K = (D::F1 + 31) / 32;                // fc1 dgrad
+  static constexpr int B1P = cmin(3, (B1T + 7) / 8);  // fc1 dgrad tiles per wave 0-7 (w + 8 j)
+  static constexpr int P2T = round8(D::F2), P3F = round8(D::F2), P3T = round8(D::NC);
+  static_assert(D::FLAT % 8 == 0 && D::F1 % 8 == 0 && D::F1 * D::FLAT <= 400 * 120, "fc1 fragments");
+  static_assert(T1 <= 8 && T2 <= 6 && D::NC <= 16 && B3T <= 8 && B2T <= 8 && B1T <= 8 * B1P + 1, "fc waves");
+  static_assert(D::F1 * P2T <= 120 * 88 && D::NC * P3F <= 10 * 88 && D::F2 * P3T <= 84 * 16, "fc images");
 };
 
 template <class D>
 struct KsLds {
-  using L2 = BLinear<D::F1, D::F2, kT>;
-  using L3 = BLinear<D::F2, D::NC, kT>;
-  using F = Fc1<D>;
-  static constexpr int SCR = cmax(cmax(L2::SCRATCH, L3::SCRATCH), 3 * 5 * 256);
+  using F = Fc<D>;
+  static constexpr int SCR = 3 * 5 * 256;
   // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
   // MFMA fragment reads
   alignas(16) uint16_t p1h[14 * P1HS * 8];           // pooled conv1 [y][x][ic8]
@@ -297,8 +222,13 @@ struct KsLds {
   alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
   alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
   alignas(16) uint16_t w2d[15 * 64 * 8];             // conv2 dgrad B fragments
-  alignas(16) uint16_t fb16[32 * F::FKS];           // flattened pooled conv2, bf16 (fc1 A row; tail zero)
-  alignas(16) uint16_t dh1b[32 * F::BKS];            // fc1 output gradient, bf16 (fc1 dgrad A row; tail zero)
+  // bf16 A rows of the fc MFMAs (tails zero to the k-step multiple)
+  alignas(16) uint16_t fb16[32 * F::K1];             // flattened pooled conv2 (fc1)
+  alignas(16) uint16_t h1b[32 * F::K2];              // fc1 output (fc2)
+  alignas(16) uint16_t h2b[32 * F::K3];              // fc2 output (fc3)
+  alignas(16) uint16_t dlb[32 * F::B3K];             // logit gradient (fc3 dgrad)
+  alignas(16) uint16_t dh2b[32 * F::B2K];            // fc2 output gradient (fc2 dgrad)
+  alignas(16) uint16_t dh1b[32 * F::B1K];            // fc1 output gradient (fc1 dgrad)
   alignas(16) float df[D::FLAT];                     // its gradient
   alignas(16) float sh1[D::F1];
   alignas(16) float sh2[D::F2];
@@ -306,7 +236,7 @@ struct KsLds {
   alignas(16) float sdh2[D::F2];
   alignas(16) float slog[64];
   alignas(16) float sdl[64];
-  alignas(16) float scr[SCR];                        // fc bwd row-group partials / conv1 wgrad partials
+  alignas(16) float scr[SCR];                        // conv1 wgrad partials
   alignas(16) float f32[D::FLAT];                    // flattened pooled conv2, fp32 (stored for the fc1 wgrad)
   unsigned long long tr[32];                         // LENET_TRACE stamps
   double ce[2];                                      // this sample's (loss / B, hit / B)
@@ -392,6 +322,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     }
   };
   stamp(0);
+  unsigned long long tb0 = 0;
+  if (mode & LENET_TRACE) tb0 = __builtin_amdgcn_s_memrealtime();
 
   // ---- P0: every independent load in flight together ----------------------------------------
   // straight-line and unconditional (ctrl / meta2 / stage2 are host-checked), ctrl first: the
@@ -415,28 +347,22 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     for (int c = 0; c < 3; ++c) xin[c] = P.x[(int64_t)b * 3072 + c * 1024 + t];
   }
   // conv weight B-fragment images (bf16, packed by the optimizer / lenet_mpack): 24 KB, linear
+  // (the forward fragments only: conv2's dgrad fragments follow in P3, off the critical path)
   const uint4* wimg4 = reinterpret_cast<const uint4*>(P.wimg);
-  constexpr int WI1 = kWimg / 8 - 1024;  // uint4s of the image past the first 1024
-  const uint4 wi0 = wimg4[t], wi1 = wimg4[1024 + min(t, WI1 - 1)];
+  constexpr int WIF = kW2D / 8, WID = (kWimg - kW2D) / 8;  // uint4s: forward part, dgrad part
+  static_assert(WIF <= kT && WID <= kT, "fragment image staging");
+  const uint4 wi0 = wimg4[min(t, WIF - 1)];
   const float b1v = P.b1[min(t, C1 - 1)], b2v = P.b2[min(t, C2 - 1)];
   constexpr int NFB = F1 + F2 + NC;
   const float fbv = t < F1 ? P.b3[t] : (t < F1 + F2 ? P.b4[min(t - F1, F2 - 1)] : P.b5[min(max(t - F1 - F2, 0), NC - 1)]);
   using F1M = typename S::F;
-  u32x4 f1w[F1M::FKS];  // fc1 forward B fragments (row-major W rows of the shadow: 16 B per lane)
-  typename S::L2 l2;
-  typename S::L3 l3;
+  constexpr int P2T = F1M::P2T, P3F = F1M::P3F, P3T = F1M::P3T;
+  u32x4 f1w[F1M::K1];  // fc1 forward B fragments (row-major W rows of the shadow: 16 B per lane)
   // fc weights: issued once this step's image and conv fragments are in LDS (fc1: start of P2; fc2 /
   // fc3: start of P3, where conv1's registers are free), so that their transfer does not delay
   // those. Padding lanes re-read a valid lane's line (coalesced).
   auto load_fc = [&]() {
-    if (w >= F1M::FW0) {
-      const unsigned row = min(16u * (w - F1M::FW0) + m, (unsigned)F1 - 1);
-#pragma unroll
-      for (int q = 0; q < F1M::FKS; ++q) {
-        const unsigned col = min(32u * q + 8 * g, (unsigned)FLAT - 8);
-        f1w[q] = *reinterpret_cast<const u32x4*>(P.shadow + O.off[4] + row * FLAT + col);
-      }
-    }
+    if (w >= F1M::W1F) frag_rows<F1M::K1, FLAT, F1, FLAT>(f1w, P.shadow + O.off[4], w - F1M::W1F);
   };
   __builtin_amdgcn_sched_barrier(0);  // keep the index math below behind the load issue
   int64_t pos = sie * A.batch_stride + b;
@@ -453,11 +379,14 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     uint4* z = reinterpret_cast<uint4*>(L.p1h);
     for (int e = t; e < ZB / 16; e += kT) z[e] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 3 * 32 * 2) reinterpret_cast<uint4*>(L.xc + (t >> 1) * XCS + 32)[t & 1] = make_uint4(0u, 0u, 0u, 0u);
-    if (t < 32 * S::F::FKS - FLAT) L.fb16[FLAT + t] = 0;
-    if (t < 32 * S::F::BKS - F1) L.dh1b[F1 + t] = 0;
+    if (t < 32 * F1M::K1 - FLAT) L.fb16[FLAT + t] = 0;
+    if (t < 32 * F1M::K2 - F1) L.h1b[F1 + t] = 0;
+    if (t < 32 * F1M::K3 - F2) L.h2b[F2 + t] = 0;
+    if (t < 32 * F1M::B3K - NC) L.dlb[NC + t] = 0;
+    if (t < 32 * F1M::B2K - F2) L.dh2b[F2 + t] = 0;
+    if (t < 32 * F1M::B1K - F1) L.dh1b[F1 + t] = 0;
     uint4* wl = reinterpret_cast<uint4*>(L.w1f);  // w1f | w2f | w2d are contiguous
-    wl[t] = wi0;
-    if (t < WI1) wl[1024 + t] = wi1;
+    if (t < WIF) wl[t] = wi0;
     if (t < NFB) L.fb[t] = fbv;
     if (t < 16) {
       L.b1s[t] = t < C1 ? b1v : 0.f;
@@ -545,8 +474,10 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   lbar();
   stamp(2);
 
-  l2.load(P.shadow + O.off[6]);
-  l3.load(P.shadow + O.off[8]);
+  const uint4 wid = wimg4[WIF + min(t, WID - 1)];  // conv2 dgrad fragments (to LDS in P10)
+  u32x4 f2w[F1M::K2], f3w[F1M::K3];  // fc2 fwd (waves 8-13) / fc3 fwd (wave 14, fetched in P4) B fragments
+  if (w >= F1M::W2F && w < F1M::W2F + F1M::T2)
+    frag_rows<F1M::K2, F1, F2, F1>(f2w, P.shadow + O.off[6], w - F1M::W2F);
   // next-step staging (wave 15, two steps deep so that no load waits on another inside this kernel):
   // metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1; when it
   // matches, the raw image of step + 1 is gathered now (stored to stage2 in P10). The perm entry
@@ -606,43 +537,44 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   lbar();
   stamp(3);
 
-  // ---- P4-P9: fc1 -> fc2 -> fc3 -> softmax-CE -> fc dgrad chain -------------------------------
-  if (w >= F1M::FW0) {
-    const int tn = w - F1M::FW0;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < F1M::FKS; ++q) {
-      const int col = 32 * q + 8 * g;
-      const u32x4 av = *reinterpret_cast<const u32x4*>(L.fb16 + col);
-      const bool ok = 16 * tn + m < F1 && col < FLAT;
-      acc = mfma(av, ok ? f1w[q] : u32x4{0u, 0u, 0u, 0u}, acc);
+  // ---- P4-P9: fc1 -> fc2 -> fc3 + softmax-CE -> fc dgrad chain, all on the matrix cores -------
+  if (w >= F1M::W1F) {  // fc1 forward
+    const int r = 16 * (w - F1M::W1F) + m;
+    const float v = row_dot(f1w, L.fb16);
+    if (g == 0 && r < F1) {
+      const float h = fmaxf(v + L.fb[r], 0.f);
+      L.sh1[r] = h;
+      L.h1b[r] = f32_to_bf16(h);
     }
-    const int r = 16 * tn + m;
-    if (g == 0 && r < F1) L.sh1[r] = fmaxf(acc[0] + L.fb[r], 0.f);  // C row 0 (all rows are equal)
+  }
+  // dgrad fragments of waves 0-7 (first needed first: vmcnt retires in issue order)
+  u32x4 f3t[F1M::B3K], f2t[F1M::B2K], f1t[F1M::B1P][F1M::B1K];
+  if (w < 8) {
+    if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, P.wimg + kFc3T, w);
+    if (w < F1M::B2T) frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
+#pragma unroll
+    for (int j = 0; j < F1M::B1P; ++j) frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[j], P.wimg + kFc1T, w + 8 * j);
   }
   lbar();
   stamp(18);
-  l2.template fwd<true>(L.sh1, L.fb + F1, L.sh2, nullptr);
-  lbar();
-  stamp(19);
-  l3.template fwd<false>(L.sh2, L.fb + F1 + F2, L.slog, nullptr);
-  lbar();
-  stamp(4);
-  u32x4 f1t[F1M::BTP][F1M::BKS];  // fc1 backward-data B fragments (waves 1-15), fetched during the CE
-  if (w > 0) {
-#pragma unroll
-    for (int tp = 0; tp < F1M::BTP; ++tp) {
-      const unsigned c = min(16u * (w - 1 + 15 * tp) + m, (unsigned)FLAT - 1);
-#pragma unroll
-      for (int ks = 0; ks < F1M::BKS; ++ks) {
-        const unsigned r0 = min(32u * ks + 8 * g, (unsigned)F1 - 8);
-        f1t[tp][ks] = *reinterpret_cast<const u32x4*>(P.wimg + kFc1T + c * F1 + r0);
-      }
+  if (w == 15 && F1M::B1T > 8 * F1M::B1P)  // the 25th fc1 dgrad tile (wave 15 idles in fc2 / fc3)
+    frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[0], P.wimg + kFc1T, 8 * F1M::B1P);
+  if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, P.wimg + kFc3F, 0);
+  if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // fc2 forward
+    const int r = 16 * (w - F1M::W2F) + m;
+    const float v = row_dot(f2w, L.h1b);
+    if (g == 0 && r < F2) {
+      const float h = fmaxf(v + L.fb[F1 + r], 0.f);
+      L.sh2[r] = h;
+      L.h2b[r] = f32_to_bf16(h);
     }
   }
-  if (w == 0) {
+  lbar();
+  stamp(19);
+  if (w == F1M::W3F) {  // fc3 forward + softmax-CE in one wave (the logits are in lanes 0 .. NC-1)
+    const float v = row_dot(f3w, L.h2b);
     constexpr int GC = pow2_ge(NC);
-    const float z = lane < NC ? L.slog[lane] : -INFINITY;
+    const float z = lane < NC ? v + L.fb[F1 + F2 + lane] : -INFINITY;
     const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC, true>(z)), GC - 1));
     const float e = lane < NC ? expf(z - mx) : 0.f;
     const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC>(e)), GC - 1));
@@ -650,10 +582,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     const bool valid = tgt >= 0 && tgt < NC;
     const unsigned long long am_mask = __ballot(lane < NC && z == mx);
     const int am = __ffsll((long long)am_mask) - 1;
-    const float loss = valid ? lse - L.slog[valid ? tgt : 0] : 0.f;
+    const float zt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), valid ? (int)tgt : 0));
+    const float loss = valid ? lse - zt : 0.f;
     if (lane < NC) {
       const float dl = valid ? (e / s - (lane == tgt ? 1.f : 0.f)) * inv_B : 0.f;
+      L.slog[lane] = z;
       L.sdl[lane] = dl;
+      L.dlb[lane] = f32_to_bf16(dl);
     }
     if (lane == 0) {
       L.ce[0] = (double)loss * (double)inv_B;
@@ -661,31 +596,48 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     }
   }
   lbar();
-  stamp(20);
-  l3.bwd(L.sdl, L.scr, L.sdh2, nullptr, L.sh2);
-  stamp(21);
-  l2.bwd(L.sdh2, L.scr, L.sdh1, nullptr, L.sh1, L.dh1b);
-  stamp(22);
-  // (l2.bwd also wrote the bf16 copy dh1b: fc1's dgrad A row)
-#pragma unroll
-  for (int tp = 0; tp < F1M::BTP; ++tp) {
-    const int tile = w - 1 + 15 * tp;
-    if (w > 0 && tile < F1M::BNT) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < F1M::BKS; ++ks) {
-        const u32x4 av = *reinterpret_cast<const u32x4*>(L.dh1b + 32 * ks + 8 * g);
-        const bool ok = 16 * tile + m < FLAT && 32 * ks + 8 * g < F1;
-        acc = mfma(av, ok ? f1t[tp][ks] : u32x4{0u, 0u, 0u, 0u}, acc);
-      }
-      const int c = 16 * tile + m;
-      if (g == 0 && c < FLAT) L.df[c] = acc[0];
+  stamp(4);
+  if (w < F1M::B3T) {  // fc3 dgrad (x the fc2 ReLU mask)
+    const int k = 16 * w + m;
+    const float v = row_dot(f3t, L.dlb);
+    if (g == 0 && k < F2) {
+      const float d = L.sh2[k] > 0.f ? v : 0.f;
+      L.sdh2[k] = d;
+      L.dh2b[k] = f32_to_bf16(d);
     }
+  }
+  lbar();
+  stamp(20);
+  if (w < F1M::B2T) {  // fc2 dgrad (x the fc1 ReLU mask)
+    const int k = 16 * w + m;
+    const float v = row_dot(f2t, L.dh2b);
+    if (g == 0 && k < F1) {
+      const float d = L.sh1[k] > 0.f ? v : 0.f;
+      L.sdh1[k] = d;
+      L.dh1b[k] = f32_to_bf16(d);
+    }
+  }
+  lbar();
+  stamp(21);
+  stamp(22);
+  // fc1 dgrad -> the flattened pooled-conv2 gradient
+  if (w < 8) {
+#pragma unroll
+    for (int j = 0; j < F1M::B1P; ++j) {
+      const int c = 16 * (w + 8 * j) + m;
+      const float v = row_dot(f1t[j], L.dh1b);
+      if (g == 0 && c < FLAT) L.df[c] = v;
+    }
+  } else if (w == 15 && F1M::B1T > 8 * F1M::B1P) {
+    const int c = 16 * (8 * F1M::B1P) + m;
+    const float v = row_dot(f1t[0], L.dh1b);
+    if (g == 0 && c < FLAT) L.df[c] = v;
   }
   lbar();
   stamp(5);
 
   // ---- P10: unpool2 -> the conv2-output gradient images (zero except at arg-max cells) ---------
+  if (t < WID) reinterpret_cast<uint4*>(L.w2d)[t] = wid;
   for (int e = t; e < FLAT; e += kT) {
     const int code = L.i2[e];
     if (code < 4) {
@@ -851,6 +803,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   }
   stamp(13);
   if ((mode & LENET_TRACE) && b == 0 && t < 32 && P.trace) reinterpret_cast<unsigned long long*>(P.trace)[t] = L.tr[t];
+  if ((mode & LENET_TRACE) && P.trace && b < 200) {  // per-block wall clock: slots 600 + 2 b (+1)
+    lbar();
+    if (t == 0) {
+      reinterpret_cast<unsigned long long*>(P.trace)[600 + 2 * b] = tb0;
+      reinterpret_cast<unsigned long long*>(P.trace)[601 + 2 * b] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -876,109 +835,99 @@ template <class D>
 __host__ __device__ constexpr int mw_conv_blocks() {
   return (D::S1 + D::S2 + kWgT - 1) / kWgT;
 }
-// fc weight gradients: a block holds kFcItems (row, 4-column) items x kFcQ batch quarters; each
-// thread sums its quarter of the batch (all its loads in flight at once: one round trip at batch
-// 32), the quarters are combined in a fixed order through LDS
-constexpr int kFcQ = 4, kFcItems = kWgT / kFcQ;
-template <int NCOLS>
-__host__ __device__ constexpr int fc_items(int nrows) {
-  return nrows * (NCOLS / 4);
+// fc weight gradients + update on the matrix cores, exact f32: v_mfma_f32_16x16x4_f32 is a
+// k-ordered fma chain, so 8 of them over a 32-sample chunk sum the batch in sample order, exactly as
+// a sequential loop would. A wave owns a 16 (inputs c; c == NIN is the bias, fed by a ones column)
+// x 16 (outputs j) tile of dW^T: C[c][j] = sum_b X[b][c] dY[b][j]; its lane then holds 4 consecutive
+// inputs of one output row -- one float4 of each optimizer buffer.
+template <int NIN, int NOUT>
+struct FcW {
+  static constexpr int CT = (NIN + 1 + 15) / 16, JT = (NOUT + 15) / 16, TILES = CT * JT;
+  static_assert(NIN % 4 == 0, "bias row alignment");
+};
+template <class D>
+__host__ __device__ constexpr int mw_fc_waves() {
+  return FcW<D::FLAT, D::F1>::TILES + FcW<D::F1, D::F2>::TILES + FcW<D::F2, D::NC>::TILES;
 }
 template <class D>
 __host__ __device__ constexpr int mw_fc_blocks() {
-  return (fc_items<D::FLAT>(D::F1) + kFcItems - 1) / kFcItems + (fc_items<D::F1>(D::F2) + kFcItems - 1) / kFcItems +
-         (fc_items<D::F2>(D::NC) + kFcItems - 1) / kFcItems;
+  return (mw_fc_waves<D>() + kWgT / 64 - 1) / (kWgT / 64);
 }
 
-template <int NCOLS>
-__device__ __forceinline__ void fc_wgrad(int blk, int nrows, int B, const float* __restrict__ dY,
-                                         const float* __restrict__ X, const LeNetOpt& O, const Ctx& c,
-                                         uint16_t* shadow, int64_t offW, int64_t offb, float* red,
-                                         uint16_t* __restrict__ timg = nullptr) {
-  constexpr int NV = NCOLS / 4;
-  const int t = threadIdx.x, q = t & (kFcQ - 1);
-  const int item = blk * kFcItems + (t >> 2);
-  const bool ok = item < nrows * NV;
-  const int it = ok ? item : 0, j = it / NV, v = it - j * NV;
-  const int64_t iw = offW + 4 * (int64_t)it, ib = offb + j;
+template <int NIN, int NOUT>
+__device__ __forceinline__ void fc_wgrad(int tile, int B, const float* __restrict__ dY, const float* __restrict__ X,
+                                         const LeNetOpt& O, const Ctx& c, uint16_t* shadow, int64_t offW, int64_t offb,
+                                         uint16_t* __restrict__ timg, int tpitch, uint16_t* __restrict__ fimg = nullptr,
+                                         int fpitch = 0) {
+  using W = FcW<NIN, NOUT>;
+  const int ct = tile % W::CT, jt = tile / W::CT;
+  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  const int ca = 16 * ct + n, jb = 16 * jt + n;   // this lane's A row (input) / B column (output)
+  const int c0 = 16 * ct + 4 * g, j = 16 * jt + n;  // its C rows c0 .. c0 + 3, column j
+  const bool jok = j < NOUT, wrow = jok && c0 < NIN, brow = jok && c0 == NIN;
+  const int64_t iw = offW + (int64_t)j * NIN + c0, ib = offb + j;
   float4 pw = make_float4(0.f, 0.f, 0.f, 0.f), aw = pw, sw = pw;
   float pb = 0.f, ab = 0.f, sb = 0.f;
-  if (c.on && q == 0 && ok) {  // optimizer state in flight together with the batch loads
+  if (c.on && wrow) {  // optimizer state in flight together with the batch loads
     pw = *reinterpret_cast<const float4*>(O.p + iw);
     if (O.s1) aw = *reinterpret_cast<const float4*>(O.s1 + iw);
     if (O.s2) sw = *reinterpret_cast<const float4*>(O.s2 + iw);
-    if (v == 0) {
-      pb = O.p[ib];
-      if (O.s1) ab = O.s1[ib];
-      if (O.s2) sb = O.s2[ib];
-    }
   }
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  float bacc = 0.f;
-  const float4* x4 = reinterpret_cast<const float4*>(X);
-  for (int b0 = 0; b0 < B; b0 += 8 * kFcQ) {  // this thread: samples b0 + 8q .. b0 + 8q + 7
-    float d[8];
-    float4 xv[8];
+  if (c.on && brow) {
+    pb = O.p[ib];
+    if (O.s1) ab = O.s1[ib];
+    if (O.s2) sb = O.s2[ib];
+  }
+  const int cl = min(ca, NIN - 1), jl = min(jb, NOUT - 1);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = 0; b0 < B; b0 += 32) {
+    float a[8], d[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // MFMA u, k = g: sample b0 + 4u + g
+      const int bb = min(b0 + 4 * u + g, B - 1);
+      a[u] = X[(int64_t)bb * NIN + cl];
+      d[u] = dY[(int64_t)bb * NOUT + jl];
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int bb = min(b0 + 8 * q + u, B - 1);
-      d[u] = dY[(int64_t)bb * nrows + j];
-      xv[u] = x4[(int64_t)bb * NV + v];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float du = b0 + 8 * q + u < B ? d[u] : 0.f;
-      acc.x = fmaf(du, xv[u].x, acc.x);
-      acc.y = fmaf(du, xv[u].y, acc.y);
-      acc.z = fmaf(du, xv[u].z, acc.z);
-      acc.w = fmaf(du, xv[u].w, acc.w);
-      bacc += du;
+      const bool ok = b0 + 4 * u + g < B;
+      const float av = ok ? (ca < NIN ? a[u] : (ca == NIN ? 1.f : 0.f)) : 0.f;
+      const float dv = ok && jb < NOUT ? d[u] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dv, acc, 0, 0, 0);
     }
   }
-  float* r = red + 5 * t;
-  r[0] = acc.x;
-  r[1] = acc.y;
-  r[2] = acc.z;
-  r[3] = acc.w;
-  r[4] = bacc;
-  __syncthreads();
-  if (q != 0 || !ok) return;
-#pragma unroll
-  for (int k = 1; k < kFcQ; ++k) {  // fixed order: quarter 0 + 1 + 2 + 3
-    acc.x += r[5 * k];
-    acc.y += r[5 * k + 1];
-    acc.z += r[5 * k + 2];
-    acc.w += r[5 * k + 3];
-    bacc += r[5 * k + 4];
-  }
-  *reinterpret_cast<float4*>(O.g + iw) = acc;
-  if (c.on) {
-    opt_update(O.h, c.lr, c.t, pw.x, acc.x, aw.x, sw.x);
-    opt_update(O.h, c.lr, c.t, pw.y, acc.y, aw.y, sw.y);
-    opt_update(O.h, c.lr, c.t, pw.z, acc.z, aw.z, sw.z);
-    opt_update(O.h, c.lr, c.t, pw.w, acc.w, aw.w, sw.w);
-    *reinterpret_cast<float4*>(O.p + iw) = pw;
-    if (O.s1) *reinterpret_cast<float4*>(O.s1 + iw) = aw;
-    if (O.s2) *reinterpret_cast<float4*>(O.s2 + iw) = sw;
-    const uint16_t h0 = f32_to_bf16(pw.x), h1 = f32_to_bf16(pw.y), h2 = f32_to_bf16(pw.z), h3 = f32_to_bf16(pw.w);
-    if (shadow) *reinterpret_cast<uint2*>(shadow + iw) = make_uint2(pack2(h0, h1), pack2(h2, h3));
-    if (timg) {  // transposed bf16 image [in][out] (the per-sample kernel's fc1 dgrad operand)
-      timg[(4 * v + 0) * nrows + j] = h0;
-      timg[(4 * v + 1) * nrows + j] = h1;
-      timg[(4 * v + 2) * nrows + j] = h2;
-      timg[(4 * v + 3) * nrows + j] = h3;
+  if (wrow) {
+    float4 gv = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(O.g + iw) = gv;
+    if (c.on) {
+      opt_update(O.h, c.lr, c.t, pw.x, gv.x, aw.x, sw.x);
+      opt_update(O.h, c.lr, c.t, pw.y, gv.y, aw.y, sw.y);
+      opt_update(O.h, c.lr, c.t, pw.z, gv.z, aw.z, sw.z);
+      opt_update(O.h, c.lr, c.t, pw.w, gv.w, aw.w, sw.w);
+      *reinterpret_cast<float4*>(O.p + iw) = pw;
+      if (O.s1) *reinterpret_cast<float4*>(O.s1 + iw) = aw;
+      if (O.s2) *reinterpret_cast<float4*>(O.s2 + iw) = sw;
+      const uint16_t h0 = f32_to_bf16(pw.x), h1 = f32_to_bf16(pw.y), h2 = f32_to_bf16(pw.z), h3 = f32_to_bf16(pw.w);
+      if (shadow) *reinterpret_cast<uint2*>(shadow + iw) = make_uint2(pack2(h0, h1), pack2(h2, h3));
+      if (timg) {  // transposed bf16 image [in][out] (the per-sample kernel's dgrad operand)
+        timg[(c0 + 0) * tpitch + j] = h0;
+        timg[(c0 + 1) * tpitch + j] = h1;
+        timg[(c0 + 2) * tpitch + j] = h2;
+        timg[(c0 + 3) * tpitch + j] = h3;
+      }
+      if (fimg)  // row-padded copy [out][round8(in)] (16-byte fragment rows)
+        *reinterpret_cast<uint2*>(fimg + j * fpitch + c0) = make_uint2(pack2(h0, h1), pack2(h2, h3));
     }
   }
-  if (v == 0) upd1(O, c, shadow, ib, bacc, pb, ab, sb);
+  if (brow) upd1(O, c, shadow, ib, acc[0], pb, ab, sb);
 }
 
 template <class D>
-__global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
+__device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNetOpt& O, int B, int64_t* __restrict__ ctrl) {
   constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
   constexpr int NBC = mw_conv_blocks<D>();
-  constexpr int NB3 = (fc_items<FLAT>(F1) + kFcItems - 1) / kFcItems,
-                NB4 = (fc_items<F1>(F2) + kFcItems - 1) / kFcItems, NB5 = (fc_items<F2>(NC) + kFcItems - 1) / kFcItems;
-  __shared__ float red[5 * kWgT];
+  constexpr int NB = mw_fc_blocks<D>(), NW3 = FcW<FLAT, F1>::TILES, NW4 = FcW<F1, F2>::TILES,
+                NW5 = FcW<F2, NC>::TILES;
   const int t = threadIdx.x;
   int blk = blockIdx.x;
   // the step's counters / lr as the per-sample kernel saw them (nothing here reads ctrl, which
@@ -1047,18 +996,29 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
     return;
   }
   blk -= NBC;
-  if (blk < NB3) {
-    fc_wgrad<FLAT>(blk, F1, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], red, P.wimg ? P.wimg + kFc1T : nullptr);
-  } else if ((blk -= NB3) < NB4) {
-    fc_wgrad<F1>(blk, F2, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], red);
-  } else if ((blk -= NB4) < NB5) {
-    fc_wgrad<F2>(blk, NC, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9], red);
+  if (blk < NB) {  // one fc weight-gradient tile per wave
+    int wv = blk * (kWgT / 64) + (t >> 6);
+    wv = __builtin_amdgcn_readfirstlane(wv);
+    if (wv < NW3) {
+      fc_wgrad<FLAT, F1>(wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], P.wimg ? P.wimg + kFc1T : nullptr, F1);
+    } else if ((wv -= NW3) < NW4) {
+      fc_wgrad<F1, F2>(wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
+                       Fc<D>::P2T);
+    } else if ((wv -= NW4) < NW5) {
+      fc_wgrad<F2, NC>(wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9], P.wimg ? P.wimg + kFc3T : nullptr,
+                       Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);
+    }
   } else {
-    // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats
-    double* red2 = reinterpret_cast<double*>(red);
-    const int lane = t & 63, wid = t >> 6;
+    // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats.
+    // One wave, the running totals fetched together with the per-sample values (one round trip).
+    if (t >= 64) return;
+    double st0 = 0.0, st1 = 0.0;
+    if (t == 0) {
+      st0 = P.stats[0];
+      st1 = P.stats[1];
+    }
     double s0 = 0.0, s1 = 0.0;
-    for (int i = t; i < B; i += kWgT) {
+    for (int i = t; i < B; i += 64) {
       s0 += P.cestat[2 * i];
       s1 += P.cestat[2 * i + 1];
     }
@@ -1067,14 +1027,9 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
       s0 += __shfl_xor(s0, o, 64);
       s1 += __shfl_xor(s1, o, 64);
     }
-    if (lane == 0) {
-      red2[wid] = s0;
-      red2[4 + wid] = s1;
-    }
-    __syncthreads();
     if (t == 0) {
-      P.stats[0] += ((red2[0] + red2[1]) + red2[2]) + red2[3];
-      P.stats[1] += ((red2[4] + red2[5]) + red2[6]) + red2[7];
+      P.stats[0] = st0 + s0;
+      P.stats[1] = st1 + s1;
       if (ctrl) {  // advance the device step counters (next step / lr index / Adam t)
         ctrl[0] = step + 1;
         ctrl[1] = sie + 1;
@@ -1083,20 +1038,43 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
   }
 }
 
+template <class D>
+__global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
+  unsigned long long t0 = 0;
+  if (mode & LENET_TRACE) t0 = __builtin_amdgcn_s_memrealtime();
+  mw_body<D>(mode, P, O, B, ctrl);
+  // LENET_TRACE: 100 MHz wall clock per block (start) and per wave (end): P.trace slots 64 + 5 blk (+1 + wave)
+  if ((mode & LENET_TRACE) && P.trace && blockIdx.x < 100) {
+    unsigned long long* tr = reinterpret_cast<unsigned long long*>(P.trace) + 64 + 5 * blockIdx.x;
+    if (threadIdx.x == 0) tr[0] = t0;
+    if ((threadIdx.x & 63) == 0) tr[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
 // bf16 shadow of the flat parameters + the conv fragment image, from the fp32 masters (start of
 // every captured step sequence, and after each data-parallel optimizer launch)
 template <class D>
 __global__ __launch_bounds__(256) void lenet_mpack(const float* __restrict__ p, int64_t n, uint16_t* __restrict__ shadow,
                                                   uint16_t* __restrict__ wimg, int64_t off_w1, int64_t off_w2,
-                                                  int64_t off_w3) {
+                                                  int64_t off_w3, int64_t off_w4, int64_t off_w5) {
+  using F = Fc<D>;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) shadow[i] = f32_to_bf16(p[i]);
   if (i < kWimg) {
     const int64_t src = wimg_src<D::C1, D::C2>((int)i, off_w1, off_w2);
     wimg[i] = src >= 0 ? f32_to_bf16(p[src]) : (uint16_t)0;
-  } else if (i < kWimgTot) {  // fc1 transposed: [c][r] = W3[r][c]
+  } else if (i < kFc2T) {  // fc1 transposed: [c][r] = W3[r][c]
     const int e = (int)(i - kFc1T), cc = e / D::F1, r = e - cc * D::F1;
     wimg[i] = cc < D::FLAT ? f32_to_bf16(p[off_w3 + (int64_t)r * D::FLAT + cc]) : (uint16_t)0;
+  } else if (i < kFc3F) {  // fc2 transposed [F1][P2T]
+    const int e = (int)(i - kFc2T), cc = e / F::P2T, r = e - cc * F::P2T;
+    wimg[i] = cc < D::F1 && r < D::F2 ? f32_to_bf16(p[off_w4 + (int64_t)r * D::F1 + cc]) : (uint16_t)0;
+  } else if (i < kFc3T) {  // fc3 row-padded [NC][P3F]
+    const int e = (int)(i - kFc3F), r = e / F::P3F, cc = e - r * F::P3F;
+    wimg[i] = r < D::NC && cc < D::F2 ? f32_to_bf16(p[off_w5 + (int64_t)r * D::F2 + cc]) : (uint16_t)0;
+  } else if (i < kWimgTot) {  // fc3 transposed [F2][P3T]
+    const int e = (int)(i - kFc3T), cc = e / F::P3T, r = e - cc * F::P3T;
+    wimg[i] = cc < D::F2 && r < D::NC ? f32_to_bf16(p[off_w5 + (int64_t)r * D::F2 + cc]) : (uint16_t)0;
   }
 }
 
@@ -1104,7 +1082,7 @@ template <class D>
 void pack(const LeNetPtrs& P, const LeNetOpt& O, hipStream_t st) {
   const int64_t tot = O.n > kWimgTot ? O.n : kWimgTot;
   hipLaunchKernelGGL(lenet_mpack<D>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, O.p, O.n, P.shadow, P.wimg,
-                     O.off[0], O.off[2], O.off[4]);
+                     O.off[0], O.off[2], O.off[4], O.off[6], O.off[8]);
 }
 
 template <class D>
@@ -1119,6 +1097,10 @@ void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt&
 
 int lenet_mfma_slab_floats(int cfg) { return cfg == LENET_TINY ? lm::DmTiny::SLABN : lm::DmDefault::SLABN; }
 int lenet_mfma_wimg_elems() { return lm::kWimgTot; }
+int lenet_mfma_kw_blocks(int cfg) {
+  return cfg == LENET_TINY ? lm::mw_conv_blocks<lm::DmTiny>() + lm::mw_fc_blocks<lm::DmTiny>() + 1
+                           : lm::mw_conv_blocks<lm::DmDefault>() + lm::mw_fc_blocks<lm::DmDefault>() + 1;
+}
 
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream) {
   if (cfg == LENET_TINY)

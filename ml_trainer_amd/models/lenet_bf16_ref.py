@@ -4,10 +4,10 @@ The native step rounds to bf16 exactly where an MFMA operand is formed and nowhe
 
 * the (augmented) input image, the conv weights, the pooled conv1 map (conv2's input), the
   unpooled conv2-output gradient (conv2 dgrad / wgrad operand), the unpooled conv1-output
-  gradient (conv1 wgrad operand), the fc weights, and fc1's input row / output gradient row
-  (fc1 forward and backward-data run on the matrix cores);
-* every sum is accumulated in fp32 (here: float64); the stored activations and gradients, the
-  fc2 / fc3 chain, the loss, every weight gradient and the optimizer stay fp32.
+  gradient (conv1 wgrad operand), the fc weights, and every fc layer's input row / output
+  gradient row (the fc forward and backward-data products run on the matrix cores);
+* every sum is accumulated in fp32 (here: float64); the stored activations and gradients (ReLU
+  masks, biases, softmax), the loss, every weight gradient and the optimizer stay fp32.
 
 ``lenet_bf16_grads`` reproduces those rounding points in float64, so the kernel can be checked to
 within fp32 accumulation-order noise. With ``rnd=identity`` it is the exact fp32 model
@@ -74,14 +74,14 @@ def lenet_bf16_grads(params: Dict[str, torch.Tensor], x: torch.Tensor, y: torch.
     p2, code2, alive2 = _pool_codes(F.conv2d(p1b, w2), P["conv2.bias"])
     f = p2.reshape(B, -1)
     h1 = torch.relu(rnd(f) @ w3.t() + P["fc1.bias"])  # fc1 on the matrix cores: bf16 input row
-    h2 = torch.relu(h1 @ w4.t() + P["fc2.bias"])
-    logits = h2 @ w5.t() + P["fc3.bias"]
+    h2 = torch.relu(rnd(h1) @ w4.t() + P["fc2.bias"])
+    logits = rnd(h2) @ w5.t() + P["fc3.bias"]
     loss = F.cross_entropy(logits, y)
     acc = (logits.argmax(1) == y).double().mean()
     # backward
     dlog = (torch.softmax(logits, 1) - F.one_hot(y, logits.shape[1]).to(d)) / B
-    dh2 = (dlog @ w5) * (h2 > 0)
-    dh1 = (dh2 @ w4) * (h1 > 0)
+    dh2 = (rnd(dlog) @ w5) * (h2 > 0)
+    dh1 = (rnd(dh2) @ w4) * (h1 > 0)
     dflat = rnd(dh1) @ w3  # fc1 dgrad on the matrix cores: bf16 gradient row
     dc = rnd(_unpool(dflat.view_as(p2), code2, alive2))
     g1 = torch.nn.grad.conv2d_input(p1b.shape, w2, dc)

@@ -313,9 +313,21 @@ class LeNetStepEngine:
         self.captures += 1
         return 1
 
+    def _note_host_writes(self) -> None:
+        """bf16: a torch in-place change of any parameter (each Parameter keeps its own version
+        counter, not the flat buffer's) since the last replay -> re-pack the bf16 shadow / fragment
+        images ahead of the next one (the engine also watches the flat buffer's own counter)."""
+        if self.precision != "bf16":
+            return
+        sig = tuple(p._version for p in self.flat.params)
+        if sig != getattr(self, "_host_sig", None):
+            self.eng.invalidate_shadow()
+            self._host_sig = sig
+
     def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8) -> None:
         """Run ``n`` full training steps of batch ``B`` from the device dataset."""
         mode = self._train_mode()
+        self._note_host_writes()
         if self.fused or self.in_graph_collective:
             if not use_graph:
                 for _ in range(n):
@@ -356,6 +368,7 @@ class LeNetStepEngine:
                           h["weight_decay"], h["beta1"], h["beta2"], h["eps"], h["lr_decay"], h["grad_scale"],
                           h["nesterov"], h["maximize"], self._lr_arg, self.ctrl[1:2] if self._use_table else None,
                           self.ctrl[0:1], 1.0, None, None)
+        self.eng.invalidate_shadow()  # a native write of the masters: the bf16 step re-packs before its next replay
 
     def eval_steps(self, B: int, n: int = 1) -> None:
         """Forward + CE + accuracy only (validation / test)."""

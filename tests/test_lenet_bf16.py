@@ -256,3 +256,26 @@ def test_bf16_eval_uses_fp32_forward(dev):
     loss, _ = eng.read_stats(1)
     ref = F.cross_entropy(m.forward_reference(x), y).item()
     assert abs(loss - ref) < 1e-4 * max(1.0, ref)
+
+
+@pytest.mark.gpu
+def test_bf16_host_change_of_masters_is_packed(dev):
+    """A host-side in-place change of the fp32 masters between replays reaches the bf16 shadow /
+    fragment images (one pack ahead of the next replay, keyed on the flat buffer's version): the
+    graph path then matches the eager path (which packs before every step) bitwise."""
+    data, targets = _toy_data(256, 13)
+    runs = []
+    for use_graph in (True, False):
+        m = _mk("default", 21).to(dev)
+        eng, flat = _engine(m, "sgd", max_batch=32, lr=1e-2)
+        eng.set_dataset(data, targets, batch_size=32)
+        eng.start_epoch(torch.arange(256))
+        eng.train_steps(32, 2, use_graph=True, steps_per_graph=2)
+        with torch.no_grad():
+            m.fc1.weight.mul_(0.5)
+            m.conv1.weight.mul_(-1.0)
+            m.conv2.weight.add_(0.01)
+        eng.train_steps(32, 2, use_graph=use_graph, steps_per_graph=2)
+        torch.cuda.synchronize()
+        runs.append(flat.data.clone())
+    assert torch.equal(runs[0], runs[1])
