@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (BERT modes)")
     ap.add_argument("--bucket-mb", type=float, default=None, help="BERT modes, N>1: DDP bucket cap (MB)")
     ap.add_argument("--first-bucket-mb", type=float, default=None, help="BERT modes, N>1: first DDP bucket (MB)")
+    ap.add_argument("--ddp-timing", action="store_true",
+                    help="BERT modes, N>1: hipEvent bucket timings (all-reduce ms, overlap %%) in the JSON line; "
+                         "off by default so the timed steps take the Trainer's gradient path")
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
                     help="BERT modes, N>1: gradient all-reduce wire dtype (bf16 = cast in the bucket, reduce, "
                          "cast back into the fp32 gradient)")
@@ -102,7 +105,8 @@ def bench_bert(args, world, rank, dev):
         fwd = ddp
     elif world > 1:
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
-                                      comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, timing=True)
+                                      comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None,
+                                      timing=args.ddp_timing)
         opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, flat=ddp.flat)
         fwd = ddp
     else:
@@ -153,11 +157,12 @@ def bench_bert(args, world, rank, dev):
     value = total / elapsed
     comm = None
     if world > 1 and hasattr(ddp, "comm_stats"):
-        comm = ddp.comm_stats()  # hipEvent bucket timings (synchronises after the timed region)
-        vals = torch.tensor([comm.get("allreduce_ms", 0.0), comm.get("exposed_ms", 0.0)], dtype=torch.float64,
-                            device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-        comm["allreduce_ms_max_rank"], comm["exposed_ms_max_rank"] = [round(float(v), 4) for v in vals.tolist()]
+        comm = ddp.comm_stats()  # bucket layout + comm backend; hipEvent timings with --ddp-timing
+        if args.ddp_timing:
+            vals = torch.tensor([comm.get("allreduce_ms", 0.0), comm.get("exposed_ms", 0.0)], dtype=torch.float64,
+                                device=dev if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+            comm["allreduce_ms_max_rank"], comm["exposed_ms_max_rank"] = [round(float(v), 4) for v in vals.tolist()]
     return {
         "metric": "samples/sec/node",
         "value": round(value, 1),
@@ -181,6 +186,7 @@ def bench_bert(args, world, rank, dev):
                    "model_tflops": round(model.flops_per_token(args.seq_len) * value * args.seq_len / 1e12, 1),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
                    "ddp_comm": comm,
+                   "comm": (comm or {}).get("comm") if world > 1 else None,
                    "loss_finite": math.isfinite(float(loss_acc.item()))},
     }
 

@@ -151,6 +151,44 @@ def test_xgmi_oneshot_allreduce_two_ranks_one_gpu(algo):
     assert torch.equal(r[0]["p"], ref[0]["p"])
 
 
+def _xgmi_sizes_worker(rank, world, port, out_dir, algo):
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
+    x = create_xgmi_allreduce(None, 70000, dev, allow_gloo=True)
+    assert x is not None and x.two_shot_ok
+    x.algo = algo
+    res = []
+    g = torch.Generator().manual_seed(200 + rank)
+    inv = torch.tensor(1.0 / world, dtype=torch.float32)
+    # odd lengths, lengths below 4 * world (empty / partial slices of the two-shot split), a float4
+    # tail, and the LeNet bucket; small-integer values keep every sum exact in any order
+    for n in (1, 3, 4 * world - 1, 4 * world + 1, 13, 4099, 62006, 69999):
+        t = torch.randint(-64, 64, (n,), generator=g).float()
+        ref = t.clone()
+        dist.all_reduce(ref)  # gloo SUM on the host copy (exact)
+        td = t.to(dev)
+        x.all_reduce(td, average=True)
+        torch.cuda.synchronize()
+        res.append(bool(torch.equal(td.cpu(), ref * inv)))
+    torch.save({"ok": torch.tensor(res), "err": torch.tensor([x.error()])}, os.path.join(out_dir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [3, 4])
+@pytest.mark.parametrize("algo", [0, 1])
+def test_xgmi_allreduce_three_four_ranks_one_gpu(world, algo):
+    """The one-shot / two-shot kernels at W = 3, 4 (the 4- and 8-GPU node's code paths: slice and
+    flag indexing, partial and empty slices) rehearsed as W processes on the box's one GPU."""
+    r = _run(_xgmi_sizes_worker, world, algo)
+    assert len(r) == world
+    for d in r:
+        assert d["ok"].all(), d["ok"]
+        assert d["err"].tolist() == [0]
+
+
 def _bert_zero_worker(rank, world, port, out_dir):
     """ZeRO-1 around the fused BERT blocks (direct flat-gradient writes -> reduce-scatter, sharded
     fused AdamW on the GPU, all-gather + bf16 shadow re-cast) against replicated DDP."""
