@@ -1137,20 +1137,24 @@ class LeNetEngine {
         // transport's sticky error word: a step with any timed-out slice is applied on no slice
         // of this rank (all-or-nothing; the host raises TransportError after the replay)
         xgmi->launch(O.g, O.n, 1.f / xgmi->world(), s, nullptr);
+        if (mfma) {  // bf16: update + shadow + fragment images in one launch, vetoed like the flat update
+          launch_lenet_mfma_apply(cfg, P, O, xgmi->error_dev(), s);
+          return;
+        }
         launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
                           nullptr, nullptr, s, xgmi->error_dev());
-        if (mfma) launch_lenet_mfma_pack(cfg, P, O, s);
         return;
       }
       if (comm)  // (size 1 too: the W=1 RCCL rehearsal captures a real ncclAllReduce)
         comm->all_reduce(O.g, O.g, (size_t)O.n, CommDtype::F32, CommOp::AVG, s);
+      if (mfma) {  // the bf16 step reads its weights from the shadow / fragment images: one apply launch
+        launch_lenet_mfma_apply(cfg, P, O, nullptr, s);
+        return;
+      }
       // ctrl[0] = steps taken (already advanced by the backward kernel) -> Adam t; ctrl[1] -> lr table index
       launch_flat_optim(O.p, O.g, O.s1, O.s2, O.n, O.h, O.lr_ptr, O.lr_table ? A.ctrl + 1 : nullptr, A.ctrl, 1.0,
                         nullptr, nullptr, s);
     }
-    // the bf16 step reads its weights from the shadow / fragment image: refresh them after the
-    // data-parallel update (the single-rank step's wgrad kernel writes them itself)
-    if (mfma && (mode & LENET_REDUCE)) launch_lenet_mfma_pack(cfg, P, O, s);
   }
 
   // Capture `nsteps` consecutive steps (the device step counter advances inside)

@@ -100,6 +100,9 @@ void launch_lenet_mfma(int cfg, int mode, int B, const LeNetPtrs& P, const LeNet
                        hipStream_t stream);
 int lenet_mfma_slab_floats(int cfg);
 int lenet_mfma_kw_blocks(int cfg);  // grid of the batch-reduction / optimizer kernel
+// data-parallel bf16 step: optimizer update from the all-reduced gradient + bf16 shadow + fragment
+// images in one launch (skip: nonzero vetoes the update)
+void launch_lenet_mfma_apply(int cfg, const LeNetPtrs& P, const LeNetOpt& O, const unsigned* skip, hipStream_t stream);
 int lenet_mfma_wimg_elems();
 // shadow + wimg from the fp32 masters (O.p)
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);

@@ -13,7 +13,8 @@
 //   transpose read ds_read_b64_tr_b16. The S x S score matrix never touches HBM; the
 //   log-sum-exp per query is saved for the backward pass.
 // Backward = two kernels over the same (64-block, head, batch) grid, no atomics, bitwise
-// reproducible (>= B*H*S/64 workgroups, e.g. 1536 for BERT-base b16 s512):
+// reproducible (>= B*H*S/64 workgroups, e.g. 1536 for BERT-base b16 s512); the ring variants run
+// dQ first, which also produces delta = rowsum(dO * O) for dK/dV:
 //   dK/dV: block = 64 keys, wave = 16 keys (keys on lanes): S = Q K^T, dP = dO V^T,
 //     P = exp2(S*scale*log2e - LSE2), dS = P (dP - delta); dV^T += dO^T P, dK^T += Q^T dS with
 //     accumulators in registers across the whole query loop;
@@ -925,11 +926,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
   }
 }
 
+// The dQ ring kernel runs FIRST and computes delta = rowsum(dO * O) for its own queries in its
+// prologue (dO is in its registers anyway; O is one more 16-byte load per fragment), publishing it
+// for the dK/dV kernel that follows -- no separate delta pass over dO and O.
 template <int NQ, int kRing>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                const uint16_t* __restrict__ dout,
+                                                               const uint16_t* __restrict__ out,
                                                                const float* __restrict__ lse,
-                                                               const float* __restrict__ delta,
+                                                               float* __restrict__ delta,
                                                                const int* __restrict__ lens,
                                                                uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                                float* __restrict__ colpart) {
@@ -967,7 +972,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
                       : bf16x8{};
     }
     lq[n] = q[n] < S ? lse[((int64_t)b * H + h) * S + q[n]] : 0.f;
-    dl[n] = q[n] < S ? delta[(base + q[n]) * H + h] : 0.f;
+    {  // delta of query q[n], bit-identical to attn_delta_kernel: its 16 four-dim partials (dims 4 sub ..)
+       // are this lane's (kh, half) quads, sub = 8 kh + 2 g + half, summed in group_sum<16>'s
+       // butterfly order (xor 8 = kh in-lane, xor 4 = lane ^ 32, xor 2 = lane ^ 16, xor 1 = half)
+      float s4[2][2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const bf16x8 o8 = q[n] < S ? *reinterpret_cast<const bf16x8*>(out + (base + q[n]) * (int64_t)D + h * AH +
+                                                                        kh * 32 + 8 * g)
+                                   : bf16x8{};
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int j = 4 * hf;
+          s4[kh][hf] = (float)of[n][kh][j] * (float)o8[j] + (float)of[n][kh][j + 1] * (float)o8[j + 1] +
+                       (float)of[n][kh][j + 2] * (float)o8[j + 2] + (float)of[n][kh][j + 3] * (float)o8[j + 3];
+        }
+      }
+      float w[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float v = s4[0][hf] + s4[1][hf];
+        v += __shfl_xor(v, 32, 64);
+        v += __shfl_xor(v, 16, 64);
+        w[hf] = v;
+      }
+      const float sacc = w[0] + w[1];
+      dl[n] = q[n] < S ? sacc : 0.f;
+      if (g == 0 && q[n] < S) delta[(base + q[n]) * H + h] = sacc;
+    }
 #pragma unroll
     for (int d = 0; d < 4; ++d) acc[n][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -1081,8 +1113,6 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      float* colpart_q, float* colpart_kv, int* rows_q, int* rows_kv) {
   if (B <= 0 || S <= 0) return false;
   const int64_t pairs = (int64_t)B * S * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
-                     (int64_t)B * S, H);
   const dim3 g2((S + 127) / 128 * H * B), g1((S + 63) / 64 * H * B);
   // MLT_ATTN_RING: 0 = register-staged kernels, 3 / 4 = ring depth (default 4)
   const char* rv = getenv("MLT_ATTN_RING");
@@ -1091,18 +1121,18 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     const bool k2 = attn_groups("MLT_ATTN_DKDV_GROUPS", S, 2) == 2, q2 = attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2;
 #define MLT_RING_LAUNCH(RD)                                                                                         \
   {                                                                                                                 \
+    if (q2)                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, out, lse, delta, lens,  \
+                         dqkv, S, H, scale, colpart_q);                                                             \
+    else                                                                                                            \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, out, lse, delta, lens,  \
+                         dqkv, S, H, scale, colpart_q);                                                             \
     if (k2)                                                                                                         \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
                          dqkv, S, H, scale, colpart_kv);                                                            \
     else                                                                                                            \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
                          dqkv, S, H, scale, colpart_kv);                                                            \
-    if (q2)                                                                                                         \
-      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
-                         S, H, scale, colpart_q);                                                                   \
-    else                                                                                                            \
-      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, \
-                         S, H, scale, colpart_q);                                                                   \
   }
     if (ring == 3)
       MLT_RING_LAUNCH(3)
@@ -1114,6 +1144,8 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     if (rows_q) *rows_q = B * ((S + (q2 ? 127 : 63)) / (q2 ? 128 : 64));
     return colpart_q != nullptr && colpart_kv != nullptr;
   }
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
+                     (int64_t)B * S, H);
   if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, g2, dim3(256), 0, st, qkv, dout, lse, delta, lens, dqkv, S, H, scale);
   else

@@ -1078,6 +1078,54 @@ __global__ __launch_bounds__(256) void lenet_mpack(const float* __restrict__ p, 
   }
 }
 
+// Data-parallel step, after the all-reduce of the flat gradient: the optimizer update of every
+// element plus everything the per-sample kernel reads (bf16 shadow, conv fragment images, fc
+// transposed / padded images) in ONE launch -- the fused single-rank step's update path for
+// reduced gradients. `skip` (the transport's sticky error word) vetoes the whole update on this
+// rank (all-or-nothing step).
+template <class D>
+__global__ __launch_bounds__(256) void lenet_mapply(LeNetPtrs P, LeNetOpt O, const unsigned* __restrict__ skip) {
+  if (skip && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+  using F = Fc<D>;
+  constexpr int C1 = D::C1, F1 = D::F1, F2 = D::F2, FLAT = D::FLAT;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= O.n) return;
+  const int64_t step = P.stepinfo[0];
+  Ctx c;
+  c.on = true;
+  c.t = (float)(step + 1);
+  c.lr = __uint_as_float((unsigned)P.stepinfo[2]);
+  float p = O.p[e], a = O.s1 ? O.s1[e] : 0.f, s = O.s2 ? O.s2[e] : 0.f;
+  const float g = O.g[e];
+  opt_update(O.h, c.lr, c.t, p, g, a, s);
+  O.p[e] = p;
+  if (O.s1) O.s1[e] = a;
+  if (O.s2) O.s2[e] = s;
+  const uint16_t hb = f32_to_bf16(p);
+  P.shadow[e] = hb;
+  uint16_t* wi = P.wimg;
+  if (e >= O.off[0] && e < O.off[0] + D::C1 * 75) {
+    const int i = (int)(e - O.off[0]), oc = i / 75, tap = i - 75 * oc, ch = tap / 25, kh = (tap % 25) / 5, kw = tap % 5;
+    wi[w1f_slot(oc, ch, kh, kw, 0)] = hb;
+    wi[w1f_slot(oc, ch, kh, kw, 1)] = hb;
+  } else if (e >= O.off[2] && e < O.off[2] + D::C2 * C1 * 25) {
+    const int i = (int)(e - O.off[2]), oc = i / (C1 * 25), ic = (i / 25) % C1, tap = i % 25;
+    wi[w2f_slot(oc, ic, tap)] = hb;
+    wi[w2d_slot(oc, ic, tap, 0)] = hb;
+    wi[w2d_slot(oc, ic, tap, 1)] = hb;
+  } else if (e >= O.off[4] && e < O.off[4] + F1 * FLAT) {
+    const int i = (int)(e - O.off[4]), r = i / FLAT, cc = i - r * FLAT;
+    wi[kFc1T + cc * F1 + r] = hb;
+  } else if (e >= O.off[6] && e < O.off[6] + F2 * F1) {
+    const int i = (int)(e - O.off[6]), r = i / F1, cc = i - r * F1;
+    wi[kFc2T + cc * F::P2T + r] = hb;
+  } else if (e >= O.off[8] && e < O.off[8] + D::NC * F2) {
+    const int i = (int)(e - O.off[8]), r = i / F2, cc = i - r * F2;
+    wi[kFc3F + r * F::P3F + cc] = hb;
+    wi[kFc3T + cc * F::P3T + r] = hb;
+  }
+}
+
 template <class D>
 void pack(const LeNetPtrs& P, const LeNetOpt& O, hipStream_t st) {
   const int64_t tot = O.n > kWimgTot ? O.n : kWimgTot;
@@ -1100,6 +1148,15 @@ int lenet_mfma_wimg_elems() { return lm::kWimgTot; }
 int lenet_mfma_kw_blocks(int cfg) {
   return cfg == LENET_TINY ? lm::mw_conv_blocks<lm::DmTiny>() + lm::mw_fc_blocks<lm::DmTiny>() + 1
                            : lm::mw_conv_blocks<lm::DmDefault>() + lm::mw_fc_blocks<lm::DmDefault>() + 1;
+}
+
+void launch_lenet_mfma_apply(int cfg, const LeNetPtrs& P, const LeNetOpt& O, const unsigned* skip, hipStream_t stream) {
+  if (O.n <= 0) return;
+  const dim3 grid((unsigned)((O.n + 255) / 256));
+  if (cfg == LENET_TINY)
+    hipLaunchKernelGGL(lm::lenet_mapply<lm::DmTiny>, grid, dim3(256), 0, stream, P, O, skip);
+  else
+    hipLaunchKernelGGL(lm::lenet_mapply<lm::DmDefault>, grid, dim3(256), 0, stream, P, O, skip);
 }
 
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream) {
