@@ -36,10 +36,11 @@ eng.start_epoch(torch.randperm(N))
 eng.train_steps(B, 20, use_graph=False)
 C = eng.C
 # stamp slots in kernel order (lenet_mfma.hip stamp(k)); a name per interval
-idx = [0, 16, 17, 1, 2, 3, 18, 19, 4, 20, 21, 22, 5, 6, 7, 13]
+idx = [0, 16, 17, 1, 2, 3, 18, 19, 4, 20, 21, 22, 5, 6, 7, 23, 24, 13]
 names = ["P0 loads issued (+ctrl/meta scalar wait)", "P1 zero fill + raw image to LDS", "P1 augment -> xh/xc",
          "P2 conv1", "P3 conv2", "P4 fc1 fwd", "P4 fc2 fwd", "P4 fc3 fwd + softmax-CE", "P6 fc3 dgrad",
-         "P7 fc2 dgrad", "-", "P8 fc1 dgrad", "P10 unpool", "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad + slabs"]
+         "P7 fc2 dgrad", "-", "P8 fc1 dgrad", "P10 unpool", "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad MFMAs",
+         "P13 partial sums + slab stores", "end-of-kernel stores"]
 rows = []
 for rep in range(9):
     eng.eng.run(C.LENET_FWD | C.LENET_CE | C.LENET_BWD | C.LENET_TRACE, B)

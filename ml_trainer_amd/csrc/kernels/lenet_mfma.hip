@@ -36,6 +36,8 @@
 //   conv1 wgrad M = (kw | c, kh) taps (+ ones row), N = out channel, K = the 28x32 positions of the
 //               unpooled conv1 gradient; split over 3 K-ranges, summed in a fixed order
 // All batch reductions (KW) run in sample order: results are bitwise reproducible run to run.
+#include <type_traits>
+
 #include "mlt_common.h"
 #include "mlt_kernels.h"
 #include "mlt_optim.h"
@@ -152,6 +154,7 @@ constexpr int DCHS = 19;         // [Y+4][X+4][oc16] padded conv2-output grad: p
 constexpr int DCCS = 24;         // [oc][Y][X] conv2-output grad: row stride (conv2 wgrad B, 1-way)
 constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel stride (conv1 wgrad B, 1-way vs 5)
 constexpr int kWgT = 256;        // KW threads
+constexpr int kP13W = 7;         // conv1 wgrad waves (28 output rows / 4 each)
 
 // ---------------------------------------------------------------------------
 // fc layers on the matrix cores: y = W x for ONE sample, its input row x (bf16 in LDS, zero past K
@@ -208,7 +211,7 @@ struct Fc {
 template <class D>
 struct KsLds {
   using F = Fc<D>;
-  static constexpr int SCR = 3 * 5 * 256;
+  static constexpr int SCR = kP13W * 5 * 256;
   // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
   // MFMA fragment reads
   alignas(16) uint16_t p1h[14 * P1HS * 8];           // pooled conv1 [y][x][ic8]
@@ -236,7 +239,7 @@ struct KsLds {
   alignas(16) float sdh2[D::F2];
   alignas(16) float slog[64];
   alignas(16) float sdl[64];
-  alignas(16) float scr[SCR];                        // conv1 wgrad partials
+  alignas(16) float scr[SCR];                        // conv1 wgrad row-range partials
   alignas(16) float f32[D::FLAT];                    // flattened pooled conv2, fp32 (stored for the fc1 wgrad)
   unsigned long long tr[32];                         // LENET_TRACE stamps
   double ce[2];                                      // this sample's (loss / B, hit / B)
@@ -704,74 +707,89 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     const int t0 = w - 7, t1 = w == 7 ? 2 : w - 6;
     for (int tt0 = t0; tt0 < t1; ++tt0) {
       const int tt = w == 7 && tt0 == 1 ? 9 : tt0;
-      const int kw = tt >> 1, h = tt & 1, i = 16 * h + m, ic = i / 5, kh = i - 5 * ic;
-      const bool valid = ic < C1, ones = tt == 1 && m == 15;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      // the window shift kw is wave-uniform: one dispatch per tile, then a branch-free unrolled
+      // K loop with the shift as a compile-time constant (a switch inside the loop cost a branch
+      // and an lgkmcnt(0) wait per step)
+      auto tile = [&](auto KWc) __attribute__((always_inline)) {
+        constexpr int kw = decltype(KWc)::value;
+        const int h = tt & 1, i = 16 * h + m, ic = i / 5, kh = i - 5 * ic;
+        const bool valid = ic < C1, ones = tt == 1 && m == 15;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 5; ++s) {
-        const int y = 2 * s + (g >> 1), x0 = 8 * (g & 1);
-        const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * DCCS + x0);
-        const uint16_t* rowp = L.p1c + ((valid ? ic : 0) * 14 + y + (valid ? kh : 0)) * P1CS + x0;
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp), hi = *reinterpret_cast<const u32x4*>(rowp + 8);
-        u32x4 a;
-        switch (kw) {
-          case 0: a = fshift<0>(lo, hi); break;
-          case 1: a = fshift<1>(lo, hi); break;
-          case 2: a = fshift<2>(lo, hi); break;
-          case 3: a = fshift<3>(lo, hi); break;
-          default: a = fshift<4>(lo, hi); break;
+        for (int s = 0; s < 5; ++s) {
+          const int y = 2 * s + (g >> 1), x0 = 8 * (g & 1);
+          const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * DCCS + x0);
+          const uint16_t* rowp = L.p1c + ((valid ? ic : 0) * 14 + y + (valid ? kh : 0)) * P1CS + x0;
+          const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp), hi = *reinterpret_cast<const u32x4*>(rowp + 8);
+          u32x4 a = fshift<kw>(lo, hi);
+          if (!valid) a = ones ? u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u32x4{0u, 0u, 0u, 0u};
+          acc = mfma(a, bq, acc);
         }
-        if (!valid) a = ones ? u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u32x4{0u, 0u, 0u, 0u};
-        acc = mfma(a, bq, acc);
-      }
-      const int oc = m;
+        const int oc = m;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ir = 16 * h + 4 * g + r, icr = ir / 5, khr = ir - 5 * icr;
-        if (oc < C2 && icr < C1) slab[D::S2OFF + (oc * C1 + icr) * 25 + khr * 5 + kw] = acc[r];
-        if (oc < C2 && tt == 1 && ir == 31) slab[D::S2OFF + C2 * C1 * 25 + oc] = acc[r];
+        for (int r = 0; r < 4; ++r) {
+          const int ir = 16 * h + 4 * g + r, icr = ir / 5, khr = ir - 5 * icr;
+          if (oc < C2 && icr < C1) slab[D::S2OFF + (oc * C1 + icr) * 25 + khr * 5 + kw] = acc[r];
+          if (oc < C2 && tt == 1 && ir == 31) slab[D::S2OFF + C2 * C1 * 25 + oc] = acc[r];
+        }
+      };
+      switch (tt >> 1) {
+        case 0: tile(std::integral_constant<int, 0>{}); break;
+        case 1: tile(std::integral_constant<int, 1>{}); break;
+        case 2: tile(std::integral_constant<int, 2>{}); break;
+        case 3: tile(std::integral_constant<int, 3>{}); break;
+        default: tile(std::integral_constant<int, 4>{}); break;
       }
     }
   }
   lbar();
   stamp(7);
 
-  // ---- P13: conv1 wgrad (waves 0-14: tile kw = w / 3, K range w % 3) ---------------------------
-  //           next-step staging (wave 15)
-  if (w < 15) {
-    const int kw = w / 3, kp = w - 3 * kw, c = m / 5, kh = m - 5 * c;
-    const bool valid = m < 15, ones = m == 15 && kw == 0;
-    const int ya = 10 * kp, yb = min(ya + 10, 28), x0 = 8 * g;
+  // ---- P13: conv1 wgrad (waves 0-6: 4 output rows Y each, all 5 kw tiles) ---------------------
+  // One read of the input rows (lo / hi) and of the gradient row feeds the five kw-shifted
+  // windows' MFMAs: 84 operand reads in all (450 with one tile per wave); the 7 row-range partials
+  // are summed in a fixed order.
+  if (w < kP13W) {
+    const int c = m / 5, kh = m - 5 * c;
+    const bool valid = m < 15;
+    const int x0 = 8 * g;
     const uint16_t* xrow = L.xc + ((valid ? c : 0) * 32 + (valid ? kh : 0)) * XCS + x0;
     const uint16_t* drow = L.d1 + min(m, C1 - 1) * D1S + x0;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int Y = ya; Y < yb; ++Y) {
+    constexpr u32x4 ONES = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bias row (m = 15, kw = 0)
+    const u32x4 Z = {0u, 0u, 0u, 0u};
+    f32x4 acc[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int yy = 0; yy < 28 / kP13W; ++yy) {
+      const int Y = (28 / kP13W) * w + yy;
       u32x4 bq = *reinterpret_cast<const u32x4*>(drow + Y * 32);
-      if (m >= C1) bq = u32x4{0u, 0u, 0u, 0u};
+      if (m >= C1) bq = Z;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xrow + Y * XCS), hi = *reinterpret_cast<const u32x4*>(xrow + Y * XCS + 8);
-      u32x4 a;
-      switch (kw) {
-        case 0: a = fshift<0>(lo, hi); break;
-        case 1: a = fshift<1>(lo, hi); break;
-        case 2: a = fshift<2>(lo, hi); break;
-        case 3: a = fshift<3>(lo, hi); break;
-        default: a = fshift<4>(lo, hi); break;
-      }
-      if (!valid) a = ones ? u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u32x4{0u, 0u, 0u, 0u};
-      acc = mfma(a, bq, acc);
+      acc[0] = mfma(valid ? fshift<0>(lo, hi) : (m == 15 ? ONES : Z), bq, acc[0]);
+      acc[1] = mfma(valid ? fshift<1>(lo, hi) : Z, bq, acc[1]);
+      acc[2] = mfma(valid ? fshift<2>(lo, hi) : Z, bq, acc[2]);
+      acc[3] = mfma(valid ? fshift<3>(lo, hi) : Z, bq, acc[3]);
+      acc[4] = mfma(valid ? fshift<4>(lo, hi) : Z, bq, acc[4]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) L.scr[((kp * 5 + kw) * 16 + 4 * g + r) * 16 + m] = acc[r];
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L.scr[((w * 5 + kw) * 16 + 4 * g + r) * 16 + m] = acc[kw][r];
   }
   lbar();
+  stamp(23);
   for (int e = t; e < 5 * 256; e += kT) {
     const int kw = e >> 8, i = (e >> 4) & 15, oc = e & 15;
-    const float v = (L.scr[e] + L.scr[1280 + e]) + L.scr[2560 + e];
+    float v = L.scr[e];
+#pragma unroll
+    for (int p = 1; p < kP13W; ++p) v += L.scr[p * 1280 + e];
     if (oc < C1) {
       if (i < 15) slab[oc * 76 + (i / 5) * 25 + (i % 5) * 5 + kw] = v;
       else if (kw == 0) slab[oc * 76 + 75] = v;
     }
   }
+  stamp(24);
   static_assert(F1 <= 128 && F2 <= 128 && NC <= 64, "end-of-kernel store mapping");
   // activations / gradients for the batch reductions of KW (and inspection), all stored here: no
   // load of this kernel is waited for after this point
