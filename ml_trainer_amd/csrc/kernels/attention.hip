@@ -787,6 +787,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
                       : bf16x8{};
     }
   }
+  const bool kfull = k0b + 64 * NK <= len;  // block-uniform: no key of this block is masked
   float sl2k[NK], kinf[NK];  // masked keys: scale 0 and +inf shift -> exp2(-inf) = 0
 #pragma unroll
   for (int n = 0; n < NK; ++n) {
@@ -837,7 +838,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
       const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
       const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
       const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
-      if (qfull) {  // key mask folded into per-lane constants: x = s * sl2k - (lse + kinf)
+      if (qfull && kfull) {  // every key of the block valid: x = s * sl2 - lse (one fma per score)
+#pragma unroll
+        for (int n = 0; n < NK; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = fast_exp2(sv[n][r] * sl2 - lr[r]);
+            p[n][qt][r] = pv;
+            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
+          }
+      } else if (qfull) {  // key mask folded into per-lane constants: x = s * sl2k - (lse + kinf)
 #pragma unroll
         for (int n = 0; n < NK; ++n)
 #pragma unroll
@@ -1012,6 +1022,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
     if (kb + kRing - 1 < nkb) issue((kb + kRing - 1) % kRing, kb + kRing - 1);
     const uint8_t* Ks = smem + (kb % kRing) * STAGE;
     const uint8_t* Vs = Ks + kTile;
+    const bool kfull = (kb + 1) * AB <= len;
     f32x4 ds[NQ][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -1030,14 +1041,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
           dp[n] = mfma(va, of[n][kh], dp[n]);
         }
       }
+      if (kfull) {  // block-uniform: every key of this block is valid
 #pragma unroll
-      for (int n = 0; n < NQ; ++n)
+        for (int n = 0; n < NQ; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * AB + kt * 16 + 4 * g + r;
-          const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
-          ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
-        }
+          for (int r = 0; r < 4; ++r) {
+            const float pv = fast_exp2(sv[n][r] * sl2 - lq[n]);
+            ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+          }
+      } else {
+#pragma unroll
+        for (int n = 0; n < NQ; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb * AB + kt * 16 + 4 * g + r;
+            const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
+            ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+          }
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
