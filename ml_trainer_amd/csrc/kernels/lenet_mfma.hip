@@ -155,6 +155,7 @@ constexpr int DCCS = 24;         // [oc][Y][X] conv2-output grad: row stride (co
 constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel stride (conv1 wgrad B, 1-way vs 5)
 constexpr int kWgT = 256;        // KW threads
 constexpr int kP13W = 7;         // conv1 wgrad waves (28 output rows / 4 each)
+constexpr int kC1W = 8;          // conv1 forward waves (the fc1 forward waves 8-15 fetch weights meanwhile)
 
 // ---------------------------------------------------------------------------
 // fc layers on the matrix cores: y = W x for ONE sample, its input row x (bf16 in LDS, zero past K
@@ -436,14 +437,16 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   // ---- P2: conv1 (MFMA) + bias + ReLU + maxpool in registers -> p1 images, i1 ------------------
   // M = (pooled cell, window y) rows, N = (out channel, window x) columns, K = (kh, x pair, c4): a
   // lane's accumulators are the window rows of two cells, the partner lane (n ^ 1) holds the other
-  // window column. 25 tiles x 4 k-steps; B fragments (4 x 16 B per lane) read once per wave.
+  // window column. 25 tiles x 4 k-steps on waves 0-7; B fragments (4 x 16 B per lane) read once per wave.
   {
     u32x4 bw[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) bw[s] = *reinterpret_cast<const u32x4*>(L.w1f + (s * 64 + lane) * 8);
     const int a = m >> 2, r = m & 3, dx = m & 1, oc = m >> 1;
     const float bias = L.b1s[min(oc, 15)];
-    for (int T = w; T < 25; T += 16) {
+    // tiles on waves 0 .. kC1W-1 only: the other waves spend this phase issuing the fc1 forward
+    // weight fetch (~100 KB, load_fc above), whose queueing would otherwise delay their tiles
+    for (int T = w; w < kC1W && T < 25; T += kC1W) {
       const int cell = min(8 * T + 2 * a + (r >> 1), 195);
       const int py = cell / 14, pxx = cell - 14 * py, Y = 2 * py + (r & 1);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
