@@ -3,11 +3,17 @@
 //
 //   KS  lenet_ms<D>  grid B x 1024 threads, one CU per sample, the whole per-sample chain in LDS:
 //       [staged / augmented input] -> conv1 (MFMA) + bias + ReLU + maxpool -> conv2 (MFMA) + bias +
-//       ReLU + maxpool -> fc1 / fc2 / fc3 (+ReLU) -> softmax-CE -> fc dgrad chain -> unpool2 ->
-//       conv2 dgrad (MFMA) -> pool1 liveness mask -> conv2 wgrad (MFMA) and conv1 wgrad (MFMA) of
-//       the sample -> per-sample weight-gradient slab; + the NEXT step's raw input image gathered
-//       (epoch permutation -> dataset row) and staged by an otherwise idle wave, so the next step
-//       starts with one round trip instead of ctrl -> perm -> image.
+//       ReLU + maxpool -> fc1 / fc2 / fc3 (+ReLU, MFMA) -> softmax-CE -> fc dgrad chain (MFMA) ->
+//       unpool2 -> conv2 dgrad (MFMA) -> pool1 liveness mask -> conv2 wgrad (MFMA) and conv1 wgrad
+//       (MFMA) of the sample -> per-sample weight-gradient slab; + the NEXT step's raw input image
+//       gathered (epoch permutation -> dataset row) and staged by an otherwise idle wave, so the
+//       next step starts with one round trip instead of ctrl -> perm -> image.
+//       The ~250 KB of fc weight fragments a CU fetches per step are the other cost besides the
+//       latency chain (a CU's vector memory path moves ~35 B/clk and a wave stalls while its loads
+//       queue), so fetches go to waves without work in that phase: waves 8-15 fetch fc1 while 0-7
+//       run conv1; from conv2 to the fc1 dgrad the waves form two roles (two branches with the
+//       same barrier sequence): 0-7 fetch and run the fc dgrad chain, 8-15 run conv2, the forward
+//       chain and the CE.
 //   KW  lenet_mw<D>  role-split grid: conv slab sums over the batch (sample order), fc weight
 //       gradients over the batch (exact-f32 MFMA tiles, sample-ordered), the fused optimizer update
 //       (fp32 masters + bf16 shadow + the per-sample kernel's fragment images), the fixed-order loss
@@ -197,6 +203,7 @@ __device__ __forceinline__ float row_dot(const u32x4 (&f)[KS], const uint16_t* x
 template <class D>
 struct Fc {
   static constexpr int T1 = (D::F1 + 15) / 16, K1 = (D::FLAT + 31) / 32, W1F = 16 - T1;  // fc1 fwd
+  static_assert(W1F >= 8, "fc1 forward runs on the role-B waves 8-15");
   static constexpr int T2 = (D::F2 + 15) / 16, K2 = (D::F1 + 31) / 32, W2F = 8;           // fc2 fwd
   static constexpr int K3 = (D::F2 + 31) / 32, W3F = 14;                                  // fc3 fwd
   static constexpr int B3T = (D::F2 + 15) / 16, B3K = (D::NC + 31) / 32;                  // fc3 dgrad
@@ -481,166 +488,203 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   stamp(2);
 
   const uint4 wid = wimg4[WIF + min(t, WID - 1)];  // conv2 dgrad fragments (to LDS in P10)
-  u32x4 f2w[F1M::K2], f3w[F1M::K3];  // fc2 fwd (waves 8-13) / fc3 fwd (wave 14, fetched in P4) B fragments
-  if (w >= F1M::W2F && w < F1M::W2F + F1M::T2)
-    frag_rows<F1M::K2, F1, F2, F1>(f2w, P.shadow + O.off[6], w - F1M::W2F);
-  // next-step staging (wave 15, two steps deep so that no load waits on another inside this kernel):
-  // metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1; when it
-  // matches, the raw image of step + 1 is gathered now (stored to stage2 in P10). The perm entry
-  // for step + 2 is looked up here and published to metaN in P10. A mismatch (epoch start, new
-  // permutation, ...) stages nothing: the next step then gathers its images itself. All vector
-  // loads, first waited for in P10.
-  int64_t pos1 = 0, pos2 = 0, idx1 = 0;
-  bool st1 = false;
-  int nperm2v = 0;
-  long long ntgtv = 0;
-  uint4 nraw0 = make_uint4(0u, 0u, 0u, 0u), nraw1 = nraw0, nraw2 = nraw0;
-  if (stage_on) {
-    pos1 = (sie + 1) * A.batch_stride + b;
-    if (pos1 >= A.perm_len) pos1 %= A.perm_len;
-    pos2 = (sie + 2) * A.batch_stride + b;
-    if (pos2 >= A.perm_len) pos2 %= A.perm_len;
-    nperm2v = A.perm[pos2];
-    auto rfl64 = [](long long v) {
-      return (int64_t)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)((uint64_t)v >> 32)) << 32) |
-                       (unsigned)__builtin_amdgcn_readfirstlane((int)v));
-    };
-    const int64_t sN = rfl64(mN01.x), pN = rfl64(mN01.y), iN = rfl64(mN2);
-    st1 = sN == step + 1 && pN == pos1 && iN >= 0 && iN < A.n;
-    if (st1) {
-      idx1 = iN;
-      const uint4* src = reinterpret_cast<const uint4*>(A.data + idx1 * 3072);
-      nraw0 = src[lane];
-      nraw1 = src[lane + 64];
-      nraw2 = src[lane + 128];
-      ntgtv = P.dtargets[idx1];
-    }
-  }
 
-  // ---- P3: conv2 (MFMA) + bias + ReLU + maxpool -> f (flatten order oc*25 + cell), i2 ----------
-  if (w < 7) {
-    const int r = 16 * w + m, cell = min(r >> 2, 24), q = r & 3;
-    const int py = cell / 5, pxx = cell - 5 * py, y = 2 * py + (q >> 1), x = 2 * pxx + (q & 1);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      const int tap = 4 * s + g, kh = tap / 5, kw = tap - 5 * kh;
-      u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * P1HS + x + kw : 0)) * 8);
-      if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
-      acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2f + (s * 64 + lane) * 8), acc);
-    }
-    const int cc = 4 * w + g, oc = m;
-    float pv;
-    uint8_t code;
-    pool4(acc, L.b2s[oc], pv, code);
-    if (cc < 25 && oc < C2) {
-      const int o = oc * 25 + cc;
-      L.fb16[o] = f32_to_bf16(pv);
-      L.f32[o] = pv;
-      L.i2[o] = code;
-    }
-  }
-  lbar();
-  stamp(3);
-
-  // ---- P4-P9: fc1 -> fc2 -> fc3 + softmax-CE -> fc dgrad chain, all on the matrix cores -------
-  if (w >= F1M::W1F) {  // fc1 forward
-    const int r = 16 * (w - F1M::W1F) + m;
-    const float v = row_dot(f1w, L.fb16);
-    if (g == 0 && r < F1) {
-      const float h = fmaxf(v + L.fb[r], 0.f);
-      L.sh1[r] = h;
-      L.h1b[r] = f32_to_bf16(h);
-    }
-  }
-  // dgrad fragments of waves 0-7 (first needed first: vmcnt retires in issue order)
-  u32x4 f3t[F1M::B3K], f2t[F1M::B2K], f1t[F1M::B1P][F1M::B1K];
+  // ---- P3-P8 as two wave roles (the same barrier sequence in both) ------------------------------
+  // waves 0-7 fetch the fc dgrad fragments during conv2 and run the dgrad chain; waves 8-15 run
+  // conv2, the forward fc chain and the softmax-CE and do the next-step staging (wave 15). As two
+  // branches, each role's register-resident fragments share registers with the other's.
   if (w < 8) {
+    // ---- role A: fc dgrad ----
+    u32x4 f3t[F1M::B3K], f2t[F1M::B2K], f1t[F1M::B1P][F1M::B1K];  // first needed first (vmcnt order)
     if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, P.wimg + kFc3T, w);
     if (w < F1M::B2T) frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
 #pragma unroll
     for (int j = 0; j < F1M::B1P; ++j) frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[j], P.wimg + kFc1T, w + 8 * j);
-  }
-  lbar();
-  stamp(18);
-  if (w == 15 && F1M::B1T > 8 * F1M::B1P)  // the 25th fc1 dgrad tile (wave 15 idles in fc2 / fc3)
-    frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[0], P.wimg + kFc1T, 8 * F1M::B1P);
-  if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, P.wimg + kFc3F, 0);
-  if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // fc2 forward
-    const int r = 16 * (w - F1M::W2F) + m;
-    const float v = row_dot(f2w, L.h1b);
-    if (g == 0 && r < F2) {
-      const float h = fmaxf(v + L.fb[F1 + r], 0.f);
-      L.sh2[r] = h;
-      L.h2b[r] = f32_to_bf16(h);
+    lbar();  // P3 (conv2)
+    stamp(3);
+    lbar();  // P4a (fc1 forward)
+    stamp(18);
+    lbar();  // P4b (fc2 forward)
+    stamp(19);
+    lbar();  // P4c (fc3 forward + CE)
+    stamp(4);
+    if (w < F1M::B3T) {  // fc3 dgrad (x the fc2 ReLU mask)
+      const int k = 16 * w + m;
+      const float v = row_dot(f3t, L.dlb);
+      if (g == 0 && k < F2) {
+        const float d = L.sh2[k] > 0.f ? v : 0.f;
+        L.sdh2[k] = d;
+        L.dh2b[k] = f32_to_bf16(d);
+      }
     }
-  }
-  lbar();
-  stamp(19);
-  if (w == F1M::W3F) {  // fc3 forward + softmax-CE in one wave (the logits are in lanes 0 .. NC-1)
-    const float v = row_dot(f3w, L.h2b);
-    constexpr int GC = pow2_ge(NC);
-    const float z = lane < NC ? v + L.fb[F1 + F2 + lane] : -INFINITY;
-    const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC, true>(z)), GC - 1));
-    const float e = lane < NC ? expf(z - mx) : 0.f;
-    const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC>(e)), GC - 1));
-    const float lse = mx + logf(s);
-    const bool valid = tgt >= 0 && tgt < NC;
-    const unsigned long long am_mask = __ballot(lane < NC && z == mx);
-    const int am = __ffsll((long long)am_mask) - 1;
-    const float zt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), valid ? (int)tgt : 0));
-    const float loss = valid ? lse - zt : 0.f;
-    if (lane < NC) {
-      const float dl = valid ? (e / s - (lane == tgt ? 1.f : 0.f)) * inv_B : 0.f;
-      L.slog[lane] = z;
-      L.sdl[lane] = dl;
-      L.dlb[lane] = f32_to_bf16(dl);
+    lbar();
+    stamp(20);
+    if (w < F1M::B2T) {  // fc2 dgrad (x the fc1 ReLU mask)
+      const int k = 16 * w + m;
+      const float v = row_dot(f2t, L.dh2b);
+      if (g == 0 && k < F1) {
+        const float d = L.sh1[k] > 0.f ? v : 0.f;
+        L.sdh1[k] = d;
+        L.dh1b[k] = f32_to_bf16(d);
+      }
     }
-    if (lane == 0) {
-      L.ce[0] = (double)loss * (double)inv_B;
-      L.ce[1] = (am == tgt) ? (double)inv_B : 0.0;
-    }
-  }
-  lbar();
-  stamp(4);
-  if (w < F1M::B3T) {  // fc3 dgrad (x the fc2 ReLU mask)
-    const int k = 16 * w + m;
-    const float v = row_dot(f3t, L.dlb);
-    if (g == 0 && k < F2) {
-      const float d = L.sh2[k] > 0.f ? v : 0.f;
-      L.sdh2[k] = d;
-      L.dh2b[k] = f32_to_bf16(d);
-    }
-  }
-  lbar();
-  stamp(20);
-  if (w < F1M::B2T) {  // fc2 dgrad (x the fc1 ReLU mask)
-    const int k = 16 * w + m;
-    const float v = row_dot(f2t, L.dh2b);
-    if (g == 0 && k < F1) {
-      const float d = L.sh1[k] > 0.f ? v : 0.f;
-      L.sdh1[k] = d;
-      L.dh1b[k] = f32_to_bf16(d);
-    }
-  }
-  lbar();
-  stamp(21);
-  stamp(22);
-  // fc1 dgrad -> the flattened pooled-conv2 gradient
-  if (w < 8) {
+    lbar();
+    stamp(21);
+    stamp(22);
 #pragma unroll
-    for (int j = 0; j < F1M::B1P; ++j) {
+    for (int j = 0; j < F1M::B1P; ++j) {  // fc1 dgrad -> the flattened pooled-conv2 gradient
       const int c = 16 * (w + 8 * j) + m;
       const float v = row_dot(f1t[j], L.dh1b);
       if (g == 0 && c < FLAT) L.df[c] = v;
     }
-  } else if (w == 15 && F1M::B1T > 8 * F1M::B1P) {
-    const int c = 16 * (8 * F1M::B1P) + m;
-    const float v = row_dot(f1t[0], L.dh1b);
-    if (g == 0 && c < FLAT) L.df[c] = v;
+    lbar();
+    stamp(5);
+  } else {
+    // ---- role B: conv2, forward fc chain, softmax-CE, next-step staging ----
+    u32x4 f2w[F1M::K2], f3w[F1M::K3], f1tx[F1M::B1K];
+    if (w >= F1M::W2F && w < F1M::W2F + F1M::T2)
+      frag_rows<F1M::K2, F1, F2, F1>(f2w, P.shadow + O.off[6], w - F1M::W2F);
+    // next-step staging (wave 15, two steps deep so that no load waits on another inside this
+    // kernel): metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1;
+    // when it matches, the raw image of step + 1 is gathered now (stored to stage2 at the end of
+    // this role). The perm entry for step + 2 is looked up here and published to metaN. A mismatch
+    // (epoch start, new permutation, ...) stages nothing: the next step then gathers its images
+    // itself. All vector loads, waited for after the fc chain.
+    int64_t pos1 = 0, pos2 = 0, idx1 = 0;
+    bool st1 = false;
+    int nperm2v = 0;
+    long long ntgtv = 0;
+    uint4 nraw0 = make_uint4(0u, 0u, 0u, 0u), nraw1 = nraw0, nraw2 = nraw0;
+    if (stage_on) {
+      pos1 = (sie + 1) * A.batch_stride + b;
+      if (pos1 >= A.perm_len) pos1 %= A.perm_len;
+      pos2 = (sie + 2) * A.batch_stride + b;
+      if (pos2 >= A.perm_len) pos2 %= A.perm_len;
+      nperm2v = A.perm[pos2];
+      auto rfl64 = [](long long v) {
+        return (int64_t)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)((uint64_t)v >> 32)) << 32) |
+                         (unsigned)__builtin_amdgcn_readfirstlane((int)v));
+      };
+      const int64_t sN = rfl64(mN01.x), pN = rfl64(mN01.y), iN = rfl64(mN2);
+      st1 = sN == step + 1 && pN == pos1 && iN >= 0 && iN < A.n;
+      if (st1) {
+        idx1 = iN;
+        const uint4* src = reinterpret_cast<const uint4*>(A.data + idx1 * 3072);
+        nraw0 = src[lane];
+        nraw1 = src[lane + 64];
+        nraw2 = src[lane + 128];
+        ntgtv = P.dtargets[idx1];
+      }
+    }
+    // P3: conv2 (MFMA) + bias + ReLU + maxpool -> f (flatten order oc*25 + cell), i2 (waves 8-14)
+    if (w < 15) {
+      const int wt = w - 8;
+      const int r = 16 * wt + m, cell = min(r >> 2, 24), q = r & 3;
+      const int py = cell / 5, pxx = cell - 5 * py, y = 2 * py + (q >> 1), x = 2 * pxx + (q & 1);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        const int tap = 4 * s + g, kh = tap / 5, kw = tap - 5 * kh;
+        u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * P1HS + x + kw : 0)) * 8);
+        if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
+        acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2f + (s * 64 + lane) * 8), acc);
+      }
+      const int cc = 4 * wt + g, oc = m;
+      float pv;
+      uint8_t code;
+      pool4(acc, L.b2s[oc], pv, code);
+      if (cc < 25 && oc < C2) {
+        const int o = oc * 25 + cc;
+        L.fb16[o] = f32_to_bf16(pv);
+        L.f32[o] = pv;
+        L.i2[o] = code;
+      }
+    }
+    lbar();
+    stamp(3);
+    if (w >= F1M::W1F) {  // P4a: fc1 forward (the last T1 waves)
+      const int r = 16 * (w - F1M::W1F) + m;
+      const float v = row_dot(f1w, L.fb16);
+      if (g == 0 && r < F1) {
+        const float h = fmaxf(v + L.fb[r], 0.f);
+        L.sh1[r] = h;
+        L.h1b[r] = f32_to_bf16(h);
+      }
+    }
+    lbar();
+    stamp(18);
+    if (w == 15 && F1M::B1T > 8 * F1M::B1P)  // the 25th fc1 dgrad tile (wave 15 idles in fc2 / fc3)
+      frag_rows<F1M::B1K, F1, FLAT, F1>(f1tx, P.wimg + kFc1T, 8 * F1M::B1P);
+    if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, P.wimg + kFc3F, 0);
+    if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // P4b: fc2 forward
+      const int r = 16 * (w - F1M::W2F) + m;
+      const float v = row_dot(f2w, L.h1b);
+      if (g == 0 && r < F2) {
+        const float h = fmaxf(v + L.fb[F1 + r], 0.f);
+        L.sh2[r] = h;
+        L.h2b[r] = f32_to_bf16(h);
+      }
+    }
+    lbar();
+    stamp(19);
+    if (w == F1M::W3F) {  // P4c: fc3 forward + softmax-CE in one wave (the logits are in lanes 0 .. NC-1)
+      const float v = row_dot(f3w, L.h2b);
+      constexpr int GC = pow2_ge(NC);
+      const float z = lane < NC ? v + L.fb[F1 + F2 + lane] : -INFINITY;
+      const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC, true>(z)), GC - 1));
+      const float e = lane < NC ? expf(z - mx) : 0.f;
+      const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group_reduce_last<GC>(e)), GC - 1));
+      const float lse = mx + logf(s);
+      const bool valid = tgt >= 0 && tgt < NC;
+      const unsigned long long am_mask = __ballot(lane < NC && z == mx);
+      const int am = __ffsll((long long)am_mask) - 1;
+      const float zt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), valid ? (int)tgt : 0));
+      const float loss = valid ? lse - zt : 0.f;
+      if (lane < NC) {
+        const float dl = valid ? (e / s - (lane == tgt ? 1.f : 0.f)) * inv_B : 0.f;
+        L.slog[lane] = z;
+        L.sdl[lane] = dl;
+        L.dlb[lane] = f32_to_bf16(dl);
+      }
+      if (lane == 0) {
+        L.ce[0] = (double)loss * (double)inv_B;
+        L.ce[1] = (am == tgt) ? (double)inv_B : 0.0;
+      }
+    }
+    lbar();
+    stamp(4);
+    lbar();  // P5 (fc3 dgrad)
+    stamp(20);
+    lbar();  // P6 (fc2 dgrad)
+    stamp(21);
+    stamp(22);
+    if (w == 15 && F1M::B1T > 8 * F1M::B1P) {  // P8: the 25th fc1 dgrad tile
+      const int c = 16 * (8 * F1M::B1P) + m;
+      const float v = row_dot(f1tx, L.dh1b);
+      if (g == 0 && c < FLAT) L.df[c] = v;
+    }
+    if (stage_on) {  // wave 15: publish the next step's raw image + tags
+      if (st1) {
+        uint4* dst = reinterpret_cast<uint4*>(P.stage2 + (int64_t)b * 3072);
+        dst[lane] = nraw0;
+        dst[lane + 64] = nraw1;
+        dst[lane + 128] = nraw2;
+      }
+      if (lane == 0) {
+        if (st1) {
+          P.meta2[4 * b] = step + 1;
+          P.meta2[4 * b + 1] = pos1;
+          P.meta2[4 * b + 2] = idx1;
+          P.meta2[4 * b + 3] = ntgtv;
+        }
+        P.metaN[4 * b] = step + 2;
+        P.metaN[4 * b + 1] = pos2;
+        P.metaN[4 * b + 2] = nperm2v;
+      }
+    }
+    lbar();
+    stamp(5);
   }
-  lbar();
-  stamp(5);
 
   // ---- P10: unpool2 -> the conv2-output gradient images (zero except at arg-max cells) ---------
   if (t < WID) reinterpret_cast<uint4*>(L.w2d)[t] = wid;
@@ -652,25 +696,6 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
       const uint16_t v = f32_to_bf16(L.df[e]);
       L.dch[((Y + 4) * DCHS + X + 4) * 16 + oc] = v;
       L.dcc[(oc * 10 + Y) * DCCS + X] = v;
-    }
-  }
-  if (stage_on) {  // wave 15 (no unpool work): publish the next step's raw image + tags
-    if (st1) {
-      uint4* dst = reinterpret_cast<uint4*>(P.stage2 + (int64_t)b * 3072);
-      dst[lane] = nraw0;
-      dst[lane + 64] = nraw1;
-      dst[lane + 128] = nraw2;
-    }
-    if (lane == 0) {
-      if (st1) {
-        P.meta2[4 * b] = step + 1;
-        P.meta2[4 * b + 1] = pos1;
-        P.meta2[4 * b + 2] = idx1;
-        P.meta2[4 * b + 3] = ntgtv;
-      }
-      P.metaN[4 * b] = step + 2;
-      P.metaN[4 * b + 1] = pos2;
-      P.metaN[4 * b + 2] = nperm2v;
     }
   }
   lbar();
