@@ -45,6 +45,7 @@ def _fake_engine():
     e.eng = _FakeCEngine()
     e.world_size = 1
     e.dp_transport = "none"
+    e.precision = "fp32"
     e.captures = 0
     e.comm = e.xgmi = None
     return e
