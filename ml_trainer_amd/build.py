@@ -56,9 +56,18 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "include", "*.h"))
 
 
-def _newer(src: str, obj: str, deps) -> bool:
+def _newer(src: str, obj: str, deps, cmd=None) -> bool:
+    """Rebuild when the object is missing, older than its source or a header, or was compiled with
+    a different command line (``<obj>.cmd`` records the last one: a flag change rebuilds)."""
     if not os.path.exists(obj):
         return True
+    if cmd is not None:
+        try:
+            with open(obj + ".cmd") as f:
+                if f.read() != " ".join(cmd):
+                    return True
+        except OSError:
+            return True
     t = os.path.getmtime(obj)
     if os.path.getmtime(src) > t:
         return True
@@ -77,7 +86,10 @@ def _run(cmd):
 # register file is unified). By default hipcc puts them in AGPRs and copies every S^T tile to
 # VGPRs for the softmax VALU work and every O tile back and forth for the rescale (~80
 # v_accvgpr_read/write per 64-key block of the forward); the VGPR form removes those copies.
-FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds / muls of the softmax VALU work
+# into v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32, which cost more than two scalar ops when they
+# sit between MFMAs (MI355X_MICROARCH.md, "price of one filler beside MFMAs").
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
@@ -101,23 +113,26 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
     for s in kernel_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(s, o, hdrs):
-            jobs_list.append([HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common,
-                              "-munsafe-fp-atomics", "-Wno-unused-result",
-                              *FILE_FLAGS.get(os.path.basename(s), [])])
+        cmd = [HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common, "-munsafe-fp-atomics",
+               "-Wno-unused-result", *FILE_FLAGS.get(os.path.basename(s), [])]
+        if force or _newer(s, o, hdrs, cmd):
+            jobs_list.append(cmd)
     for s in host_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(s, o, hdrs):
-            jobs_list.append([HIPCC, "-c", s, "-o", o, *opt, *common, "-DTORCH_EXTENSION_NAME=_C",
-                              "-DTORCH_API_INCLUDE_EXTENSION_H", f"-I{pyinc}",
-                              f"-I{pybind11.get_include()}", *[f"-isystem{i}" for i in tinc],
-                              "-I/opt/rocm/include", "-Wno-deprecated-declarations", "-Wno-unused-result"])
+        cmd = [HIPCC, "-c", s, "-o", o, *opt, *common, "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               f"-I{pyinc}", f"-I{pybind11.get_include()}", *[f"-isystem{i}" for i in tinc], "-I/opt/rocm/include",
+               "-Wno-deprecated-declarations", "-Wno-unused-result"]
+        if force or _newer(s, o, hdrs, cmd):
+            jobs_list.append(cmd)
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             futs = {ex.submit(_run, c): c for c in jobs_list}
             for f in cf.as_completed(futs):
                 dt, _ = f.result()
+                c = futs[f]
+                with open(c[c.index("-o") + 1] + ".cmd", "w") as fh:  # the command that built it
+                    fh.write(" ".join(c))
                 if verbose:
                     src = futs[f][2]
                     print(f"[mlt-build] {os.path.relpath(src, REPO_DIR)}  {dt:.1f}s", flush=True)
