@@ -89,7 +89,8 @@ def _run(cmd):
 # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds / muls of the softmax VALU work
 # into v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32, which cost more than two scalar ops when they
 # sit between MFMAs (MI355X_MICROARCH.md, "price of one filler beside MFMAs").
-FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
+              "lenet_mfma.hip": ["-fno-slp-vectorize"]}
 
 
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
