@@ -14,7 +14,7 @@ CIFAR-shaped dataset and says so in the log.
 
 Extension flags (not in the reference): ``--model`` (default/tiny/bert-base/
 large), ``--synthetic``, ``--per_device_batch``, ``--no_engine``,
-``--no_parallel``, ``--resume``, ``--amp bf16``, ``--precision bf16``, ``--metrics_jsonl``, ``--log_jsonl``, ``--zero_stage``.
+``--no_parallel``, ``--resume``, ``--amp bf16``, ``--precision bf16``, ``--metrics_jsonl``, ``--log_jsonl``, ``--zero_stage``, ``--async_checkpoint``.
 """
 from __future__ import annotations
 
@@ -90,7 +90,7 @@ def main(args):
     options = {"per_device_batch": args.per_device_batch, "resume": args.resume,
                "metrics_jsonl": args.metrics_jsonl, "amp": args.amp, "progress": not args.no_progress,
                "precision": getattr(args, "precision", "fp32"),
-               "zero_stage": args.zero_stage}
+               "zero_stage": args.zero_stage, "async_checkpoint": args.async_checkpoint}
     if args.no_engine:
         options["use_engine"] = False
     if args.log_jsonl:  # every structured log record, one JSON object per line
@@ -137,6 +137,8 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--no_engine", action="store_true", help="disable the fused LeNet step engine")
     parser.add_argument("--no_parallel", action="store_true", help="do not initialise torch.distributed")
     parser.add_argument("--resume", action="store_true")
+    parser.add_argument("--async_checkpoint", action="store_true",
+                        help="write model.pth / trainer_state.pt from a pinned-host snapshot in a background thread")
     parser.add_argument("--zero_stage", type=int, default=0, choices=(0, 1),
                         help="1: ZeRO-1 sharded optimizer state (reduce-scatter / all-gather) under DDP")
     parser.add_argument("--amp", type=str, default=None, choices=[None, "bf16"])

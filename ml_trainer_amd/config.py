@@ -65,6 +65,8 @@ class TrainerOptions:
     # --- fault tolerance / checkpoints ---------------------------------------------------
     resume: bool = False                  # reload model.pth + trainer_state.pt from model_dir
     save_trainer_state: bool = True       # write trainer_state.pt (optimizer/scheduler/epoch/RNG) per epoch
+    async_checkpoint: bool = False        # model.pth from a pinned-host snapshot, written by a background
+                                          # thread (utils/checkpoint.AsyncCheckpointer); fit() waits at the end
     watchdog_s: Optional[float] = None    # >0: abort if no step progress this long / a collective fails
                                           # (None: 600 s for multi-rank jobs, off otherwise; 0: off)
     fault_inject_step: int = -1           # testing: raise at this global step on rank fault_inject_rank

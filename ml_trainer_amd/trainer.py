@@ -568,9 +568,26 @@ class Trainer:
         return self.evaluate(test_loader, model=model)
 
     # ------------------------------------------------------------------ artifacts
-    def save_model(self, model_dir):
+    def save_model(self, model_dir, trainer_state=None):
+        """model.pth (+ trainer_state.pt when given). With ``async_checkpoint`` both are written by
+        a background thread from host snapshots taken here, model.pth first."""
         logger.info("Saving the model.")
-        return ckpt.save_model_file(self.model, model_dir)
+        if self.opts.async_checkpoint:
+            if getattr(self, "_ackpt", None) is None:
+                self._ackpt = ckpt.AsyncCheckpointer()
+            path = os.path.join(model_dir, "model.pth")
+            extra = [] if trainer_state is None else [(os.path.join(model_dir, "trainer_state.pt"),
+                                                       ckpt.to_host(trainer_state))]
+            self._ackpt.save(self.model, path, extra)  # on disk by the next save / the end of fit()
+            return path
+        path = ckpt.save_model_file(self.model, model_dir)
+        if trainer_state is not None:
+            ckpt.save_trainer_state(trainer_state, model_dir)
+        return path
+
+    def _checkpoint_wait(self) -> None:
+        if getattr(self, "_ackpt", None) is not None:
+            self._ackpt.wait()
 
     def save_history_(self, model_dir):
         logger.info("Saving the training history.")
@@ -622,14 +639,12 @@ class Trainer:
             # ZeRO: gathering the sharded optimizer state is collective, so every rank builds it
             st = self._trainer_state(epoch) if (self.opts.save_trainer_state and self._zero is not None) else None
             if mdist.rank() == 0:
-                self.save_model(self.model_dir)
-                if self.opts.save_trainer_state:
-                    ckpt.save_trainer_state(st if st is not None else self._trainer_state(epoch), self.model_dir)
+                if self.opts.save_trainer_state and st is None:
+                    st = self._trainer_state(epoch)
+                self.save_model(self.model_dir, st if self.opts.save_trainer_state else None)
             mdist.barrier()  # reference has no barrier after the rank-0 save
         else:
-            self.save_model(self.model_dir)
-            if self.opts.save_trainer_state:
-                ckpt.save_trainer_state(self._trainer_state(epoch), self.model_dir)
+            self.save_model(self.model_dir, self._trainer_state(epoch) if self.opts.save_trainer_state else None)
 
     def _global_mean(self, loss, metric):
         vals = mdist.all_reduce_scalars([loss, metric if metric is not None else 0.0], "sum")
@@ -674,6 +689,7 @@ class Trainer:
         finally:
             if self._watchdog:
                 self._watchdog.stop()
+            self._checkpoint_wait()  # the last async model.pth is on disk when fit() returns
         self.history = {
             "epochs": [*range(1, self.epochs + 1)],
             "train_loss": self.train_losses,

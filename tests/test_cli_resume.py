@@ -76,6 +76,45 @@ def test_resume_equals_uninterrupted(tmp_path):
         torch.testing.assert_close(v, w, rtol=1e-6, atol=1e-7)
 
 
+def test_async_checkpoint_resume_equals_sync(tmp_path):
+    """async_checkpoint (pinned-host snapshot + background writer) produces the same artifacts as
+    the synchronous save, and a resume from them continues identically."""
+    tr, va = TensorCifar(96, 0), TensorCifar(32, 1)
+    runs = {}
+    for mode in ("sync", "async"):
+        torch.manual_seed(5)
+        t = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=2, batch_size=32, model_dir=str(tmp_path / mode),
+                    optimizer="adam", lr=0.01, options={"progress": False, "async_checkpoint": mode == "async"})
+        t.fit()
+        runs[mode] = t
+    a = torch.load(tmp_path / "sync" / "model.pth", weights_only=True)
+    b = torch.load(tmp_path / "async" / "model.pth", weights_only=True)
+    assert list(a) == list(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    sa = torch.load(tmp_path / "sync" / "trainer_state.pt", weights_only=True)
+    sb = torch.load(tmp_path / "async" / "trainer_state.pt", weights_only=True)
+    assert sa["epoch"] == sb["epoch"] == 2 and sa["global_step"] == sb["global_step"]
+    res = Trainer(MLModel("tiny"), datasets=(tr, va), epochs=3, batch_size=32, model_dir=str(tmp_path / "async"),
+                  optimizer="adam", lr=0.01, options={"progress": False, "resume": True, "async_checkpoint": True})
+    assert res.start_epoch == 3
+    res.fit()
+    assert res.history["train_loss"][:2] == runs["async"].history["train_loss"]
+
+
+def test_async_checkpointer_write_error_surfaces(tmp_path):
+    from ml_trainer_amd.utils.checkpoint import AsyncCheckpointer
+    ck = AsyncCheckpointer()
+    blocker = tmp_path / "f"
+    blocker.write_text("x")  # a FILE where the checkpoint directory would be
+    ck.save(MLModel("tiny"), str(blocker / "model.pth"))
+    with pytest.raises(OSError):
+        ck.wait()
+    ck.save(MLModel("tiny"), str(tmp_path / "ok" / "model.pth"))
+    assert ck.wait() == str(tmp_path / "ok" / "model.pth")
+    ck.close()
+
+
 def test_watchdog_fires_and_beats():
     fired = []
     w = Watchdog(0.3, on_timeout=lambda: fired.append(1), poll_s=0.05).start()

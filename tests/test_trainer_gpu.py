@@ -56,3 +56,40 @@ def test_generic_model_native_path(tmp_path):
                 options={"progress": False})
     t.fit()
     assert t.history["train_loss"][1] < t.history["train_loss"][0]
+
+
+def test_async_checkpointer_snapshot_isolated_from_later_updates(tmp_path):
+    """The pinned-host snapshot holds the parameters as of save(): updates queued on the same
+    stream right after it (while earlier work is still running) do not reach the file."""
+    from ml_trainer_amd.utils.checkpoint import AsyncCheckpointer
+    dev = torch.device("cuda", 0)
+    m = torch.nn.Linear(1024, 1024).to(dev)
+    x = torch.randn(4096, 4096, device=dev)
+    for _ in range(10):  # keep the stream busy so the copy is still queued when save() returns
+        x = x @ x.t() * 1e-3
+    with torch.no_grad():
+        m.weight.fill_(1.0)
+    ck = AsyncCheckpointer()
+    ck.save(m, str(tmp_path / "model.pth"))
+    with torch.no_grad():
+        m.weight.fill_(2.0)
+    assert ck.wait() == str(tmp_path / "model.pth")
+    ck.close()
+    sd = torch.load(tmp_path / "model.pth", weights_only=True)
+    assert sd["weight"].device.type == "cpu" and torch.all(sd["weight"] == 1.0)
+    assert torch.all(m.weight == 2.0)
+
+
+def test_engine_async_checkpoint_matches_sync(tmp_path):
+    tf = custom_pre_process_function()
+    tr = SyntheticCIFAR10(320, train=True, transform=tf, seed=0, learnable=True)
+    va = SyntheticCIFAR10(128, train=False, transform=tf, seed=0, learnable=True)
+    sds = []
+    for mode in (False, True):
+        torch.manual_seed(0)
+        t = Trainer(MLModel(), datasets=(tr, va), epochs=2, batch_size=64, model_dir=str(tmp_path / str(mode)),
+                    lr=0.01, options={"progress": False, "use_engine": True, "async_checkpoint": mode})
+        t.fit()
+        sds.append(torch.load(tmp_path / str(mode) / "model.pth", weights_only=True))
+    for k in sds[0]:
+        assert torch.equal(sds[0][k], sds[1][k]), k
