@@ -672,6 +672,28 @@ __device__ __forceinline__ bf16x8 frag_tr_asm(const uint8_t* lds, int r0, int r1
   const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
+// the same read at a compile-time byte offset from `base` (the instruction's offset field): rows
+// r0 and r0 + 16 of a tile_off image share their XOR swizzle (16 = 0 mod 8), so the hi half is
+// the lo address + 2048, and tiles a constant number of bytes apart share one address register
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr_asm_off(uint32_t a) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+template <int OFF>  // fragment of the tile at `lds` + OFF, rows r0 .. and r0 + 16 .. (see frag_tr_asm)
+__device__ __forceinline__ bf16x8 frag_tr16_off(uint32_t a) {
+  const s16x4 lo = ds_tr_asm_off<OFF>(a);
+  const s16x4 hi = ds_tr_asm_off<OFF + 16 * 128>(a);
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+// lane address of frag_tr_asm(lds, r0, r0 + 16, col) as a 32-bit LDS byte address
+__device__ __forceinline__ uint32_t frag_tr_addr(const uint8_t* lds, int r0, int col) {
+  const int lane = threadIdx.x & 63, i = lane & 15, q = i >> 2, p = i & 3;
+  const int cc = col + 4 * p, chunk = cc >> 3, half = (cc & 7) * 2;
+  return (uint32_t)reinterpret_cast<uintptr_t>((lds_s16x4*)(lds + tile_off(r0 + q, chunk) + half));
+}
 template <int N>
 __device__ __forceinline__ void frag_tr_wait(bf16x8 (&f)[N]) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -879,9 +901,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
       }
       bf16x8 tf[8];  // dO^T (d = 0..3), Q^T (d = 0..3)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        tf[d] = frag_tr_asm(Os, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
-        tf[4 + d] = frag_tr_asm(Qs, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+      for (int d = 0; d < 4; ++d) {  // Q^T and dO^T (kTile bytes further) from one address
+        const uint32_t a = frag_tr_addr(Qs, 32 * ks + 4 * g, d * 16);
+        tf[d] = frag_tr16_off<kTile>(a);
+        tf[4 + d] = frag_tr16_off<0>(a);
       }
       frag_tr_wait(tf);
 #pragma unroll
@@ -1067,7 +1090,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
       for (int n = 0; n < NQ; ++n) sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
       bf16x8 tf[4];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) tf[d] = frag_tr_asm(Ks, 32 * ks + 4 * g, 32 * ks + 16 + 4 * g, d * 16);
+      for (int d = 0; d < 4; ++d) tf[d] = frag_tr16_off<0>(frag_tr_addr(Ks, 32 * ks + 4 * g, d * 16));
       frag_tr_wait(tf);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
