@@ -23,6 +23,7 @@
 // Global->LDS staging of the next tile is register-staged (loads issued before the MFMA work
 // of the current tile, LDS writes after it), so HBM latency overlaps the math.
 #include <cstdlib>
+#include <type_traits>
 
 #include "mlt_common.h"
 #include "mlt_kernels.h"
@@ -1047,42 +1048,46 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
     const uint8_t* Vs = Ks + kTile;
     const bool kfull = (kb + 1) * AB <= len;
     f32x4 ds[NQ][4];
+    // mask-path choice hoisted out of the kt loop (block-uniform): one basic block per path, so
+    // MFMAs and the exp / dS VALU work of neighbouring kt tiles interleave (see the dK/dV kernel)
+    auto ktiles = [&](auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      f32x4 sv[NQ], dp[NQ];
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) {
-        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        const bf16x8 ka = frag_row(Ks, kt * 16, kh), va = frag_row(Vs, kt * 16, kh);
+      for (int kt = 0; kt < 4; ++kt) {
+        f32x4 sv[NQ], dp[NQ];
 #pragma unroll
         for (int n = 0; n < NQ; ++n) {
-          sv[n] = mfma(ka, qf[n][kh], sv[n]);
-          dp[n] = mfma(va, of[n][kh], dp[n]);
+          sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      }
-      if (kfull) {  // block-uniform: every key of this block is valid
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const bf16x8 ka = frag_row(Ks, kt * 16, kh), va = frag_row(Vs, kt * 16, kh);
+#pragma unroll
+          for (int n = 0; n < NQ; ++n) {
+            sv[n] = mfma(ka, qf[n][kh], sv[n]);
+            dp[n] = mfma(va, of[n][kh], dp[n]);
+          }
+        }
 #pragma unroll
         for (int n = 0; n < NQ; ++n)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(sv[n][r] * sl2 - lq[n]);
-            ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
-          }
-      } else {
-#pragma unroll
-        for (int n = 0; n < NQ; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kb * AB + kt * 16 + 4 * g + r;
-            const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
+            float pv;
+            if constexpr (FULL) {  // every key of this block is valid
+              pv = fast_exp2(sv[n][r] * sl2 - lq[n]);
+            } else {
+              const int key = kb * AB + kt * 16 + 4 * g + r;
+              pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
+            }
             ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
           }
       }
-    }
+    };
+    if (kfull)
+      ktiles(std::true_type{});
+    else
+      ktiles(std::false_type{});
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 sb[NQ];
