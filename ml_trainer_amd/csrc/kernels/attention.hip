@@ -840,65 +840,77 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
     const float* del_s = lse_s + AB;
     const int q0 = qb * AB;
     const bool qfull = q0 + AB <= S;
-    f32x4 p[NK][4], ds[NK][4];
+    // P and dS leave the fp32 accumulators as bf16 MFMA operands as soon as a qt pair is done
+    // (half the registers of keeping all four qt tiles in fp32), and the block-uniform score-path
+    // choice is taken once outside the qt loop, so each path's qt iterations are ONE basic block in
+    // which one tile's MFMAs interleave with the previous tile's exp / dS VALU work
+    bf16x8 pbk[NK][2], sbk[NK][2];
+    auto qtiles = [&](auto pathc) __attribute__((always_inline)) {
+      constexpr int PATH = decltype(pathc)::value;  // 0 all valid, 1 key mask, 2 key + query mask
+      f32x4 pe[NK], dse[NK];  // the even qt of the current pair
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
-      f32x4 sv[NK], dp[NK];
-#pragma unroll
-      for (int n = 0; n < NK; ++n) {
-        sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        const bf16x8 qa = frag_row(Qs, qt * 16, kh), oa = frag_row(Os, qt * 16, kh);
+      for (int qt = 0; qt < 4; ++qt) {
+        f32x4 sv[NK], dp[NK];
 #pragma unroll
         for (int n = 0; n < NK; ++n) {
-          sv[n] = mfma(qa, kf[n][kh], sv[n]);
-          dp[n] = mfma(oa, vf[n][kh], dp[n]);
+          sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const bf16x8 qa = frag_row(Qs, qt * 16, kh), oa = frag_row(Os, qt * 16, kh);
+#pragma unroll
+          for (int n = 0; n < NK; ++n) {
+            sv[n] = mfma(qa, kf[n][kh], sv[n]);
+            dp[n] = mfma(oa, vf[n][kh], dp[n]);
+          }
+        }
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
+        const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
+        const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+        f32x4 pc[NK], dsc[NK];
+#pragma unroll
+        for (int n = 0; n < NK; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float pv;
+            if constexpr (PATH == 0) {  // every key of the block valid: x = s * sl2 - lse (one fma per score)
+              pv = fast_exp2(sv[n][r] * sl2 - lr[r]);
+            } else if constexpr (PATH == 1) {  // key mask folded into per-lane constants
+              pv = fast_exp2(sv[n][r] * sl2k[n] - (lr[r] + kinf[n]));
+            } else {
+              const int ql = qt * 16 + 4 * g + r;
+              const bool ok = key[n] < len && q0 + ql < S;
+              pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
+            }
+            pc[n][r] = pv;
+            dsc[n][r] = pv * (dp[n][r] - dr[r]);
+          }
+#pragma unroll
+        for (int n = 0; n < NK; ++n) {
+          if (qt & 1) {
+            pbk[n][qt >> 1] = pack_acc(pe[n], pc[n]);
+            sbk[n][qt >> 1] = pack_acc(dse[n], dsc[n]);
+          } else {
+            pe[n] = pc[n];
+            dse[n] = dsc[n];
+          }
         }
       }
-      const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
-      const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
-      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
-      if (qfull && kfull) {  // every key of the block valid: x = s * sl2 - lse (one fma per score)
-#pragma unroll
-        for (int n = 0; n < NK; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(sv[n][r] * sl2 - lr[r]);
-            p[n][qt][r] = pv;
-            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
-          }
-      } else if (qfull) {  // key mask folded into per-lane constants: x = s * sl2k - (lse + kinf)
-#pragma unroll
-        for (int n = 0; n < NK; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(sv[n][r] * sl2k[n] - (lr[r] + kinf[n]));
-            p[n][qt][r] = pv;
-            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
-          }
-      } else {
-#pragma unroll
-        for (int n = 0; n < NK; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = qt * 16 + 4 * g + r;
-            const bool ok = key[n] < len && q0 + ql < S;
-            const float pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
-            p[n][qt][r] = pv;
-            ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
-          }
-      }
-    }
+    };
+    if (qfull && kfull)
+      qtiles(std::integral_constant<int, 0>{});
+    else if (qfull)
+      qtiles(std::integral_constant<int, 1>{});
+    else
+      qtiles(std::integral_constant<int, 2>{});
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 pb[NK], sb[NK];
 #pragma unroll
       for (int n = 0; n < NK; ++n) {
-        pb[n] = pack_acc(p[n][2 * ks], p[n][2 * ks + 1]);
-        sb[n] = pack_acc(ds[n][2 * ks], ds[n][2 * ks + 1]);
+        pb[n] = pbk[n][ks];
+        sb[n] = sbk[n][ks];
       }
       bf16x8 tf[8];  // dO^T (d = 0..3), Q^T (d = 0..3)
 #pragma unroll
