@@ -89,8 +89,11 @@ def _run(cmd):
 # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds / muls of the softmax VALU work
 # into v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32, which cost more than two scalar ops when they
 # sit between MFMAs (MI355X_MICROARCH.md, "price of one filler beside MFMAs").
+# lenet_mfma.hip: the max-memory-clause machine scheduler (loads grouped into clauses issued ahead
+# of their uses) measured 1-2 % faster on the latency-chain per-sample step than the default,
+# max-ilp and iterative-ilp strategies (profiles/ab_lenet_sched_r3.jsonl).
 FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
-              "lenet_mfma.hip": ["-fno-slp-vectorize"]}
+              "lenet_mfma.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 
 
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:

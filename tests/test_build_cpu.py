@@ -35,4 +35,5 @@ def test_file_flags_cover_the_measured_files():
     # the per-file flags measured in profiles/ab_*_r3.jsonl: no SLP packing beside MFMAs
     assert "-fno-slp-vectorize" in build.FILE_FLAGS["attention.hip"]
     assert "-fno-slp-vectorize" in build.FILE_FLAGS["lenet_mfma.hip"]
+    assert "-amdgpu-sched-strategy=max-memory-clause" in build.FILE_FLAGS["lenet_mfma.hip"]
     assert "gemm_tile.hip" not in build.FILE_FLAGS  # measured slower there
