@@ -10,8 +10,15 @@ Each timed step is a FULL reference training step (src/trainer.py:180-197):
 sample a batch from the dataset (synthetic CIFAR-shaped uint8 data resident in
 HBM), RandomCrop(32, pad 4) + HFlip + Normalize (src/utils/functions.py:5-12),
 forward, softmax-cross-entropy, loss + accuracy accumulation (on device),
-backward, DDP gradient all-reduce (RCCL, W > 1) and the SGD(lr=1e-3,
-momentum=0.9) update -- random-init weights, fp32 compute.
+backward, DDP gradient all-reduce (W > 1) and the SGD(lr=1e-3, momentum=0.9)
+update -- random-init weights. Compute dtype: bf16 by default (BASELINE.json
+configs 2/3 "default config bf16": bf16 MFMA operands, fp32 accumulation,
+activations, master weights and optimizer state; two kernels per step at every
+W, the gradient exchange over xGMI folded into the second); ``--precision fp32``
+is the reference model's own dtype. The headline run is followed by the same
+measurement of the fp32 engine (same steps / warmup / protocol), reported as
+config.fp32_samples_per_s / config.fp32_ms_per_step: a same-dtype comparison with
+the reference every run (``--no-fp32-companion`` skips it).
 
 Scaling modes:
   weak (default)  per-GPU batch fixed at --batch (32 = the reference's batch), global batch = 32*N
@@ -29,7 +36,7 @@ BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgr
 delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
 
 BASELINE.json config 4 (BERT-base classifier, seq 512, bf16, DDP): ``--model bert-base``
-(per-GPU batch --batch, default 32; native MFMA GEMM / flash-attention / LayerNorm kernels,
+(per-GPU batch --batch, default 512; native MFMA GEMM / flash-attention / LayerNorm kernels,
 fused AdamW on flat fp32 masters with bf16 shadows, bucketed RCCL all-reduce overlapped with
 backward for N > 1).
 """
@@ -80,6 +87,11 @@ def parse():
                     help="LeNet step: bf16 (BASELINE.json configs 2/3 'default config bf16': bf16 MFMA "
                          "operands, fp32 accumulation / activations / masters / optimizer state; 2 kernels "
                          "per step) or fp32 (the reference model's dtype; 4 kernels per step)")
+    ap.add_argument("--no-fp32-companion", action="store_true",
+                    help="LeNet bf16: skip the fp32 engine measurement that follows the headline run")
+    ap.add_argument("--transport", choices=["auto", "xgmi-loopback", "rccl-loopback"], default="auto",
+                    help="LeNet, 1 GPU: time the data-parallel step against this rank itself (xgmi-loopback: "
+                         "the bf16 two-launch exchange step; rccl-loopback: a real ncclAllReduce in the graph)")
     ap.add_argument("--seed", type=int, default=32)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -303,59 +315,11 @@ def bench_cpu(args, world, rank):
     }
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(_self_launch(args))
+def bench_lenet(args, world, rank, dev, backend, precision):
+    """The LeNet headline (BASELINE.json metric): the fused step engine on an HBM-resident
+    synthetic dataset, every hipGraph captured before the timed region."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring WORLD_SIZE ranks",
-              file=sys.stderr)
-    backend = os.environ.get("MLT_BENCH_BACKEND", "nccl")
-    if args.batch is None:
-        # LeNet: the reference batch (src/trainer.py / main.py: 32). Transformer configs: micro-batches
-        # sized for 288 GB of HBM per GPU (per-GPU throughput keeps rising with the micro-batch:
-        # BERT-base 2,552 / 2,665 / 2,710 samples/s at 128 / 256 / 512 using 21 / 40 / 77 GiB; the fp8
-        # `large` config, BASELINE config 5 "sized to fill HBM": 1,013 / 1,030 samples/s at 256 / 512
-        # using 126 / 245 GiB; profiles/batch_sweep_r2.jsonl)
-        args.batch = {"bert-base": 512, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
-
-    if args.device == "cpu" or not torch.cuda.is_available():
-        if world > 1:
-            dist.init_process_group("gloo")
-        if args.steps == 3000 and args.warmup == 300:
-            args.steps, args.warmup = 50, 5
-        _emit(bench_cpu(args, world, rank), rank, args)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    # rehearsal knob for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
-    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
-    dev = torch.device("cuda", 0 if same_dev else local_rank)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-        world = dist.get_world_size()
-
-    if args.model in ("bert-base", "bert-tiny", "bert-large", "large"):
-        if args.steps == 3000 and args.warmup == 300:  # LeNet-sized defaults -> BERT-sized
-            args.steps, args.warmup = 20, 5
-        _emit(bench_bert(args, world, rank, dev), rank, args)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
     from ml_trainer_amd.models.lenet import MLModel
     from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
     from ml_trainer_amd.ops.optim import build_optimizer
@@ -370,11 +334,19 @@ def main():
     opt = build_optimizer(args.optimizer, model.parameters(), lr=1e-3, momentum=0.9, weight_decay=0.0, flat=flat)
     per_gpu = args.batch if args.scaling == "weak" else max(args.batch // world, 1)
     engine = LeNetStepEngine(model, flat, max_batch=per_gpu, optimizer=opt, world_size=world, seed=args.seed,
-                             precision=args.precision)
-    if os.environ.get("MLT_BENCH_FORCE_RCCL") == "1" and world == 1:
-        # W=1 rehearsal of the data-parallel step: real ncclAllReduce inside the captured graph
+                             precision=precision)
+    transport = args.transport
+    if os.environ.get("MLT_BENCH_FORCE_RCCL") == "1":
+        transport = "rccl-loopback"
+    if transport != "auto" and world == 1:
+        # W=1 rehearsal of the data-parallel step: a real ncclAllReduce inside the captured graph, or
+        # the xGMI exchange against this rank itself (bf16: folded into the reduction kernel)
         C = engine.C
-        engine.use_transport(comm=C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index))
+        if transport == "rccl-loopback":
+            engine.use_transport(comm=C.Communicator(C.Communicator.unique_id(), 1, 0, dev.index))
+        else:
+            from ml_trainer_amd.parallel.comm import create_xgmi_loopback
+            engine.use_transport(xgmi=create_xgmi_loopback(flat.numel, dev))
 
     # Synthetic CIFAR-10-shaped dataset (uint8 HWC) resident in HBM; random labels.
     N = args.dataset_size
@@ -461,6 +433,7 @@ def main():
         key = {"xgmi-oneshot": "xgmi", "xgmi-twoshot": "xgmi2", "rccl": "rccl"}.get(engine.dp_transport)
         comm = {"buckets": 1, "bucket_mb": [round(flat.numel * 4 / 2 ** 20, 3)], "comm_dtype": "float32",
                 "in_graph": engine.in_graph_collective, "overlap_pct": 0.0,
+                "fused_into_reduction_kernel": engine.dp_transport == "xgmi-fused",
                 "allreduce_ms": round(tt[key], 4) if (tt and key in tt) else None}
     out = {
         "metric": "samples/sec/node",
@@ -473,7 +446,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak" if args.scaling == "weak" else "strong",
         "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2),
-        "dtype": args.precision,
+        "dtype": precision,
         "data": "synthetic (CIFAR-10-shaped uint8 in HBM, on-GPU RandomCrop+HFlip+Normalize), random-init weights",
         "config": {"model": f"src/model.py MLModel ({args.model} LeNet-5, 62,006 params)" if args.model == "default"
                    else f"src/model.py MLModel ({args.model})",
@@ -488,6 +461,73 @@ def main():
                    "transport_ms": getattr(engine, "transport_times_ms", None),
                    "loss_finite": math.isfinite(loss_sum)},
     }
+    if world > 1:
+        dist.barrier()
+    return out
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args))
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring WORLD_SIZE ranks",
+              file=sys.stderr)
+    backend = os.environ.get("MLT_BENCH_BACKEND", "nccl")
+    if args.batch is None:
+        # LeNet: the reference batch (src/trainer.py / main.py: 32). Transformer configs: micro-batches
+        # sized for 288 GB of HBM per GPU (per-GPU throughput keeps rising with the micro-batch:
+        # BERT-base 2,552 / 2,665 / 2,710 samples/s at 128 / 256 / 512 using 21 / 40 / 77 GiB; the fp8
+        # `large` config, BASELINE config 5 "sized to fill HBM": 1,013 / 1,030 samples/s at 256 / 512
+        # using 126 / 245 GiB; profiles/batch_sweep_r2.jsonl)
+        args.batch = {"bert-base": 512, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
+
+    if args.device == "cpu" or not torch.cuda.is_available():
+        if world > 1:
+            dist.init_process_group("gloo")
+        if args.steps == 3000 and args.warmup == 300:
+            args.steps, args.warmup = 50, 5
+        _emit(bench_cpu(args, world, rank), rank, args)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # rehearsal knob for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
+    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
+    dev = torch.device("cuda", 0 if same_dev else local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        world = dist.get_world_size()
+
+    if args.model in ("bert-base", "bert-tiny", "bert-large", "large"):
+        if args.steps == 3000 and args.warmup == 300:  # LeNet-sized defaults -> BERT-sized
+            args.steps, args.warmup = 20, 5
+        _emit(bench_bert(args, world, rank, dev), rank, args)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    out = bench_lenet(args, world, rank, dev, backend, args.precision)
+    if args.precision == "bf16" and not args.no_fp32_companion:
+        # same-dtype comparison with the reference (fp32), same protocol, after the headline run
+        comp = bench_lenet(args, world, rank, dev, backend, "fp32")
+        out["config"]["fp32_samples_per_s"] = comp["value"]
+        out["config"]["fp32_ms_per_step"] = comp["ms_per_step"]
+        out["config"]["fp32_device_ms_per_step"] = comp["config"]["device_ms_per_step"]
+        out["config"]["fp32_vs_baseline"] = comp["vs_baseline"]
+        out["config"]["fp32_dp_transport"] = comp["config"]["dp_transport"]
     _emit(out, rank, args)
     if world > 1:
         dist.barrier()

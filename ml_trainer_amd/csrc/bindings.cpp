@@ -1101,6 +1101,13 @@ class LeNetEngine {
     graphs_.clear();
   }
   int precision() const { return prec_; }
+  // bf16 + xGMI: the two-launch data-parallel step (default) or the four-launch one (per-sample
+  // kernel, batch reductions, xGMI all-reduce, apply) kept for A/B and bitwise cross-checks
+  void set_fused_dp(bool f) {
+    fused_dp_ = f;
+    graphs_.clear();
+  }
+  bool fused_dp() const { return fused_dp_; }
 
   void check_mode(int mode, int B) const {
     TORCH_CHECK(B > 0 && B <= max_b_, "batch ", B, " outside [1, ", max_b_, "]");
@@ -1121,11 +1128,18 @@ class LeNetEngine {
     check_mode(mode, B);
     const bool mf = prec_ == 1 && (mode & LENET_BWD);
     if (mf) launch_lenet_mfma_pack(cfg_, P_, O_, cur_stream());  // shadow / fragment image from the masters
-    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream(), mf);
+    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream(), mf, fused_dp_);
   }
 
   static void launch_step(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
-                          Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s, bool mfma = false) {
+                          Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s, bool mfma = false,
+                          bool fused_dp = false) {
+    if (mfma && (mode & LENET_REDUCE) && xgmi && fused_dp) {
+      // bf16 data-parallel step in two launches: the per-sample kernel, then batch reductions +
+      // xGMI exchange + rank-ordered sum + update (lenet_mwx; world size 1 = loopback)
+      launch_lenet_mfma_dp(cfg, mode & ~LENET_REDUCE, B, P, A, O, xgmi->fused_view(), s);
+      return;
+    }
     if (mfma) {
       launch_lenet_mfma(cfg, mode & ~LENET_REDUCE, B, P, A, O, s);
     } else {
@@ -1171,9 +1185,10 @@ class LeNetEngine {
     Communicator* comm = comm_;
     XgmiAllReduce* xgmi = xgmi_;
     const bool mf = prec_ == 1 && (mode & LENET_BWD);
+    const bool fused = fused_dp_;
     g->capture([&](hipStream_t s) {
       // (no pack here: replay() re-packs when the host changed the masters since the last pack)
-      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf);
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf, fused);
     });
     graphs_[key(mode, B, nsteps)] = std::move(g);
   }
@@ -1224,6 +1239,7 @@ class LeNetEngine {
   py::object xgmi_keep_ = py::none();
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
   int prec_ = 0;
+  bool fused_dp_ = true;
   int64_t shadow_n_ = 0;
   Tensor master_;          // the fp32 masters (version counter: host-side changes)
   int64_t pack_ver_ = -1;  // master_._version() at the last pack
@@ -1339,6 +1355,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_aug", &LeNetEngine::set_aug)
       .def("set_comm", &LeNetEngine::set_comm)
       .def("set_xgmi", &LeNetEngine::set_xgmi)
+      .def_property("fused_dp", &LeNetEngine::fused_dp, &LeNetEngine::set_fused_dp)
       .def("clear_aug", &LeNetEngine::clear_aug)
       .def("set_ctrl", &LeNetEngine::set_ctrl)
       .def("set_opt", &LeNetEngine::set_opt)

@@ -12,9 +12,11 @@ static void hcheck(hipError_t e, const char* what) {
 }
 
 // region: data [2][cap] | flags [2][G][W] | t1 [2][W][slot] | t2 [2][W][slot] | f1 [2][G][W] | f2 [2][G][W]
-// (the t* / f* parts belong to the two-shot algorithm), every part 256-byte aligned
+//         | ff [2][kFusedBlocks][W]
+// (the t* / f* parts belong to the two-shot algorithm, ff to the fused LeNet step's exchange, which
+// shares `data`), every part 256-byte aligned
 struct RegionLayout {
-  size_t flags, t1, t2, f1, f2, bytes;
+  size_t flags, t1, t2, f1, f2, ff, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
@@ -25,7 +27,8 @@ static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t sl
   L.t2 = align256(L.t1 + tb);
   L.f1 = align256(L.t2 + tb);
   L.f2 = align256(L.f1 + fl);
-  L.bytes = L.f2 + fl;
+  L.ff = align256(L.f2 + fl);
+  L.bytes = L.ff + (size_t)2 * XgmiAllReduce::kFusedBlocks * world * sizeof(uint64_t);
   return L;
 }
 
@@ -46,6 +49,8 @@ XgmiAllReduce::XgmiAllReduce(int64_t cap_floats, int world, int rank, int device
   hcheck(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_), err_host_, 0), "hipHostGetDevicePointer(err)");
   hcheck(hipMalloc(reinterpret_cast<void**>(&seqs_), sizeof(uint64_t) * blocks), "hipMalloc(seqs)");
   hcheck(hipMemset(seqs_, 0, sizeof(uint64_t) * blocks), "hipMemset(seqs)");
+  hcheck(hipMalloc(reinterpret_cast<void**>(&fseqs_), sizeof(uint64_t) * kFusedBlocks), "hipMalloc(fseqs)");
+  hcheck(hipMemset(fseqs_, 0, sizeof(uint64_t) * kFusedBlocks), "hipMemset(fseqs)");
   hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_host_ = new XgmiPeers();
   std::memset(peers_host_, 0, sizeof(XgmiPeers));
@@ -57,6 +62,7 @@ XgmiAllReduce::~XgmiAllReduce() {
   if (region_) (void)hipFree(region_);
   if (err_host_) (void)hipHostFree(err_host_);
   if (seqs_) (void)hipFree(seqs_);
+  if (fseqs_) (void)hipFree(fseqs_);
   delete static_cast<XgmiPeers*>(peers_host_);
 }
 
@@ -89,6 +95,7 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
     P->t2[q] = reinterpret_cast<float*>(c + L.t2);
     P->f1[q] = reinterpret_cast<uint64_t*>(c + L.f1);
     P->f2[q] = reinterpret_cast<uint64_t*>(c + L.f2);
+    ff_[q] = reinterpret_cast<uint64_t*>(c + L.ff);
   }
   opened_ = true;
 }
@@ -103,6 +110,26 @@ void XgmiAllReduce::launch(float* grad, int64_t n, float scale, hipStream_t st, 
   else
     launch_xgmi_allreduce(grad, n, *static_cast<XgmiPeers*>(peers_host_), rank_, world_, cap_, blocks_, seqs_, scale,
                           err_, ticks, post, st, fault_);
+}
+
+XgmiFused XgmiAllReduce::fused_view() const {
+  if (!opened_) throw std::runtime_error("xgmi: open() the peer handles first");
+  const XgmiPeers* P = static_cast<const XgmiPeers*>(peers_host_);
+  XgmiFused X;
+  std::memset(&X, 0, sizeof(X));
+  for (int q = 0; q < world_; ++q) {
+    X.data[q] = P->data[q];
+    X.flags[q] = ff_[q];
+  }
+  X.seqs = fseqs_;
+  X.err = err_;
+  X.cap = cap_;
+  X.timeout = timeout_ms_ * 100000LL;
+  X.rank = rank_;
+  X.W = world_;
+  X.G = kFusedBlocks;
+  X.fault = fault_;
+  return X;
 }
 
 void XgmiAllReduce::set_algo(int a) {

@@ -15,6 +15,8 @@
 
 namespace mlt {
 
+struct XgmiFused;  // mlt_kernels.h
+
 enum class CommDtype { F32 = 0, BF16 = 1, F16 = 2, I32 = 3, I64 = 4, U8 = 5 };
 enum class CommOp { SUM = 0, AVG = 1, MAX = 2, MIN = 3 };
 
@@ -75,6 +77,11 @@ class XgmiAllReduce {
   // must use the same algorithm for a given call. Graphs keep the algorithm they were captured with.
   void set_algo(int a);
   int algo() const { return algo_; }
+  // the fused LeNet data-parallel step's view (kernels/lenet_mfma.hip): the data region, a flag
+  // area of its own ([2][kFusedBlocks][W]) and per-block counters of its own; timeout / fault as
+  // set now (graphs keep the values they were captured with). World size 1 = loopback.
+  static constexpr int kFusedBlocks = 128;
+  XgmiFused fused_view() const;
 
  private:
   int64_t cap_;
@@ -88,6 +95,8 @@ class XgmiAllReduce {
   unsigned* err_host_ = nullptr;  // coherent pinned host word
   long long timeout_ms_ = 2000;
   uint64_t* seqs_ = nullptr;
+  uint64_t* fseqs_ = nullptr;
+  uint64_t* ff_[8] = {nullptr};
   bool opened_ = false;
   int fault_ = 0;
   void* peers_host_ = nullptr;  // XgmiPeers

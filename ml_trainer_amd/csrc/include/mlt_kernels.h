@@ -103,6 +103,12 @@ int lenet_mfma_kw_blocks(int cfg);  // grid of the batch-reduction / optimizer k
 // data-parallel bf16 step: optimizer update from the all-reduced gradient + bf16 shadow + fragment
 // images in one launch (skip: nonzero vetoes the update)
 void launch_lenet_mfma_apply(int cfg, const LeNetPtrs& P, const LeNetOpt& O, const unsigned* skip, hipStream_t stream);
+// data-parallel bf16 step in TWO launches (as at W = 1): the per-sample kernel, then the batch
+// reductions + xGMI exchange + rank-ordered sum + update of every gradient element in one launch
+// (struct XgmiFused; throws if X.G < lenet_mfma_kw_blocks(cfg) or X.W outside 1..8)
+struct XgmiFused;
+void launch_lenet_mfma_dp(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                          const XgmiFused& X, hipStream_t stream);
 int lenet_mfma_wimg_elems();
 // shadow + wimg from the fp32 masters (O.p)
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);
@@ -216,6 +222,20 @@ struct XgmiPostOpt {
 void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t cap, int blocks,
                            uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
                            const XgmiPostOpt* post, hipStream_t st, int fault = 0);
+// The fused bf16 LeNet data-parallel step's view of the transport (lenet_mfma.hip, lenet_mwx):
+// the batch-reduction kernel's block b publishes the gradient elements it produced into its own
+// rank's data region (parity p of step seq) and flags[q][(p * G + b) * W + rank] on every peer q,
+// waits for all W flags of (p, b), sums those elements over the W regions in rank order and applies
+// the update in the same launch. W = 1 is the loopback (the peer is this rank itself).
+struct XgmiFused {
+  float* data[kXgmiMaxRanks];      // per-rank [2][cap] fp32 (indexed by flat parameter offset)
+  uint64_t* flags[kXgmiMaxRanks];  // per-rank [2][G][W]
+  uint64_t* seqs;                  // [G] per-block launch counters (this rank)
+  unsigned* err;                   // sticky error word (host-mapped)
+  int64_t cap;
+  long long timeout;               // ticks of the 100 MHz constant clock
+  int rank, W, G, fault;
+};
 // two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,
                                  int blocks, uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,

@@ -42,6 +42,7 @@
 //   conv1 wgrad M = (kw | c, kh) taps (+ ones row), N = out channel, K = the 28x32 positions of the
 //               unpooled conv1 gradient; split over 3 K-ranges, summed in a fixed order
 // All batch reductions (KW) run in sample order: results are bitwise reproducible run to run.
+#include <stdexcept>
 #include <type_traits>
 
 #include "mlt_common.h"
@@ -877,6 +878,106 @@ __device__ __forceinline__ void upd1(const LeNetOpt& O, const Ctx& c, uint16_t* 
   if (shadow) shadow[i] = f32_to_bf16(p);
 }
 
+// Data-parallel exchange inside the batch-reduction kernel (struct XgmiFused, WT ranks; WT = 0: off).
+// Every gradient element is produced by exactly one lane of one block, the same lane and block on
+// every rank, so block b's elements form its slice: the lane puts them into its rank's region at
+// their flat offsets (parity p of this launch), the block publishes (p, b) to every peer, waits for
+// all WT peers, and the lane sums its elements over the WT regions in rank order (the same order on
+// every rank: bit-identical replicas) before the update. Producer: payload stores -> every wave's
+// vmcnt(0) -> workgroup barrier -> one system-scope release store per peer flag. Consumer: relaxed
+// system-scope polls of the own flag row -> one system acquire fence (+ its vmcnt wait) ->
+// workgroup barrier -> plain loads. Parity reuse is safe as in allreduce.hip: a rank reaches launch
+// s + 2 (parity p again) only after every peer published s + 1, which each peer does only after its
+// launch s -- including the reads of parity p -- retired.
+// Failure: the sticky error word (read at block start, checked before publishing) stops this rank
+// from publishing anything once any launch timed out, so every peer times out too; a timed-out block
+// applies nothing. Blocks that did see all peers apply their slices (the job stops with
+// TransportError; resume restores identical replicas from the checkpoint).
+template <int WT>
+struct Xch {
+  static constexpr bool on = WT > 0;
+  const XgmiFused* X;
+  int* failed;  // __shared__
+  int blk, p;
+  uint64_t seq;
+  unsigned errv;
+  float scale;
+
+  __device__ __forceinline__ float* mine() const { return X->data[X->rank] + p * X->cap; }
+  __device__ __forceinline__ void put1(int64_t i, float v) const { mine()[i] = v; }
+  __device__ __forceinline__ void put4(int64_t i, float4 v) const { *reinterpret_cast<float4*>(mine() + i) = v; }
+  // all threads of the block, once
+  __device__ __forceinline__ bool sync() const {
+    const int t = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
+    __syncthreads();
+    if (t < 64) {
+      const bool dead = __builtin_amdgcn_readfirstlane(errv) != 0u;  // lane 0's value
+      const bool withhold = X->fault == 1 && blk % (2 * WT) == X->rank;  // fault injection (tests)
+      if (t < WT) {
+        if (dead) {
+          *failed = 1;
+        } else {
+          if (!withhold) {
+            uint64_t* f = X->flags[t] + ((int64_t)p * X->G + blk) * WT + X->rank;
+            __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          const uint64_t* f = X->flags[X->rank] + ((int64_t)p * X->G + blk) * WT + t;
+          const long long t0 = wall_clock64();
+          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+            if (wall_clock64() - t0 > X->timeout) {  // 100 MHz constant clock
+              __hip_atomic_fetch_or(X->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              *failed = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: this CU's caches see the peers' stores
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const bool ok = *failed == 0;
+    if (ok && t == 0) X->seqs[blk] = seq;  // read again only by the next launch (stream order)
+    return ok;
+  }
+  // the sum over the ranks, in rank order, scaled; opaque to the compiler so that the optimizer's
+  // arithmetic cannot contract with it (bitwise equal to all-reduce -> separate update launch)
+  __device__ __forceinline__ float get1(int64_t i) const {
+    float v[WT];
+#pragma unroll
+    for (int q = 0; q < WT; ++q) v[q] = X->data[q][p * X->cap + i];
+    __builtin_amdgcn_sched_barrier(0);
+    float s = v[0];
+#pragma unroll
+    for (int q = 1; q < WT; ++q) s += v[q];
+    s *= scale;
+    asm volatile("" : "+v"(s));
+    return s;
+  }
+  __device__ __forceinline__ float4 get4(int64_t i) const {
+    float4 v[WT];
+#pragma unroll
+    for (int q = 0; q < WT; ++q) v[q] = *reinterpret_cast<const float4*>(X->data[q] + p * X->cap + i);
+    __builtin_amdgcn_sched_barrier(0);
+    float4 s = v[0];
+#pragma unroll
+    for (int q = 1; q < WT; ++q) {
+      s.x += v[q].x;
+      s.y += v[q].y;
+      s.z += v[q].z;
+      s.w += v[q].w;
+    }
+    s.x *= scale;
+    s.y *= scale;
+    s.z *= scale;
+    s.w *= scale;
+    asm volatile("" : "+v"(s.x), "+v"(s.y), "+v"(s.z), "+v"(s.w));
+    return s;
+  }
+};
+
 template <class D>
 __host__ __device__ constexpr int mw_conv_blocks() {
   return (D::S1 + D::S2 + kWgT - 1) / kWgT;
@@ -900,11 +1001,11 @@ __host__ __device__ constexpr int mw_fc_blocks() {
   return (mw_fc_waves<D>() + kWgT / 64 - 1) / (kWgT / 64);
 }
 
-template <int NIN, int NOUT>
-__device__ __forceinline__ void fc_wgrad(int tile, int B, const float* __restrict__ dY, const float* __restrict__ X,
-                                         const LeNetOpt& O, const Ctx& c, uint16_t* shadow, int64_t offW, int64_t offb,
-                                         uint16_t* __restrict__ timg, int tpitch, uint16_t* __restrict__ fimg = nullptr,
-                                         int fpitch = 0) {
+template <int NIN, int NOUT, int WT>
+__device__ __forceinline__ void fc_wgrad(const Xch<WT>& xc, int tile, int B, const float* __restrict__ dY,
+                                         const float* __restrict__ X, const LeNetOpt& O, const Ctx& c, uint16_t* shadow,
+                                         int64_t offW, int64_t offb, uint16_t* __restrict__ timg, int tpitch,
+                                         uint16_t* __restrict__ fimg = nullptr, int fpitch = 0) {
   using W = FcW<NIN, NOUT>;
   const int ct = tile % W::CT, jt = tile / W::CT;
   const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
@@ -942,8 +1043,16 @@ __device__ __forceinline__ void fc_wgrad(int tile, int B, const float* __restric
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dv, acc, 0, 0, 0);
     }
   }
+  float4 gv = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  float gb = acc[0];
+  if constexpr (Xch<WT>::on) {  // data-parallel: this lane's elements summed over the ranks
+    if (wrow) xc.put4(iw, gv);
+    if (brow) xc.put1(ib, gb);
+    if (!xc.sync()) return;
+    if (wrow) gv = xc.get4(iw);
+    if (brow) gb = xc.get1(ib);
+  }
   if (wrow) {
-    float4 gv = make_float4(acc[0], acc[1], acc[2], acc[3]);
     *reinterpret_cast<float4*>(O.g + iw) = gv;
     if (c.on) {
       opt_update(O.h, c.lr, c.t, pw.x, gv.x, aw.x, sw.x);
@@ -965,11 +1074,12 @@ __device__ __forceinline__ void fc_wgrad(int tile, int B, const float* __restric
         *reinterpret_cast<uint2*>(fimg + j * fpitch + c0) = make_uint2(pack2(h0, h1), pack2(h2, h3));
     }
   }
-  if (brow) upd1(O, c, shadow, ib, acc[0], pb, ab, sb);
+  if (brow) upd1(O, c, shadow, ib, gb, pb, ab, sb);
 }
 
-template <class D>
-__device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNetOpt& O, int B, int64_t* __restrict__ ctrl) {
+template <class D, int WT>
+__device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNetOpt& O, int B, int64_t* __restrict__ ctrl,
+                                        const Xch<WT>& xc) {
   constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
   constexpr int NBC = mw_conv_blocks<D>();
   constexpr int NB = mw_fc_blocks<D>(), NW3 = FcW<FLAT, F1>::TILES, NW4 = FcW<F1, F2>::TILES,
@@ -986,10 +1096,14 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
   uint16_t* shadow = P.shadow;
   if (blk < NBC) {
     const int e = blk * kWgT + t;
-    if (e >= D::S1 + D::S2) return;
-    int soff;
-    int64_t dst;
-    if (e < D::S1) {
+    const bool act = e < D::S1 + D::S2;
+    if constexpr (!Xch<WT>::on) {
+      if (!act) return;
+    }
+    int soff = 0;
+    int64_t dst = 0;
+    if (!act) {
+    } else if (e < D::S1) {
       const int oc = e / 76, tap = e - 76 * oc;
       soff = e;
       dst = tap < 75 ? O.off[0] + oc * 75 + tap : O.off[1] + oc;
@@ -1011,6 +1125,11 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
       for (int u = 0; u < 32; ++u) v[u] = P.slab1[(int64_t)min(b0 + u, B - 1) * D::SLABN + soff];
 #pragma unroll
       for (int u = 0; u < 32; ++u) gsum += b0 + u < B ? v[u] : 0.f;
+    }
+    if constexpr (Xch<WT>::on) {  // data-parallel: summed over the ranks
+      if (act) xc.put1(dst, gsum);
+      if (!xc.sync() || !act) return;
+      gsum = xc.get1(dst);
     }
     O.g[dst] = gsum;
     if (c.on) {
@@ -1046,13 +1165,16 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
     int wv = blk * (kWgT / 64) + (t >> 6);
     wv = __builtin_amdgcn_readfirstlane(wv);
     if (wv < NW3) {
-      fc_wgrad<FLAT, F1>(wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], P.wimg ? P.wimg + kFc1T : nullptr, F1);
+      fc_wgrad<FLAT, F1>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], P.wimg ? P.wimg + kFc1T : nullptr,
+                         F1);
     } else if ((wv -= NW3) < NW4) {
-      fc_wgrad<F1, F2>(wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
+      fc_wgrad<F1, F2>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
                        Fc<D>::P2T);
     } else if ((wv -= NW4) < NW5) {
-      fc_wgrad<F2, NC>(wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9], P.wimg ? P.wimg + kFc3T : nullptr,
-                       Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);
+      fc_wgrad<F2, NC>(xc, wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9],
+                       P.wimg ? P.wimg + kFc3T : nullptr, Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);
+    } else if constexpr (Xch<WT>::on) {
+      xc.sync();  // a wave without a tile still joins its block's exchange barriers
     }
   } else {
     // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats.
@@ -1088,13 +1210,35 @@ template <class D>
 __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
   unsigned long long t0 = 0;
   if (mode & LENET_TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-  mw_body<D>(mode, P, O, B, ctrl);
+  mw_body<D, 0>(mode, P, O, B, ctrl, Xch<0>{});
   // LENET_TRACE: 100 MHz wall clock per block (start) and per wave (end): P.trace slots 64 + 5 blk (+1 + wave)
   if ((mode & LENET_TRACE) && P.trace && blockIdx.x < 100) {
     unsigned long long* tr = reinterpret_cast<unsigned long long*>(P.trace) + 64 + 5 * blockIdx.x;
     if (threadIdx.x == 0) tr[0] = t0;
     if ((threadIdx.x & 63) == 0) tr[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// the data-parallel batch-reduction kernel: lenet_mw + the xGMI exchange of every block's slice
+// (struct Xch) + the update, in one launch (WT = rank count; 1 = loopback)
+template <class D, int WT>
+__global__ __launch_bounds__(kWgT) void lenet_mwx(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl,
+                                                  XgmiFused X) {
+  __shared__ int failed;
+  Xch<WT> xc;
+  xc.X = &X;
+  xc.failed = &failed;
+  xc.blk = blockIdx.x;
+  xc.errv = 0u;
+  if (threadIdx.x == 0) {
+    failed = 0;
+    // in flight during the reduction; checked before this block publishes anything
+    xc.errv = __hip_atomic_load(X.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  xc.seq = X.seqs[blockIdx.x] + 1;  // per-block launch counter: identical on every block and rank
+  xc.p = (int)(xc.seq & 1);
+  xc.scale = 1.f / (float)WT;
+  mw_body<D, WT>(mode, P, O, B, ctrl, xc);
 }
 
 // bf16 shadow of the flat parameters + the conv fragment image, from the fp32 masters (start of
@@ -1187,7 +1331,43 @@ void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt&
   hipLaunchKernelGGL(lenet_mw<D>, dim3(nblk), dim3(kWgT), 0, st, mode, P, O, B, A.ctrl);
 }
 
+template <class D>
+void run_dp(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, const XgmiFused& X,
+            hipStream_t st) {
+  const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
+  if (X.G < nblk) throw std::runtime_error("lenet dp step: transport flag rows < reduction blocks");
+  if (X.cap < O.n) throw std::runtime_error("lenet dp step: transport region smaller than the parameters");
+  const float inv_B = 1.f / (float)B;
+  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
+  const int m = mode | LENET_OPT;
+#define MLT_MWX(WV)                                                                                      \
+  case WV:                                                                                               \
+    hipLaunchKernelGGL((lenet_mwx<D, WV>), dim3(nblk), dim3(kWgT), 0, st, m, P, O, B, A.ctrl, X); \
+    break;
+  switch (X.W) {
+    MLT_MWX(1)
+    MLT_MWX(2)
+    MLT_MWX(3)
+    MLT_MWX(4)
+    MLT_MWX(5)
+    MLT_MWX(6)
+    MLT_MWX(7)
+    MLT_MWX(8)
+    default: throw std::runtime_error("lenet dp step: world size outside 1..8");
+  }
+#undef MLT_MWX
+}
+
 }  // namespace lm
+
+void launch_lenet_mfma_dp(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
+                          const XgmiFused& X, hipStream_t stream) {
+  if (B <= 0) return;
+  if (cfg == LENET_TINY)
+    lm::run_dp<lm::DmTiny>(mode, B, P, A, O, X, stream);
+  else
+    lm::run_dp<lm::DmDefault>(mode, B, P, A, O, X, stream);
+}
 
 int lenet_mfma_slab_floats(int cfg) { return cfg == LENET_TINY ? lm::DmTiny::SLABN : lm::DmDefault::SLABN; }
 int lenet_mfma_wimg_elems() { return lm::kWimgTot; }

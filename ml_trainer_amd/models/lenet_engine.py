@@ -4,19 +4,26 @@ One training step of the reference hot loop (``src/trainer.py:180-197``:
 zero_grad -> H2D -> forward -> CE -> loss.item() -> backward (DDP all-reduce)
 -> optimizer.step -> metric) becomes:
 
-* W = 1: six kernels ``K1..K6`` (csrc/kernels/lenet.hip) -- augmentation of an
-  HBM-resident uint8 dataset, forward, softmax-CE + on-device loss/accuracy
-  accumulation, backward and the fused optimizer update -- captured as a
-  multi-step hipGraph, so the host submits one graph per ``steps_per_graph``
-  steps and never synchronises inside an epoch (B12: no ``loss.item()``, no
-  sklearn host round trip per batch);
-* W > 1: K1..K5 -> RCCL all-reduce (AVG) of the flat gradient buffer (one
-  248 KB bucket; latency-bound, so a single collective) -> fused flat optimizer
-  launch that reads lr/step from device memory. With the native communicator
-  (parallel/comm.py) the all-reduce is enqueued by C++ on the capture stream, so
-  multi-step hipGraphs contain compute, collective and update of every step and
-  the host is out of the loop exactly as at W = 1; without it (MLT_NATIVE_COMM=0)
-  each step is graph(K1..K5) + torch.distributed all-reduce + optimizer launch.
+* W = 1, bf16 (the bench default, BASELINE configs 2/3): TWO kernels per step
+  (csrc/kernels/lenet_mfma.hip) -- ``lenet_ms`` (one CU per sample: on-GPU
+  RandomCrop/HFlip/Normalize of the HBM-resident uint8 image, conv/fc forward on
+  MFMA, softmax-CE, the whole backward of the sample) and ``lenet_mw`` (batch
+  reductions in sample order, on-device loss/accuracy sums, the fused optimizer
+  update of the fp32 masters + bf16 shadow); fp32 (the reference dtype): four
+  kernels (csrc/kernels/lenet.hip). Either way captured as a multi-step hipGraph,
+  so the host submits one graph per ``steps_per_graph`` steps and never
+  synchronises inside an epoch (B12: no ``loss.item()``, no sklearn round trip);
+* W > 1, bf16 over xGMI: still TWO kernels per step -- ``lenet_ms``, then
+  ``lenet_mwx``, whose blocks publish their batch-reduced gradient slice into an
+  IPC-shared region, pull the peers' slices over xGMI, sum them in rank order and
+  apply the update in the same launch ("xgmi-fused"; W = 1 loopback for timing);
+* W > 1 otherwise: the step's kernels -> all-reduce (AVG) of the flat gradient
+  (one 248 KB bucket; latency-bound, so a single collective: the one-/two-shot
+  xGMI kernels or RCCL, chosen by a timed vote) -> optimizer launch reading
+  lr/step from device memory, all enqueued from C++ on the capture stream, so the
+  multi-step hipGraphs contain compute, collective and update of every step;
+  without a native transport (MLT_NATIVE_COMM=0) each step is graph(kernels) +
+  torch.distributed all-reduce + optimizer launch.
 
 The device step counter ``ctrl`` (``[global_step, step_in_epoch]``) drives
 batch selection from the epoch permutation, the augmentation RNG, the lr table
@@ -35,6 +42,13 @@ from ml_trainer_amd.utils.flat import FlatParams
 
 CIFAR_MEAN = (0.4914, 0.4822, 0.4465)
 CIFAR_STD = (0.2023, 0.1994, 0.2010)
+
+
+def fused_dp_enabled() -> bool:
+    """bf16 + xGMI: fold the gradient exchange into the batch-reduction kernel (MLT_LENET_FUSED_DP=0:
+    the four-launch step, for A/B)."""
+    import os
+    return os.environ.get("MLT_LENET_FUSED_DP", "1") != "0"
 
 
 class TransportError(RuntimeError):
@@ -124,6 +138,14 @@ class LeNetStepEngine:
             self.xgmi = x = None
         if self.comm is None and self.xgmi is None:
             return
+        if x is not None and self.precision == "bf16" and fused_dp_enabled():
+            # bf16 over xGMI: exchange + update folded into the batch-reduction kernel (two
+            # launches per step, as at W = 1) -- no standalone collective to vote on
+            self.eng.set_xgmi(x)
+            self.eng.fused_dp = True
+            self.dp_transport = "xgmi-fused"
+            return
+        self.eng.fused_dp = False
         t = self.flat.grad.clone()
         cands = []
         if x is not None:
@@ -181,8 +203,14 @@ class LeNetStepEngine:
         communicator (unblocking any stuck collective) and raises TransportError."""
         if self.dp_transport.startswith("xgmi") and self.xgmi is not None:
             if self.xgmi.error():
-                raise TransportError("xGMI all-reduce: a peer did not arrive within "
-                                     f"{self.xgmi.timeout_ms} ms; this rank applied no part of that step")
+                if self.dp_transport == "xgmi-fused":
+                    what = ("the update of every gradient slice whose peers did not arrive was skipped on "
+                            "this rank, slices whose peers arrived were applied: replicas may differ, resume "
+                            "from the last checkpoint")
+                else:
+                    what = "this rank applied no part of that step (a peer may have applied it)"
+                raise TransportError(f"xGMI gradient exchange: a peer did not arrive within "
+                                     f"{self.xgmi.timeout_ms} ms; {what}")
         elif self.dp_transport == "rccl" and self.comm is not None:
             err = self.comm.async_error()
             if err:
@@ -259,10 +287,13 @@ class LeNetStepEngine:
         """Single-rank step with the optimizer fused into the backward kernels."""
         return self.world_size == 1 and self.dp_transport == "none"
 
-    def use_transport(self, comm=None, xgmi=None) -> None:
+    def use_transport(self, comm=None, xgmi=None, fused: Optional[bool] = None) -> None:
         """Route the step's gradient through ``comm`` (a ``_C.Communicator``) or ``xgmi`` inside
         the captured graph -- also at world size 1, which rehearses the data-parallel step (RCCL
-        all-reduce + flat optimizer launch) on a single GPU."""
+        all-reduce + flat optimizer launch, or the xGMI exchange against this rank itself) on a
+        single GPU. ``fused`` (bf16 + xgmi; default: on unless MLT_LENET_FUSED_DP=0): the
+        exchange runs inside the batch-reduction kernel (two launches per step) instead of a
+        standalone all-reduce + apply launch (four)."""
         if (comm is None) == (xgmi is None):
             raise ValueError("pass exactly one of comm / xgmi")
         self.comm, self.xgmi = comm, xgmi
@@ -271,13 +302,20 @@ class LeNetStepEngine:
             self.eng.set_comm(comm)
             self.dp_transport = "rccl"
         else:
+            if fused is None:
+                fused = fused_dp_enabled()
+            fused = bool(fused) and self.precision == "bf16"
             self.eng.set_comm(None)
             self.eng.set_xgmi(xgmi)
-            self.dp_transport = "xgmi-twoshot" if getattr(xgmi, "algo", 0) == 1 else "xgmi-oneshot"
+            self.eng.fused_dp = fused
+            if fused:
+                self.dp_transport = "xgmi-fused"
+            else:
+                self.dp_transport = "xgmi-twoshot" if getattr(xgmi, "algo", 0) == 1 else "xgmi-oneshot"
 
     @property
     def in_graph_collective(self) -> bool:
-        return self.dp_transport in ("rccl", "xgmi-oneshot", "xgmi-twoshot")
+        return self.dp_transport in ("rccl", "xgmi-oneshot", "xgmi-twoshot", "xgmi-fused")
 
     def _train_mode(self) -> int:
         C = self.C

@@ -94,22 +94,15 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
     if int(flag.item()) == 0:
         return None
-    # self-test of both algorithms (one-shot, then two-shot): two launches each (both buffer
-    # parities), exact small-integer sums, an odd length (tail handling). A peer timeout (sticky
-    # error word) disqualifies the object; wrong two-shot sums only disqualify the two-shot
-    # algorithm (x.two_shot_ok), every rank agreeing through the MIN vote.
+    # self-test of both algorithms (one-shot, then two-shot). A peer timeout (sticky error word)
+    # disqualifies the object; wrong two-shot sums only disqualify the two-shot algorithm
+    # (x.two_shot_ok), every rank agreeing through the MIN vote.
     n = max(4, min(int(capacity), 1 << 16))
-    n -= 1 - n % 2
+    n -= 1 - n % 2  # odd length: tail handling
     good = [True, True]
     for algo in (0, 1):
         x.algo = algo
-        for it in range(2):
-            t = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97).add_(rank + 1 + it)
-            x.all_reduce(t, average=False)
-            ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
-                world * (world + 1) // 2 + it * world)
-            torch.cuda.synchronize(dev)
-            good[algo] = good[algo] and bool(torch.equal(t, ref))
+        good[algo] = _xgmi_selftest(x, world, rank, n, dev)
     x.algo = 0
     ok = x.error() == 0
     flag = torch.tensor([1 if (ok and good[0]) else 0, 1 if (ok and good[1]) else 0], dtype=torch.int32,
@@ -119,4 +112,56 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     if one != 1:
         return None
     x.two_shot_ok = two == 1
+    return x
+
+
+def _payload(q: int, it: int, n: int) -> torch.Tensor:
+    """Rank q's random fp32 test payload of round ``it`` (any rank can regenerate any peer's)."""
+    g = torch.Generator().manual_seed(0x5EED + 7919 * q + 104729 * it)
+    return torch.randn(n, generator=g, dtype=torch.float32) * torch.exp2(torch.randint(-8, 9, (n,), generator=g)).float()
+
+
+def _xgmi_selftest(x, world: int, rank: int, n: int, dev, rounds: int = 12) -> bool:
+    """Visibility test of the current algorithm on the real fabric, every word checked:
+    (1) two launches with exact small-integer sums (both buffer parities);
+    (2) ``rounds`` back-to-back launches of random fp32 payloads (no synchronisation between
+        them, so parity reuse runs at full speed) while a side stream keeps the GPU busy with
+        GEMMs (uneven load), each result compared bitwise with the host sum in RANK ORDER --
+        what every rank's kernel computes. A stale peer read anywhere fails the test, and the
+        caller then keeps RCCL instead of training on stale data."""
+    ok = True
+    for it in range(2):
+        t = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97).add_(rank + 1 + it)
+        x.all_reduce(t, average=False)
+        ref = torch.arange(n, dtype=torch.float32, device=dev).remainder_(97) * world + (
+            world * (world + 1) // 2 + it * world)
+        torch.cuda.synchronize(dev)
+        ok = ok and bool(torch.equal(t, ref))
+    bufs = [_payload(rank, it, n).to(dev) for it in range(rounds)]
+    side = torch.cuda.Stream(dev)
+    a = torch.randn(2048, 2048, device=dev)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(side):  # load on the chip while the exchanges run
+        for _ in range(8):
+            a = torch.tanh(a @ a * 1e-3)
+    for t in bufs:
+        x.all_reduce(t, average=False)
+    torch.cuda.synchronize(dev)
+    for it, t in enumerate(bufs):
+        ref = _payload(0, it, n)
+        for q in range(1, world):
+            ref = ref + _payload(q, it, n)  # rank order, fp32: bit-identical to the kernels' sums
+        ok = ok and bool(torch.equal(t.cpu(), ref))
+    return ok and x.error() == 0
+
+
+def create_xgmi_loopback(capacity: int, device: Optional[torch.device] = None, timeout_ms: int = 30000):
+    """A one-rank xGMI transport whose only peer is this rank itself: times the data-parallel
+    step's exchange (publish, flag, poll, pull, rank-ordered sum) on a single GPU."""
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    x = C.XgmiAllReduce(int(capacity), 1, 0, dev.index)
+    x.timeout_ms = int(timeout_ms)
+    x.open([x.handle()])
     return x

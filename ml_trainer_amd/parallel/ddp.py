@@ -75,8 +75,7 @@ class DistributedDataParallel(nn.Module):
             self._ncomm = comm
             self.world_size = int(comm.size)
         elif comm is None and self.flat.device.type == "cuda" and self.world_size > 1:
-            from ml_trainer_amd.parallel.comm import create_native_comm
-            self._ncomm = create_native_comm(process_group, self.flat.device)
+            self._ncomm = self._native_comm_agreed(process_group)
         self.comm_backend = "native-rccl" if self._ncomm is not None else f"torch.distributed-{self.backend}"
         self._bucket_cap = int((bucket_cap_mb or DEFAULT_BUCKET_MB) * 2 ** 20)
         self._first_cap = int((first_bucket_mb or DEFAULT_FIRST_BUCKET_MB) * 2 ** 20)
@@ -110,6 +109,23 @@ class DistributedDataParallel(nn.Module):
             self.flat.grad_ready_hooks.append(lambda p: self._direct_hooks[id(p)](p))
         if broadcast_parameters and self.world_size > 1:
             self.broadcast_state()
+
+    def _native_comm_agreed(self, process_group):
+        """The native RCCL communicator on every rank, or on none: a bring-up failure on any rank
+        (caught, warned) is agreed through a MIN vote, and then every rank keeps torch.distributed
+        together (the LeNet engine's pattern, models/lenet_engine.py)."""
+        import warnings
+        from ml_trainer_amd.parallel.comm import create_native_comm, native_comm_enabled
+        if not native_comm_enabled() or self.backend != "nccl":
+            return None
+        try:
+            c = create_native_comm(process_group, self.flat.device)
+        except RuntimeError as e:
+            warnings.warn(f"native RCCL communicator unavailable ({e}); DDP uses torch.distributed")
+            c = None
+        ok = torch.tensor([1.0 if c is not None else 0.0], device=self.flat.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=process_group)
+        return c if ok.item() == 1.0 else None
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self) -> None:

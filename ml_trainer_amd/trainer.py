@@ -33,6 +33,7 @@ import json
 import math
 import os
 import random
+import sys
 import time
 import warnings
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -275,6 +276,7 @@ class Trainer:
     def _engine_eligible(self, for_eval: bool = False) -> bool:
         o = self.opts
         if o.use_engine is False or self.device.type != "cuda" or not native_available():
+            self._warn_precision_ignored()
             return False
         from ml_trainer_amd.models.lenet import MLModel
         ok = (isinstance(self._core, MLModel) and self.criterion_type == "cross_entropy"
@@ -286,13 +288,23 @@ class Trainer:
             if o.use_engine:
                 raise RuntimeError("use_engine=True but the model/criterion/optimizer/options are not supported "
                                    "by the fused LeNet engine")
+            self._warn_precision_ignored()
             return False
         loader = self.val_loader if for_eval else self.train_loader
         if o.device_data is False or device_dataset_spec(loader.dataset) is None:
             if o.use_engine:
                 raise RuntimeError("use_engine=True needs a device-capable dataset (uint8 [N,32,32,3])")
+            self._warn_precision_ignored()
             return False
         return True
+
+    def _warn_precision_ignored(self) -> None:
+        """precision='bf16' is the fused LeNet engine's step dtype; any other path trains in fp32."""
+        if self.opts.precision == "bf16" and not getattr(self, "_prec_warned", False):
+            self._prec_warned = True
+            warnings.warn("precision='bf16' applies to the fused LeNet engine only, which is not used for this "
+                          "run (model / criterion / optimizer / options / dataset): training runs in fp32; "
+                          "use amp='bf16' for bf16 autocast on generic models")
 
     def _get_engine(self):
         from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
@@ -578,7 +590,11 @@ class Trainer:
             path = os.path.join(model_dir, "model.pth")
             extra = [] if trainer_state is None else [(os.path.join(model_dir, "trainer_state.pt"),
                                                        ckpt.to_host(trainer_state))]
-            self._ackpt.save(self.model, path, extra)  # on disk by the next save / the end of fit()
+            self._ackpt.save(self.model, path, extra)
+            if not getattr(self, "_in_fit", False):
+                # a direct call (the reference API) returns with the files on disk and any write
+                # error raised; inside fit() they are on disk by the next save / the end of fit()
+                self._ackpt.wait()
             return path
         path = ckpt.save_model_file(self.model, model_dir)
         if trainer_state is not None:
@@ -642,7 +658,10 @@ class Trainer:
                 if self.opts.save_trainer_state and st is None:
                     st = self._trainer_state(epoch)
                 self.save_model(self.model_dir, st if self.opts.save_trainer_state else None)
-            mdist.barrier()  # reference has no barrier after the rank-0 save
+            # reference has no barrier after the rank-0 save; with async_checkpoint it
+            # publishes the host snapshot (the files land in the background, on disk by the next
+            # save / the end of fit(), whose wait re-raises a write error)
+            mdist.barrier()
         else:
             self.save_model(self.model_dir, self._trainer_state(epoch) if self.opts.save_trainer_state else None)
 
@@ -664,6 +683,7 @@ class Trainer:
         logger.info("Start training..")
         if self._watchdog:
             self._watchdog.start()
+        self._in_fit = True
         try:
             for epoch in range(self.start_epoch, self.epochs + 1):
                 logger.info(f"{'-' * 30} EPOCH {epoch} / {self.epochs} {'-' * 30}")
@@ -687,9 +707,18 @@ class Trainer:
                     logger.info(f"valid loss: {self.val_losses[-1]}\n\n")
                 self._write_metrics(epoch)
         finally:
+            self._in_fit = False
             if self._watchdog:
                 self._watchdog.stop()
-            self._checkpoint_wait()  # the last async model.pth is on disk when fit() returns
+            if sys.exc_info()[0] is None:
+                self._checkpoint_wait()  # the last async model.pth is on disk when fit() returns
+            else:
+                # training already failed: wait for the pending write, but let the ORIGINAL
+                # exception propagate (a write error is logged, not raised over it)
+                try:
+                    self._checkpoint_wait()
+                except Exception as e:  # noqa: BLE001
+                    logger.warning("checkpoint write failed while handling an earlier error", error=repr(e))
         self.history = {
             "epochs": [*range(1, self.epochs + 1)],
             "train_loss": self.train_losses,

@@ -7,6 +7,7 @@ import time
 import pytest
 import torch
 
+from ml_trainer_amd.data.cifar10 import SyntheticCIFAR10
 from ml_trainer_amd.models.lenet import MLModel
 from ml_trainer_amd.trainer import Trainer
 from ml_trainer_amd.utils.watchdog import Watchdog
@@ -113,6 +114,40 @@ def test_async_checkpointer_write_error_surfaces(tmp_path):
     ck.save(MLModel("tiny"), str(tmp_path / "ok" / "model.pth"))
     assert ck.wait() == str(tmp_path / "ok" / "model.pth")
     ck.close()
+
+
+def test_async_save_model_direct_call_is_on_disk(tmp_path):
+    """The reference API's save_model(dir) called outside fit() with async_checkpoint: the file
+    exists when it returns, and a write error is raised from the call (not lost in a Future)."""
+    tr = Trainer(MLModel("tiny"), options={"progress": False, "async_checkpoint": True})
+    d = tmp_path / "m"
+    d.mkdir()
+    path = tr.save_model(str(d))
+    assert os.path.exists(path)
+    sd = torch.load(path, weights_only=True)
+    assert set(sd) == set(MLModel("tiny").state_dict())
+    blocker = tmp_path / "f"
+    blocker.write_text("x")
+    with pytest.raises(OSError):
+        tr.save_model(str(blocker))
+
+
+def test_fit_error_not_masked_by_checkpoint_error(tmp_path, monkeypatch):
+    """An exception raised by training propagates out of fit() even if the pending async write
+    also fails (the write error is logged, not raised over it)."""
+    tr_set, va_set = SyntheticCIFAR10(64, True, seed=1), SyntheticCIFAR10(32, False, seed=1)
+    tr = Trainer(MLModel("tiny"), datasets=(tr_set, va_set), epochs=2, batch_size=32, model_dir=str(tmp_path),
+                 options={"progress": False, "async_checkpoint": True})
+
+    def boom(*a, **k):
+        raise ValueError("training failed")
+
+    def bad_wait():
+        raise OSError("disk gone")
+    monkeypatch.setattr(tr, "_train_one_epoch", boom)
+    monkeypatch.setattr(tr, "_checkpoint_wait", bad_wait)
+    with pytest.raises(ValueError, match="training failed"):
+        tr.fit()
 
 
 def test_watchdog_fires_and_beats():

@@ -279,3 +279,61 @@ def test_bf16_host_change_of_masters_is_packed(dev):
         torch.cuda.synchronize()
         runs.append(flat.data.clone())
     assert torch.equal(runs[0], runs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["sgd", "adamw"])
+def test_bf16_fused_dp_loopback_matches_fused(dev, opt):
+    """The two-launch data-parallel step (lenet_mwx: batch reductions -> publish into the xGMI
+    region -> flag -> poll -> pull -> rank-ordered sum -> update, one launch) against the loopback
+    transport (the only peer is this rank) == the fused single-rank step, bitwise; and the graph
+    holds two kernels per step."""
+    from ml_trainer_amd.parallel.comm import create_xgmi_loopback
+    data, targets = _toy_data(256, 5)
+    runs = []
+    for dp in (False, True):
+        m = _mk("default", 13).to(dev)
+        eng, flat = _engine(m, opt, max_batch=32, lr=1e-3)
+        if dp:
+            x = create_xgmi_loopback(flat.numel, dev)
+            eng.use_transport(xgmi=x)
+            assert eng.dp_transport == "xgmi-fused" and eng.in_graph_collective
+        eng.set_dataset(data, targets, batch_size=32)
+        eng.start_epoch(torch.arange(256))
+        eng.train_steps(32, 6, use_graph=True, steps_per_graph=3)
+        eng.check_transport()
+        torch.cuda.synchronize()
+        if dp:
+            assert x.error() == 0
+            assert eng.eng.graph_nodes(eng._train_mode(), 32, 3) == 6  # 2 kernels x 3 steps
+        runs.append((flat.data.clone(), flat.grad.clone(), eng.stats.clone(), eng.ctrl.clone()))
+    for a, b in zip(runs[0], runs[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_bf16_fused_dp_loopback_fault_raises(dev):
+    """Fault injection on the loopback transport: the withheld blocks time out, the sticky error
+    word makes the host raise TransportError, and every later launch publishes and applies nothing."""
+    from ml_trainer_amd.models.lenet_engine import TransportError
+    from ml_trainer_amd.parallel.comm import create_xgmi_loopback
+    data, targets = _toy_data(256, 5)
+    m = _mk("default", 13).to(dev)
+    eng, flat = _engine(m, "sgd", max_batch=32, lr=1e-3)
+    x = create_xgmi_loopback(flat.numel, dev, timeout_ms=200)
+    eng.use_transport(xgmi=x)
+    eng.set_dataset(data, targets, batch_size=32)
+    eng.start_epoch(torch.arange(256))
+    eng.train_steps(32, 2, use_graph=True, steps_per_graph=1)
+    eng.check_transport()
+    x.fault = 1
+    eng.use_transport(xgmi=x)  # recapture with the fault live
+    with pytest.raises(TransportError):
+        eng.train_steps(32, 1, use_graph=True, steps_per_graph=1)
+        eng.check_transport()
+    torch.cuda.synchronize()
+    before = flat.data.clone()
+    with pytest.raises(TransportError):  # sticky: nothing is applied any more
+        eng.train_steps(32, 2, use_graph=True, steps_per_graph=1)
+    torch.cuda.synchronize()
+    assert torch.equal(flat.data, before)

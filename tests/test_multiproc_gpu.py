@@ -157,6 +157,7 @@ def _xgmi_sizes_worker(rank, world, port, out_dir, algo):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
+    os.environ["MLT_XGMI_TIMEOUT_MS"] = "20000"
     x = create_xgmi_allreduce(None, 70000, dev, allow_gloo=True)
     assert x is not None and x.two_shot_ok
     x.algo = algo
@@ -177,16 +178,75 @@ def _xgmi_sizes_worker(rank, world, port, out_dir, algo):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [3, 4])
+@pytest.mark.parametrize("world", [3, 4, 8])
 @pytest.mark.parametrize("algo", [0, 1])
-def test_xgmi_allreduce_three_four_ranks_one_gpu(world, algo):
-    """The one-shot / two-shot kernels at W = 3, 4 (the 4- and 8-GPU node's code paths: slice and
-    flag indexing, partial and empty slices) rehearsed as W processes on the box's one GPU."""
+def test_xgmi_allreduce_three_four_eight_ranks_one_gpu(world, algo):
+    """The one-shot / two-shot kernels at W = 3, 4, 8 (the 4- and 8-GPU node's code paths: slice and
+    flag indexing, partial and empty slices; W = 8 is what the node's vote runs) rehearsed as W
+    processes on the box's one GPU; every result bit-exact against the host sum."""
     r = _run(_xgmi_sizes_worker, world, algo)
     assert len(r) == world
     for d in r:
         assert d["ok"].all(), d["ok"]
         assert d["err"].tolist() == [0]
+
+
+def _fused_dp_worker(rank, world, port, out_dir):
+    """bf16 LeNet data-parallel step over xGMI: the two-launch step (exchange folded into the
+    batch-reduction kernel) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
+    dist_env(rank, world, port)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    os.environ["MLT_XGMI_TIMEOUT_MS"] = "20000"
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.parallel.comm import create_xgmi_allreduce
+    from ml_trainer_amd.parallel.sampler import shard_indices
+    from ml_trainer_amd.utils.flat import FlatParams
+    out = {}
+    gd = torch.Generator().manual_seed(3)
+    N = 64 * world
+    data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
+    targets = torch.randint(0, 10, (N,), generator=gd)
+    for fused in (True, False):
+        torch.manual_seed(0)
+        m = MLModel().to(dev)
+        flat = FlatParams(m.parameters())
+        opt = build_optimizer("adamw", m.parameters(), lr=1e-3, weight_decay=0.01, flat=flat)
+        eng = LeNetStepEngine(m, flat, max_batch=8, optimizer=opt, world_size=world, precision="bf16")
+        xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
+        assert xe is not None
+        xe.algo = 0
+        eng.use_transport(xgmi=xe, fused=fused)
+        assert eng.dp_transport == ("xgmi-fused" if fused else "xgmi-oneshot")
+        eng.set_dataset(data, targets, batch_size=8)
+        eng.start_epoch(torch.as_tensor(shard_indices(N, world, rank, shuffle=True, seed=0, epoch=0),
+                                        dtype=torch.int32))
+        eng.train_steps(8, 6, use_graph=True, steps_per_graph=3)
+        eng.check_transport()
+        torch.cuda.synchronize()
+        out[f"p{int(fused)}"] = flat.data.cpu()
+        out[f"g{int(fused)}"] = flat.grad.cpu()
+        out[f"nodes{int(fused)}"] = eng.eng.graph_nodes(eng._train_mode(), 8, 3)
+        out[f"err{int(fused)}"] = xe.error()
+        dist.barrier()
+    torch.save(out, os.path.join(out_dir, f"f{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_lenet_bf16_fused_dp_matches_four_launch(world):
+    """Two launches per data-parallel step, bitwise equal to the four-launch step and identical on
+    every rank (W = 8: the node's size, as 8 processes on the box's one GPU)."""
+    r = _run(_fused_dp_worker, world)
+    assert len(r) == world
+    for d in r:
+        assert d["err1"] == 0 and d["err0"] == 0
+        assert torch.equal(d["p1"], d["p0"]) and torch.equal(d["g1"], d["g0"])
+        assert d["nodes1"] == 6 and d["nodes0"] == 12, (d["nodes1"], d["nodes0"])
+        assert torch.equal(d["p1"], r[0]["p1"])
 
 
 def _bert_zero_worker(rank, world, port, out_dir):
