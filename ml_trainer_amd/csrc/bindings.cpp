@@ -897,7 +897,18 @@ class PyPrefetcher {
     TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "dst must be a contiguous device tensor");
     TORCH_CHECK(nbytes >= 0 && nbytes <= bytes_ && nbytes <= (int64_t)(dst.numel() * dst.element_size()),
                 "copy size");
-    p_.copy_to_device(i, dst.data_ptr(), (size_t)nbytes, cur_stream());
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    p_.copy_to_device(i, dst.data_ptr(), (size_t)nbytes);
+  }
+  // the current stream waits for slot i's copy (call where the batch is consumed)
+  void acquire(int i) {
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    p_.acquire(i, cur_stream());
+  }
+  // the current stream's work on device buffer i is enqueued: its next copy may follow it
+  void release(int i) {
+    TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
+    p_.release(i, cur_stream());
   }
   bool ready(int i) {
     TORCH_CHECK(i >= 0 && i < p_.depth(), "slot index");
@@ -1346,6 +1357,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)
       .def("copy_to_device", &PyPrefetcher::copy_to_device)
+      .def("acquire", &PyPrefetcher::acquire)
+      .def("release", &PyPrefetcher::release)
       .def("ready", &PyPrefetcher::ready)
       .def("wait", &PyPrefetcher::wait)
       .def_property_readonly("depth", &PyPrefetcher::depth)

@@ -44,11 +44,15 @@ class HipGraph {
   size_t nodes_ = 0;
 };
 
-// Pinned-host double/triple-buffered prefetcher: a worker thread fills pinned
-// slots through a user callback (e.g. collating a batch on the host), and the
-// consumer issues hipMemcpyAsync H2D on a dedicated copy stream, recording an
-// event that the compute stream waits on. This is what feeds datasets that do
-// not live in HBM (north star: "prefetches into pinned host memory with
+// Pinned-host ring prefetcher: `depth` persistent hipHostMalloc slots, each paired by the caller
+// with a device buffer. The H2D hipMemcpyAsync runs on a dedicated copy stream and overlaps the
+// compute stream's kernels; the two streams meet only where the data dependences are:
+//   copy_to_device(i)  copy stream waits for release(i) -- the compute that last read device
+//                      buffer i -- then copies slot i and records ready(i);
+//   acquire(i, s)      stream s waits for ready(i) (at the point the batch is CONSUMED);
+//   release(i, s)      records on s, after the consumer's work on buffer i was enqueued.
+// With d buffers the copy of batch k + d - 1 runs while batch k computes. This is what feeds
+// datasets that do not live in HBM (north star: "prefetches into pinned host memory with
 // hipMemcpyAsync on a side stream").
 class PinnedPrefetcher {
  public:
@@ -57,16 +61,18 @@ class PinnedPrefetcher {
   ~PinnedPrefetcher();
   void* slot_ptr(int i) const { return slots_[i]; }
   int depth() const { return depth_; }
-  // Copy `bytes` of pinned slot `i` to `dst` on the copy stream and make
-  // `compute` wait for it. The slot may be refilled once `slot_ready(i)`.
-  void copy_to_device(int i, void* dst, size_t bytes, hipStream_t compute);
+  void copy_to_device(int i, void* dst, size_t bytes);
+  void acquire(int i, hipStream_t compute);
+  void release(int i, hipStream_t compute);
+  // the host slot may be refilled once its copy is done
   bool slot_ready(int i);
   void wait_slot(int i);
 
  private:
   std::vector<void*> slots_;
-  std::vector<hipEvent_t> events_;
-  std::vector<hipEvent_t> before_;
+  std::vector<hipEvent_t> events_;    // ready(i): copy of slot i done
+  std::vector<hipEvent_t> released_;  // release(i): compute done reading device buffer i
+  std::vector<char> has_release_;
   hipStream_t copy_stream_ = nullptr;
   size_t slot_bytes_;
   int depth_;

@@ -46,11 +46,12 @@ PinnedPrefetcher::PinnedPrefetcher(size_t slot_bytes, int depth, int device)
   hip_check(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate(copy)");
   slots_.resize(depth, nullptr);
   events_.resize(depth, nullptr);
-  before_.resize(depth, nullptr);
+  released_.resize(depth, nullptr);
+  has_release_.assign(depth, 0);
   for (int i = 0; i < depth; ++i) {
     hip_check(hipHostMalloc(&slots_[i], slot_bytes, hipHostMallocDefault), "hipHostMalloc");
     hip_check(hipEventCreateWithFlags(&events_[i], hipEventDisableTiming), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&before_[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&released_[i], hipEventDisableTiming), "hipEventCreate");
   }
 }
 
@@ -60,23 +61,31 @@ PinnedPrefetcher::~PinnedPrefetcher() {
       hipEventSynchronize(events_[i]);
       hipEventDestroy(events_[i]);
     }
-    if (before_[i]) hipEventDestroy(before_[i]);
+    if (released_[i]) hipEventDestroy(released_[i]);
     if (slots_[i]) hipHostFree(slots_[i]);
   }
   if (copy_stream_) hipStreamDestroy(copy_stream_);
 }
 
-void PinnedPrefetcher::copy_to_device(int i, void* dst, size_t bytes, hipStream_t compute) {
+void PinnedPrefetcher::copy_to_device(int i, void* dst, size_t bytes) {
   if (i < 0 || i >= depth_) throw std::out_of_range("prefetch slot");
   if (bytes > slot_bytes_) throw std::invalid_argument("prefetch copy larger than slot");
-  // The copy stream must not overwrite `dst` while compute still reads the
-  // previous batch there: order the copy after everything queued on compute.
-  // (per-slot event: re-recording it is safe, the copy stream's wait captured the prior record)
-  hip_check(hipEventRecord(before_[i], compute), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(copy_stream_, before_[i], 0), "hipStreamWaitEvent");
+  // device buffer i may still be read by the batch that used it last: wait for ITS release only
+  // (a wait captures the event's latest record, so re-recording it later is safe)
+  if (has_release_[i]) hip_check(hipStreamWaitEvent(copy_stream_, released_[i], 0), "hipStreamWaitEvent");
   hip_check(hipMemcpyAsync(dst, slots_[i], bytes, hipMemcpyHostToDevice, copy_stream_), "hipMemcpyAsync");
   hip_check(hipEventRecord(events_[i], copy_stream_), "hipEventRecord");
+}
+
+void PinnedPrefetcher::acquire(int i, hipStream_t compute) {
+  if (i < 0 || i >= depth_) throw std::out_of_range("prefetch slot");
   hip_check(hipStreamWaitEvent(compute, events_[i], 0), "hipStreamWaitEvent");
+}
+
+void PinnedPrefetcher::release(int i, hipStream_t compute) {
+  if (i < 0 || i >= depth_) throw std::out_of_range("prefetch slot");
+  hip_check(hipEventRecord(released_[i], compute), "hipEventRecord");
+  has_release_[i] = 1;
 }
 
 bool PinnedPrefetcher::slot_ready(int i) { return hipEventQuery(events_[i]) == hipSuccess; }

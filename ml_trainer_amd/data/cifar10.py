@@ -133,14 +133,28 @@ class CIFAR10(_CifarBase):
 
 
 class SyntheticCIFAR10(_CifarBase):
-    """Seeded random CIFAR-10-shaped dataset (50,000 train / 10,000 test by default)."""
+    """Seeded random CIFAR-10-shaped dataset (50,000 train / 10,000 test by default).
+
+    ``learnable``: False = uniform noise (throughput runs); True = a class-dependent brightness
+    offset (fitted within an epoch: plumbing tests); ``"pattern"`` = each class a fixed 4x4-block
+    colour template (the same for train and test: ``pattern_seed``) blended 12/88 with uniform
+    noise -- the model has to learn spatial colour filters and accuracy climbs over several epochs
+    (training-quality comparisons, e.g. bf16 vs fp32)."""
 
     def __init__(self, n: Optional[int] = None, train: bool = True, transform: Optional[Callable] = None,
-                 target_transform: Optional[Callable] = None, seed: int = 0, learnable: bool = False):
+                 target_transform: Optional[Callable] = None, seed: int = 0, learnable=False,
+                 pattern_seed: int = 1234):
         n = n if n is not None else (50000 if train else 10000)
         rng = np.random.default_rng(seed + (0 if train else 1))
         self.targets = rng.integers(0, 10, size=n).tolist()
-        if learnable:
+        if learnable == "pattern":
+            prng = np.random.default_rng(pattern_seed)
+            tmpl = prng.integers(0, 256, size=(10, 4, 4, 3)).astype(np.float32)
+            tmpl = tmpl.repeat(8, axis=1).repeat(8, axis=2)  # [10, 32, 32, 3]
+            t = np.asarray(self.targets)
+            noise = rng.integers(0, 256, size=(n, 32, 32, 3)).astype(np.float32)
+            self.data = np.clip(0.12 * tmpl[t] + 0.88 * noise, 0, 255).astype(np.uint8)
+        elif learnable:
             # class-dependent colour offset so a model can actually fit it (tests)
             t = np.asarray(self.targets, dtype=np.int16).reshape(n, 1, 1, 1)
             noise = rng.integers(0, 40, size=(n, 32, 32, 3), dtype=np.int16)

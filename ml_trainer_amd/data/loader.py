@@ -73,10 +73,12 @@ class DeviceDataset:
 
 class NativePinnedPrefetcher:
     """Batches staged through the native pinned-host ring (csrc/runtime/runtime.cpp
-    ``PinnedPrefetcher``): ``depth`` persistent hipHostMalloc slots, hipMemcpyAsync on a
-    dedicated copy stream ordered after the compute stream's prior work, and an event the
-    compute stream waits on -- no per-batch pinned allocation, no host synchronisation
-    except reusing a slot whose previous copy is still in flight."""
+    ``PinnedPrefetcher``): ``depth`` persistent hipHostMalloc slots + device buffers,
+    hipMemcpyAsync on a dedicated copy stream. The copy of batch k + depth - 1 waits only for
+    the compute that last read its device buffer (batch k - 1's, released when the consumer
+    asked for batch k), and the compute stream waits for a batch's copy only where the batch is
+    consumed -- so the copies run under the previous batches' kernels. No per-batch pinned
+    allocation, no host synchronisation except reusing a host slot whose copy is in flight."""
 
     def __init__(self, loader: DataLoader, device: torch.device, depth: int = 3):
         from ml_trainer_amd.ops._ext import require_native
@@ -97,6 +99,8 @@ class NativePinnedPrefetcher:
 
     def _ensure(self, nbytes: int) -> None:
         if self.pf is None or self.pf.slot_bytes < nbytes:
+            if self.pf is not None:
+                torch.cuda.current_stream(self.device).synchronize()  # old buffers may still be read
             self.pf = self.C.PinnedPrefetcher(int(nbytes), self.depth, self.device.index or 0)
             self.dev_bufs = [torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
                              for _ in range(self.depth)]
@@ -107,20 +111,21 @@ class NativePinnedPrefetcher:
         x, y = x.contiguous(), y.contiguous()
         xb, yo, total = self._layout(x, y)
         self._ensure(total)
-        self.pf.wait(k)  # the slot's previous H2D copy must be done before we overwrite it
+        self.pf.wait(k)  # the host slot's previous H2D copy must be done before we overwrite it
         slot = self.pf.slot(k)
         slot[:xb].copy_(x.view(-1).view(torch.uint8))
         slot[yo:total].copy_(y.view(-1).view(torch.uint8))
         dev = self.dev_bufs[k]
-        self.pf.copy_to_device(k, dev, total)  # compute stream waits on this copy
+        self.pf.copy_to_device(k, dev, total)  # after the release of buffer k only
         xd = dev[:xb].view(x.dtype).view(x.shape)
         yd = dev[yo:total].view(y.dtype).view(y.shape)
-        return xd, yd
+        return k, xd, yd
 
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
-        # slot k is re-staged only after the batch that used it has been handed out; copy_to_device
-        # orders the new copy after all compute already queued (which includes that batch's use)
         it = iter(self.loader)
+        if self.pf is not None:  # a new pass (or one that was abandoned): everything queued so far
+            for i in range(self.depth):  # may still read the buffers
+                self.pf.release(i)
         pending = []
         k = 0
         for _ in range(self.depth - 1):
@@ -129,14 +134,23 @@ class NativePinnedPrefetcher:
                 k += 1
             except StopIteration:
                 break
+        last = None
         while pending:
-            out = pending.pop(0)
+            slot, xd, yd = pending.pop(0)
+            if last is not None:
+                # the consumer enqueued its work on the previous batch when it asked for this one
+                self.pf.release(last)
             try:
+                # buffer (k % depth) was last used by the batch just released: its copy follows that
                 pending.append(self._stage(k % self.depth, next(it)))
                 k += 1
             except StopIteration:
                 pass
-            yield out
+            self.pf.acquire(slot)  # the compute stream waits for this batch's copy here
+            last = slot
+            yield xd, yd
+        if last is not None:
+            self.pf.release(last)
 
 
 class DevicePrefetcher:

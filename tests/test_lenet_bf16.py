@@ -337,3 +337,34 @@ def test_bf16_fused_dp_loopback_fault_raises(dev):
         eng.train_steps(32, 2, use_graph=True, steps_per_graph=1)
     torch.cuda.synchronize()
     assert torch.equal(flat.data, before)
+
+
+def _quality_run(precision, model_dir, epochs=6, n_train=8192):
+    from ml_trainer_amd.data.cifar10 import SyntheticCIFAR10
+    from ml_trainer_amd.data.transforms import Compose, Normalize, RandomCrop, RandomHorizontalFlip, ToTensor
+    from ml_trainer_amd.trainer import Trainer
+    norm = Normalize((0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010))
+    tr = SyntheticCIFAR10(n_train, True, transform=Compose([RandomCrop(32, padding=4), RandomHorizontalFlip(),
+                                                             ToTensor(), norm]), seed=3, learnable="pattern")
+    va = SyntheticCIFAR10(2048, False, transform=Compose([ToTensor(), norm]), seed=3, learnable="pattern")
+    torch.manual_seed(5)
+    t = Trainer(MLModel(), datasets=(tr, va), epochs=epochs, batch_size=32, metric="accuracy", lr=1e-2,
+                model_dir=str(model_dir), options={"progress": False, "use_engine": True, "precision": precision})
+    t.fit()
+    return t.history
+
+
+@pytest.mark.gpu
+def test_bf16_training_quality_matches_fp32(tmp_path):
+    """Training quality of the bf16 headline step (BASELINE configs 2/3) against the reference
+    dtype over epochs (the reference's only quality evidence is its accuracy trajectory,
+    01_ML_Training_local.ipynb:309-409): Trainer.fit() for 6 epochs on a dataset whose accuracy
+    climbs gradually (class colour templates under heavy noise, RandomCrop + HFlip), fp32 vs bf16
+    engine, same init and data order. Final val accuracy within 1.5 points, per-epoch train loss
+    within 5 %."""
+    h = {p: _quality_run(p, tmp_path / p) for p in ("fp32", "bf16")}
+    a32, a16 = h["fp32"]["val_metric"], h["bf16"]["val_metric"]
+    assert a32[-1] > 0.5, a32  # it learned something non-trivial
+    assert abs(a32[-1] - a16[-1]) <= 0.015, (a32, a16)
+    for e, (l32, l16) in enumerate(zip(h["fp32"]["train_loss"], h["bf16"]["train_loss"])):
+        assert abs(l32 - l16) <= 0.05 * l32, (e, h["fp32"]["train_loss"], h["bf16"]["train_loss"])

@@ -320,8 +320,69 @@ def test_pinned_prefetcher(dev):
         pf.wait(i % 3)
         s.fill_(i + 1)
         pf.copy_to_device(i % 3, dst, 4096)
+        pf.acquire(i % 3)  # the compute stream waits for the copy where the batch is consumed
         torch.cuda.current_stream().synchronize()
         assert int(dst[0]) == i + 1 and int(dst[-1]) == i + 1
+        pf.release(i % 3)
+
+
+def test_pinned_prefetcher_overlaps_copy_and_compute(dev):
+    """A slow consumer on a 3-deep ring: the copy of batch k + 2 runs under batch k's kernels, so
+    the pipelined time per batch is ~max(copy, compute), not their sum (the copy waits only for
+    the release of ITS device buffer, the compute stream only for the batch it consumes)."""
+    import time
+    from ml_trainer_amd.ops._ext import require_native
+    C = require_native()
+    nbytes, d, n = 64 << 20, 3, 12
+    pf = C.PinnedPrefetcher(nbytes, d, dev.index or 0)
+    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(d)]
+    for i in range(d):
+        pf.slot(i).fill_(i + 1)
+    a = torch.randn(2048, 2048, device=dev)
+    sink = torch.zeros((), device=dev)
+
+    def compute(buf, reps):  # reads the batch, then keeps the compute stream busy
+        sink.add_(buf[:1 << 20].float().sum())
+        x = a
+        for _ in range(reps):
+            x = torch.mm(x, a).mul_(1e-3)
+        sink.add_(x[0, 0])
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    def copies():
+        for k in range(n):
+            pf.copy_to_device(k % d, bufs[k % d], nbytes)
+            pf.acquire(k % d)
+            pf.release(k % d)
+    timed(copies)
+    t_copy = timed(copies) / n
+    timed(lambda: compute(bufs[0], 4))
+    t_mm = timed(lambda: compute(bufs[0], 16)) / 16
+    reps = max(4, int(round(t_copy / t_mm)))
+    t_comp = timed(lambda: [compute(bufs[k % d], reps) for k in range(n)]) / n
+
+    def pipeline():
+        for k in range(d - 1):
+            pf.copy_to_device(k, bufs[k], nbytes)
+        for k in range(n):
+            j = k + d - 1
+            if j < n:
+                pf.wait(j % d)
+                pf.copy_to_device(j % d, bufs[j % d], nbytes)  # waits for release(k - 1) only
+            pf.acquire(k % d)
+            compute(bufs[k % d], reps)
+            pf.release(k % d)
+    timed(pipeline)
+    t_pipe = timed(pipeline) / n
+    ratio = t_pipe / max(t_copy, t_comp)
+    assert 0.4 < t_copy / t_comp < 2.5, (t_copy, t_comp)  # both sides matter
+    assert ratio < 1.15, (t_pipe, t_copy, t_comp)
 
 
 def test_device_prefetcher_uses_native_ring(dev):
