@@ -52,15 +52,61 @@ from ml_trainer_amd.utils.flat import FlatParams
 DEFAULT_BUCKET_MB = 32.0
 DEFAULT_FIRST_BUCKET_MB = 4.0
 
+# alpha-beta model of one bucket's ring all-reduce on an 8 x MI355X node (RCCL over xGMI):
+#   t(M) = ALPHA + 2 (W - 1) / W * M / BUS
+# ALPHA: per-collective launch + protocol latency; BUS: the all-reduce's bus bandwidth with RCCL's
+# rings spread over the 7 point-to-point links (~153 GB/s each). Both overridable from a measured
+# bucket sweep (scripts/bucket_sweep.sh): MLT_DDP_ALPHA_US, MLT_DDP_BUS_GBPS.
+XGMI_ALPHA_US = 25.0
+XGMI_BUS_GBPS = 300.0
+MIN_BUCKET_MB, MAX_BUCKET_MB = 4.0, 128.0
+
+
+def allreduce_us(nbytes: float, world: int, alpha_us: Optional[float] = None, bus_gbps: Optional[float] = None) -> float:
+    """Model time (us) of one ring all-reduce of ``nbytes`` over ``world`` ranks."""
+    import os
+    a = alpha_us if alpha_us is not None else float(os.environ.get("MLT_DDP_ALPHA_US", XGMI_ALPHA_US))
+    b = bus_gbps if bus_gbps is not None else float(os.environ.get("MLT_DDP_BUS_GBPS", XGMI_BUS_GBPS))
+    if world <= 1:
+        return 0.0
+    return a + 2.0 * (world - 1) / world * nbytes / (b * 1e3)  # GB/s = 1e3 bytes/us
+
+
+def plan_buckets(grad_bytes: int, world: int, bwd_ms: Optional[float] = None, largest_param_bytes: int = 0,
+                 alpha_us: Optional[float] = None, bus_gbps: Optional[float] = None):
+    """Bucket caps (cap_mb, first_mb) from the alpha-beta model. Buckets launched during backward
+    overlap it as long as the comm stream keeps up: n * ALPHA + beta * M <= T_bwd; what stays exposed
+    is the last bucket's all-reduce (ALPHA + beta * C_last). So the cap is the SMALLEST that keeps
+    the stream from falling behind -- C = M * ALPHA / (T_bwd - beta * M) -- clamped to
+    [4, 128] MB; a comm-bound step (beta * M >= T_bwd) gets the largest cap (fewest collectives).
+    The first bucket (the last layers' gradients, ready first) is small so that communication
+    starts early. Without a backward-time estimate: the defaults (32 / 4 MB)."""
+    if world <= 1 or bwd_ms is None or bwd_ms <= 0:
+        return DEFAULT_BUCKET_MB, DEFAULT_FIRST_BUCKET_MB
+    a = allreduce_us(0, world, alpha_us, bus_gbps)  # alpha alone
+    total_us = allreduce_us(grad_bytes, world, alpha_us, bus_gbps) - a  # beta * M
+    slack = bwd_ms * 1e3 - total_us
+    mb = 2 ** 20
+    if slack <= a:
+        cap = MAX_BUCKET_MB
+    else:
+        cap = grad_bytes * a / slack / mb
+    cap = min(MAX_BUCKET_MB, max(MIN_BUCKET_MB, cap))
+    first = min(cap, max(1.0, DEFAULT_FIRST_BUCKET_MB))
+    return cap, first
+
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_parameters: bool = True,
                  mode: str = "overlap", flat: Optional[FlatParams] = None,
-                 comm_dtype: Optional[torch.dtype] = None, timing: bool = False, comm=None):
+                 comm_dtype: Optional[torch.dtype] = None, timing: bool = False, comm=None,
+                 bwd_ms_hint: Optional[float] = None):
         """``comm``: None = native RCCL communicator when the group is RCCL with W > 1 (else
         torch.distributed); False = always torch.distributed; a ``_C.Communicator`` = use that
-        one (also at world size 1: the single-GPU rehearsal of the native collective path)."""
+        one (also at world size 1: the single-GPU rehearsal of the native collective path).
+        ``bwd_ms_hint``: expected backward time; with no explicit caps the buckets are then sized
+        by the alpha-beta model (:func:`plan_buckets`)."""
         super().__init__()
         if mode not in ("overlap", "manual"):
             raise ValueError("mode must be 'overlap' or 'manual'")
@@ -77,8 +123,12 @@ class DistributedDataParallel(nn.Module):
         elif comm is None and self.flat.device.type == "cuda" and self.world_size > 1:
             self._ncomm = self._native_comm_agreed(process_group)
         self.comm_backend = "native-rccl" if self._ncomm is not None else f"torch.distributed-{self.backend}"
-        self._bucket_cap = int((bucket_cap_mb or DEFAULT_BUCKET_MB) * 2 ** 20)
-        self._first_cap = int((first_bucket_mb or DEFAULT_FIRST_BUCKET_MB) * 2 ** 20)
+        esz = 2 if comm_dtype == torch.bfloat16 else self.flat.grad.element_size()
+        plan_cap, plan_first = plan_buckets(self.flat.numel * esz, self.world_size, bwd_ms_hint)
+        self.bucket_plan = {"cap_mb": bucket_cap_mb or plan_cap, "first_mb": first_bucket_mb or plan_first,
+                            "source": "explicit" if bucket_cap_mb else ("alpha-beta" if bwd_ms_hint else "default")}
+        self._bucket_cap = int(self.bucket_plan["cap_mb"] * 2 ** 20)
+        self._first_cap = int(self.bucket_plan["first_mb"] * 2 ** 20)
         self._build_buckets()
         if comm_dtype is not None and comm_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("comm_dtype must be torch.float32 or torch.bfloat16")
@@ -279,7 +329,7 @@ class DistributedDataParallel(nn.Module):
         ``exposed_ms`` comm time after backward compute ended (what the step waits for),
         ``overlap_pct`` share of the collective time hidden under forward/backward,
         ``fwd_bwd_ms`` forward start -> backward compute end, plus the bucket layout."""
-        out = {"comm": self.comm_backend, "buckets": len(self._buckets),
+        out = {"comm": self.comm_backend, "buckets": len(self._buckets), "bucket_plan": self.bucket_plan,
                "bucket_mb": [round(b / 2 ** 20, 3) for b in self.bucket_sizes_bytes],
                "comm_dtype": str(self.comm_dtype or self.flat.grad.dtype).replace("torch.", ""),
                "steps_timed": 0}

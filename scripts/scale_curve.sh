@@ -21,7 +21,8 @@ for prec in bf16 fp32; do
       if [ "$n" -gt "$ngpu" ]; then echo "=== skip N=$n ($ngpu GPUs visible)"; continue; fi
       echo "=== LeNet $prec, $scaling, N=$n"
       timeout -k 10 300 python3 -u bench.py --gpus "$n" --steps "$STEPS" --warmup "$WARMUP" --precision "$prec" \
-        --scaling "$scaling" --json-out gpurun_out/_scale_last.json > "gpurun_out/scale_${prec}_${scaling}_${n}.log" 2>&1
+        --scaling "$scaling" --no-fp32-companion \
+        --json-out gpurun_out/_scale_last.json > "gpurun_out/scale_${prec}_${scaling}_${n}.log" 2>&1
       rc=$?
       if [ "$rc" -ne 0 ]; then echo "=== stopping: rc=$rc (gpurun_out/scale_${prec}_${scaling}_${n}.log)"; exit "$rc"; fi
       python3 -c "import json,sys; d=json.load(open('gpurun_out/_scale_last.json')); d['mode']='$scaling'; print(json.dumps(d))" >> "$out"
@@ -30,6 +31,29 @@ for prec in bf16 fp32; do
   done
 done
 if [ "$ngpu" -ge 8 ]; then
+  # N = 8 transport A/B of the bf16 step under both batch semantics: the fused two-launch xGMI
+  # exchange (default), the four-launch step with the one-/two-shot vote (MLT_LENET_FUSED_DP=0),
+  # and RCCL forced (MLT_XGMI_AR=0)
+  for scaling in weak reference; do
+    for variant in fused fourlaunch rccl; do
+      case $variant in
+        fused) envs="";;
+        fourlaunch) envs="MLT_LENET_FUSED_DP=0";;
+        rccl) envs="MLT_XGMI_AR=0";;
+      esac
+      echo "=== LeNet bf16 $scaling N=8 transport=$variant"
+      env $envs timeout -k 10 300 python3 -u bench.py --gpus 8 --steps "$STEPS" --warmup "$WARMUP" --scaling "$scaling" \
+        --no-fp32-companion --json-out gpurun_out/_scale_last.json > "gpurun_out/scale_ab_${variant}_${scaling}.log" 2>&1 \
+        || { echo "=== stopping: transport A/B $variant failed"; exit 1; }
+      python3 -c "import json; d=json.load(open('gpurun_out/_scale_last.json')); d['mode']='$scaling'; d['transport_ab']='$variant'; print(json.dumps(d))" >> "$out"
+      tail -n 1 "$out"
+    done
+  done
+  # kernel trace of the 8-rank reference-semantics step (per-kernel time of every rank)
+  mkdir -p gpurun_out/prof_n8
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n8 -o n8 -- \
+    python3 -u bench.py --gpus 8 --steps 500 --warmup 50 --scaling reference --no-fp32-companion \
+    > gpurun_out/prof_n8/bench.log 2>&1 || echo "=== rocprofv3 N=8 trace failed (see gpurun_out/prof_n8/bench.log)"
   bash scripts/bucket_sweep.sh 8 10 && cat gpurun_out/bucket_sweep.jsonl >> "$out"
 fi
 echo "=== $(wc -l < "$out") records in $out"

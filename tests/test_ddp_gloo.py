@@ -235,3 +235,24 @@ def test_ddp_bucket_spanning_two_direct_write_blocks():
             ys.append(torch.randn(6, 4, generator=g))
         sum(((model(x) - y) ** 2).mean() for x, y in zip(xs, ys)).div(world).backward()
         torch.testing.assert_close(r[0], fp.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_bucket_plan_alpha_beta():
+    """The alpha-beta bucket planner: defaults without a backward-time estimate; a comm-bound step
+    gets the largest cap; a compute-bound one the smallest cap that keeps the comm stream up."""
+    from ml_trainer_amd.parallel.ddp import (DEFAULT_BUCKET_MB, MAX_BUCKET_MB, MIN_BUCKET_MB, allreduce_us,
+                                             plan_buckets)
+    mb = 2 ** 20
+    assert plan_buckets(440 * mb, 8) == (DEFAULT_BUCKET_MB, 4.0)
+    assert plan_buckets(440 * mb, 1, bwd_ms=100.0)[0] == DEFAULT_BUCKET_MB
+    # BERT-base fp32 grads on 8 ranks: beta*M ~ 2.6 ms << 130 ms of backward -> small buckets
+    cap, first = plan_buckets(440 * mb, 8, bwd_ms=130.0)
+    assert cap == MIN_BUCKET_MB and first <= cap
+    # comm-bound: backward shorter than the bandwidth term -> fewest collectives
+    assert plan_buckets(440 * mb, 8, bwd_ms=1.0)[0] == MAX_BUCKET_MB
+    # in between: C = M * alpha / (T - beta M), and the model's pieces add up
+    t = allreduce_us(440 * mb, 8, alpha_us=25.0, bus_gbps=300.0)
+    assert abs(t - (25.0 + 1.75 * 440 * mb / 300e3)) < 1e-6
+    cap, _ = plan_buckets(440 * mb, 8, bwd_ms=2.9, alpha_us=25.0, bus_gbps=300.0)
+    beta_m = t - 25.0
+    assert abs(cap - min(MAX_BUCKET_MB, max(MIN_BUCKET_MB, 440 * 25.0 / (2900.0 - beta_m)))) < 1e-9
