@@ -38,6 +38,10 @@ enum LeNetMode : int {
   LENET_K4WG = 4096,    // internal: K4 wrote the conv wgrad slabs, K5 only reduces them
   LENET_FROM_P1 = 8192, // internal: the per-sample kernel starts from p1 (conv2 -> fc chain) and stops there
   LENET_STATS_DEFER = 16384,  // internal: CE writes per-sample loss / hit to cestat; K4 sums them in sample order
+  // timing probes of the bf16 per-sample kernel (wrong numerics: profiling only; env MLT_LENET_PROBE)
+  LENET_PROBE_NOF1T = 1 << 17,  // role A skips the fc1 dgrad (transposed) weight fetch
+  LENET_PROBE_NOF1W = 1 << 18,  // role B skips the fc1 forward weight fetch
+  LENET_PROBE_NOF2 = 1 << 19,   // fc2 forward + dgrad weight fetches skipped
 };
 
 struct LeNetPtrs {

@@ -42,6 +42,7 @@
 //   conv1 wgrad M = (kw | c, kh) taps (+ ones row), N = out channel, K = the 28x32 positions of the
 //               unpooled conv1 gradient; split over 3 K-ranges, summed in a fixed order
 // All batch reductions (KW) run in sample order: results are bitwise reproducible run to run.
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
@@ -374,7 +375,12 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   // fc3: start of P3, where conv1's registers are free), so that their transfer does not delay
   // those. Padding lanes re-read a valid lane's line (coalesced).
   auto load_fc = [&]() {
-    if (w >= F1M::W1F) frag_rows<F1M::K1, FLAT, F1, FLAT>(f1w, P.shadow + O.off[4], w - F1M::W1F);
+    if (mode & LENET_PROBE_NOF1W) {
+#pragma unroll
+      for (int q = 0; q < F1M::K1; ++q) f1w[q] = u32x4{0u, 0u, 0u, 0u};
+    } else if (w >= F1M::W1F) {
+      frag_rows<F1M::K1, FLAT, F1, FLAT>(f1w, P.shadow + O.off[4], w - F1M::W1F);
+    }
   };
   __builtin_amdgcn_sched_barrier(0);  // keep the index math below behind the load issue
   int64_t pos = sie * A.batch_stride + b;
@@ -498,9 +504,21 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     // ---- role A: fc dgrad ----
     u32x4 f3t[F1M::B3K], f2t[F1M::B2K], f1t[F1M::B1P][F1M::B1K];  // first needed first (vmcnt order)
     if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, P.wimg + kFc3T, w);
-    if (w < F1M::B2T) frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
+    if (mode & LENET_PROBE_NOF2) {
 #pragma unroll
-    for (int j = 0; j < F1M::B1P; ++j) frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[j], P.wimg + kFc1T, w + 8 * j);
+      for (int q = 0; q < F1M::B2K; ++q) f2t[q] = u32x4{0u, 0u, 0u, 0u};
+    } else if (w < F1M::B2T) {
+      frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
+    }
+    if (mode & LENET_PROBE_NOF1T) {
+#pragma unroll
+      for (int j = 0; j < F1M::B1P; ++j)
+#pragma unroll
+        for (int q = 0; q < F1M::B1K; ++q) f1t[j][q] = u32x4{0u, 0u, 0u, 0u};
+    } else {
+#pragma unroll
+      for (int j = 0; j < F1M::B1P; ++j) frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[j], P.wimg + kFc1T, w + 8 * j);
+    }
     lbar();  // P3 (conv2)
     stamp(3);
     lbar();  // P4a (fc1 forward)
@@ -543,8 +561,12 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   } else {
     // ---- role B: conv2, forward fc chain, softmax-CE, next-step staging ----
     u32x4 f2w[F1M::K2], f3w[F1M::K3], f1tx[F1M::B1K];
-    if (w >= F1M::W2F && w < F1M::W2F + F1M::T2)
+    if (mode & LENET_PROBE_NOF2) {
+#pragma unroll
+      for (int q = 0; q < F1M::K2; ++q) f2w[q] = u32x4{0u, 0u, 0u, 0u};
+    } else if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {
       frag_rows<F1M::K2, F1, F2, F1>(f2w, P.shadow + O.off[6], w - F1M::W2F);
+    }
     // next-step staging (wave 15, two steps deep so that no load waits on another inside this
     // kernel): metaN[b] = (step, position, perm entry) looked up by the PREVIOUS step for step + 1;
     // when it matches, the raw image of step + 1 is gathered now (stored to stage2 at the end of
@@ -1323,8 +1345,18 @@ void pack(const LeNetPtrs& P, const LeNetOpt& O, hipStream_t st) {
                      O.off[0], O.off[2], O.off[4], O.off[6], O.off[8]);
 }
 
+// MLT_LENET_PROBE: timing-probe mode bits OR-ed into the per-sample kernel's mode (profiling only)
+static int probe_bits() {
+  static const int v = [] {
+    const char* e = std::getenv("MLT_LENET_PROBE");
+    return e ? std::atoi(e) & (LENET_PROBE_NOF1T | LENET_PROBE_NOF1W | LENET_PROBE_NOF2) : 0;
+  }();
+  return v;
+}
+
 template <class D>
 void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
+  mode |= probe_bits();
   const float inv_B = 1.f / (float)B;
   hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
   const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
@@ -1337,6 +1369,7 @@ void run_dp(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetO
   const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
   if (X.G < nblk) throw std::runtime_error("lenet dp step: transport flag rows < reduction blocks");
   if (X.cap < O.n) throw std::runtime_error("lenet dp step: transport region smaller than the parameters");
+  mode |= probe_bits();
   const float inv_B = 1.f / (float)B;
   hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
   const int m = mode | LENET_OPT;
