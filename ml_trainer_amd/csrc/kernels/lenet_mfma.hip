@@ -193,6 +193,26 @@ __device__ __forceinline__ float row_dot(const u32x4 (&f)[KS], const uint16_t* x
   return acc[0];
 }
 
+// fc1 dgrad B fragment of k-step q for output tile `tile` from the LDS fc1 image (KsLds::F1S layout):
+// lane (g, i = 4 qq + p) needs W1[32 q + 8 g + j][16 tile + i], j = 0..7 -- a column of the
+// row-major image. Two ds_read_b64_tr_b16 (rows 32q + 8g + qq and + 4, columns 16 tile + 4p .. + 3
+// supplied per lane) deliver it transposed. Rows past F1 re-read row F1 - 1 (their A column, the
+// fc1 output gradient, is zero there); columns past FLAT re-read the last four (outputs not stored).
+// Every lane must execute the reads (EXEC all ones: the gather crosses lanes).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+template <int F1, int FLAT, int F1S>
+__device__ __forceinline__ u32x4 f1t_frag(const uint16_t* img, int tile, int q) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+  const int col = min(16 * tile + 4 * p, FLAT - 4), c = col >> 3, e = col & 7;
+  const int r0 = min(32 * q + 8 * g + qq, F1 - 1), r1 = min(32 * q + 8 * g + qq + 4, F1 - 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (r0 * F1S + c + (r0 & 1)) * 8 + e));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (r1 * F1S + c + (r1 & 1)) * 8 + e));
+  return u32x4{(unsigned)(uint16_t)lo[0] | ((unsigned)(uint16_t)lo[1] << 16),
+               (unsigned)(uint16_t)lo[2] | ((unsigned)(uint16_t)lo[3] << 16),
+               (unsigned)(uint16_t)hi[0] | ((unsigned)(uint16_t)hi[1] << 16),
+               (unsigned)(uint16_t)hi[2] | ((unsigned)(uint16_t)hi[3] << 16)};
+}
 
 // The fc chain's wave schedule. Fragments (~150 KB per CU and step) are fetched where the issuing
 // waves are otherwise idle or light -- the vector memory path of a CU moves them at ~35 B/clk and a
@@ -222,19 +242,19 @@ template <class D>
 struct KsLds {
   using F = Fc<D>;
   static constexpr int SCR = kP13W * 5 * 256;
+  // fc1 weight image [F1 rows][F1S 16-byte chunks]: row r holds W1[r][0 .. FLAT) (8 bf16 per chunk)
+  // at chunks (r & 1) .. (r & 1) + FLAT/8 - 1 -- the one-chunk shift of odd rows makes the transposed
+  // reads of the fc1 dgrad (ds_read_b64_tr_b16: 8 rows x 32 bytes per 32-lane half) conflict-free
+  static constexpr int F1S = D::FLAT / 8 + 1;
   // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
-  // MFMA fragment reads
+  // MFMA fragment reads before P10
   alignas(16) uint16_t p1h[14 * P1HS * 8];           // pooled conv1 [y][x][ic8]
   alignas(16) uint16_t p1c[D::C1 * 14 * P1CS];       // pooled conv1 [ic][y][x]
-  alignas(16) uint16_t dch[18 * DCHS * 16];          // unpooled conv2-out grad, padded [Y+4][X+4][oc16]
-  alignas(16) uint16_t dcc[16 * 10 * DCCS];          // unpooled conv2-out grad [oc16][Y][X]
-  alignas(16) uint16_t d1[D::C1 * D1S];              // unpooled conv1-out grad [oc][Y][X32]
   // end of the zero span
   alignas(16) uint16_t xh[32 * XHS * 4];             // input [Y][X][c4] (c = 3 zero; X >= 32 never read)
   alignas(16) uint16_t xc[3 * 32 * XCS];             // input [c][Y][X48] (X >= 32 zeroed separately)
   alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
   alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
-  alignas(16) uint16_t w2d[15 * 64 * 8];             // conv2 dgrad B fragments
   // bf16 A rows of the fc MFMAs (tails zero to the k-step multiple)
   alignas(16) uint16_t fb16[32 * F::K1];             // flattened pooled conv2 (fc1)
   alignas(16) uint16_t h1b[32 * F::K2];              // fc1 output (fc2)
@@ -249,7 +269,6 @@ struct KsLds {
   alignas(16) float sdh2[D::F2];
   alignas(16) float slog[64];
   alignas(16) float sdl[64];
-  alignas(16) float scr[SCR];                        // conv1 wgrad row-range partials
   alignas(16) float f32[D::FLAT];                    // flattened pooled conv2, fp32 (stored for the fc1 wgrad)
   unsigned long long tr[32];                         // LENET_TRACE stamps
   double ce[2];                                      // this sample's (loss / B, hit / B)
@@ -258,6 +277,18 @@ struct KsLds {
   alignas(16) float fb[D::F1 + D::F2 + D::NC];       // fc biases
   uint8_t i1[D::C1 * 196];
   uint8_t i2[D::FLAT];
+  // P4a .. P8 the fc1 weight image (written from the fc1 forward's register fragments, read
+  // transposed by the fc1 dgrad); P10 .. P13 the backward images, written (and zeroed) in P10
+  union U {
+    alignas(16) uint16_t f1img[D::F1 * F1S * 8];
+    struct Bw {
+      alignas(16) uint16_t dch[18 * DCHS * 16];      // unpooled conv2-out grad, padded [Y+4][X+4][oc16]
+      alignas(16) uint16_t dcc[16 * 10 * DCCS];      // unpooled conv2-out grad [oc16][Y][X]
+      alignas(16) uint16_t d1[D::C1 * D1S];          // unpooled conv1-out grad [oc][Y][X32]
+      alignas(16) uint16_t w2d[15 * 64 * 8];         // conv2 dgrad B fragments
+      alignas(16) float scr[SCR];                    // conv1 wgrad row-range partials
+    } b;
+  } u;
 };
 
 // RandomCrop(32, pad) + HFlip + ToTensor + Normalize of pixel (Y, X) from a raw HWC uint8 image
@@ -310,8 +341,8 @@ template <class D>
 __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A, LeNetOpt O, float inv_B) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC;
   using S = KsLds<D>;
-  static_assert(offsetof(S, w2f) == offsetof(S, w1f) + 2 * kW2F && offsetof(S, w2d) == offsetof(S, w1f) + 2 * kW2D,
-                "fragment images must be contiguous");
+  static_assert(offsetof(S, w2f) == offsetof(S, w1f) + 2 * kW2F, "forward fragment images must be contiguous");
+  static_assert(sizeof(S) <= 160 * 1024, "LDS");
   __shared__ S L;
   // w is wave-uniform: readfirstlane makes the per-wave role branches scalar (uniform) branches,
   // so a role's pending loads never force waits on the other roles' code paths
@@ -496,13 +527,15 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 
   const uint4 wid = wimg4[WIF + min(t, WID - 1)];  // conv2 dgrad fragments (to LDS in P10)
 
-  // ---- P3-P8 as two wave roles (the same barrier sequence in both) ------------------------------
-  // waves 0-7 fetch the fc dgrad fragments during conv2 and run the dgrad chain; waves 8-15 run
-  // conv2, the forward fc chain and the softmax-CE and do the next-step staging (wave 15). As two
-  // branches, each role's register-resident fragments share registers with the other's.
+  // ---- P3-P7 as two wave roles (the same barrier sequence in both), then P8 on every wave ---------
+  // waves 0-7 fetch the fc3 / fc2 dgrad fragments during conv2 and run that dgrad chain; waves 8-15
+  // run conv2, the forward fc chain and the softmax-CE, put their fc1 forward fragments into the
+  // LDS fc1 image (read back transposed by the fc1 dgrad: the transposed copy of fc1, ~96 KB per CU
+  // and step, is no longer fetched) and do the next-step staging (wave 15). As two branches, each
+  // role's register-resident fragments share registers with the other's.
   if (w < 8) {
-    // ---- role A: fc dgrad ----
-    u32x4 f3t[F1M::B3K], f2t[F1M::B2K], f1t[F1M::B1P][F1M::B1K];  // first needed first (vmcnt order)
+    // ---- role A: fc3 / fc2 dgrad ----
+    u32x4 f3t[F1M::B3K], f2t[F1M::B2K];  // first needed first (vmcnt order)
     if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, P.wimg + kFc3T, w);
     if (mode & LENET_PROBE_NOF2) {
 #pragma unroll
@@ -510,22 +543,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     } else if (w < F1M::B2T) {
       frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
     }
-    if (mode & LENET_PROBE_NOF1T) {
-#pragma unroll
-      for (int j = 0; j < F1M::B1P; ++j)
-#pragma unroll
-        for (int q = 0; q < F1M::B1K; ++q) f1t[j][q] = u32x4{0u, 0u, 0u, 0u};
-    } else {
-#pragma unroll
-      for (int j = 0; j < F1M::B1P; ++j) frag_rows<F1M::B1K, F1, FLAT, F1>(f1t[j], P.wimg + kFc1T, w + 8 * j);
-    }
     lbar();  // P3 (conv2)
     stamp(3);
     lbar();  // P4a (fc1 forward)
     stamp(18);
     lbar();  // P4b (fc2 forward)
     stamp(19);
-    lbar();  // P4c (fc3 forward + CE)
+    lbar();  // P4c (fc3 forward + CE; role B fills the fc1 image)
     stamp(4);
     if (w < F1M::B3T) {  // fc3 dgrad (x the fc2 ReLU mask)
       const int k = 16 * w + m;
@@ -549,18 +573,9 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     }
     lbar();
     stamp(21);
-    stamp(22);
-#pragma unroll
-    for (int j = 0; j < F1M::B1P; ++j) {  // fc1 dgrad -> the flattened pooled-conv2 gradient
-      const int c = 16 * (w + 8 * j) + m;
-      const float v = row_dot(f1t[j], L.dh1b);
-      if (g == 0 && c < FLAT) L.df[c] = v;
-    }
-    lbar();
-    stamp(5);
   } else {
-    // ---- role B: conv2, forward fc chain, softmax-CE, next-step staging ----
-    u32x4 f2w[F1M::K2], f3w[F1M::K3], f1tx[F1M::B1K];
+    // ---- role B: conv2, forward fc chain, softmax-CE, fc1 image, next-step staging ----
+    u32x4 f2w[F1M::K2], f3w[F1M::K3];
     if (mode & LENET_PROBE_NOF2) {
 #pragma unroll
       for (int q = 0; q < F1M::K2; ++q) f2w[q] = u32x4{0u, 0u, 0u, 0u};
@@ -636,8 +651,18 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     }
     lbar();
     stamp(18);
-    if (w == 15 && F1M::B1T > 8 * F1M::B1P)  // the 25th fc1 dgrad tile (wave 15 idles in fc2 / fc3)
-      frag_rows<F1M::B1K, F1, FLAT, F1>(f1tx, P.wimg + kFc1T, 8 * F1M::B1P);
+    // the fc1 forward fragments (W1 rows, 16 B per lane) -> the LDS fc1 image; clamped duplicates
+    // (rows past F1, chunks past FLAT / 8) are skipped. In phases where the writing wave is idle:
+    // P4c for all of them but the fc3 / CE wave, which writes in P5.
+    auto put_f1img = [&]() {
+      const int row = 16 * (w - F1M::W1F) + m;
+      if (row < F1) {
+        uint16_t* dst = L.u.f1img + (row * S::F1S + (row & 1)) * 8;
+#pragma unroll
+        for (int q = 0; q < F1M::K1; ++q)
+          if (4 * q + g < FLAT / 8) *reinterpret_cast<u32x4*>(dst + (4 * q + g) * 8) = f1w[q];
+      }
+    };
     if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, P.wimg + kFc3F, 0);
     if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // P4b: fc2 forward
       const int r = 16 * (w - F1M::W2F) + m;
@@ -673,19 +698,14 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         L.ce[0] = (double)loss * (double)inv_B;
         L.ce[1] = (am == tgt) ? (double)inv_B : 0.0;
       }
+    } else if (w >= F1M::W1F) {
+      put_f1img();
     }
     lbar();
     stamp(4);
+    if (w == F1M::W3F) put_f1img();
     lbar();  // P5 (fc3 dgrad)
     stamp(20);
-    lbar();  // P6 (fc2 dgrad)
-    stamp(21);
-    stamp(22);
-    if (w == 15 && F1M::B1T > 8 * F1M::B1P) {  // P8: the 25th fc1 dgrad tile
-      const int c = 16 * (8 * F1M::B1P) + m;
-      const float v = row_dot(f1tx, L.dh1b);
-      if (g == 0 && c < FLAT) L.df[c] = v;
-    }
     if (stage_on) {  // wave 15: publish the next step's raw image + tags
       if (st1) {
         uint4* dst = reinterpret_cast<uint4*>(P.stage2 + (int64_t)b * 3072);
@@ -705,21 +725,67 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         P.metaN[4 * b + 2] = nperm2v;
       }
     }
-    lbar();
-    stamp(5);
+    lbar();  // P6 (fc2 dgrad)
+    stamp(21);
   }
 
-  // ---- P10: unpool2 -> the conv2-output gradient images (zero except at arg-max cells) ---------
-  if (t < WID) reinterpret_cast<uint4*>(L.w2d)[t] = wid;
-  for (int e = t; e < FLAT; e += kT) {
-    const int code = L.i2[e];
-    if (code < 4) {
-      const int oc = e / 25, cell = e - 25 * oc, py = cell / 5, pxx = cell - 5 * py;
-      const int Y = 2 * py + (code >> 1), X = 2 * pxx + (code & 1);
-      const uint16_t v = f32_to_bf16(L.df[e]);
-      L.dch[((Y + 4) * DCHS + X + 4) * 16 + oc] = v;
-      L.dcc[(oc * 10 + Y) * DCCS + X] = v;
+  // ---- P8: fc1 dgrad on every wave (tiles w, w + 16) from the LDS fc1 image, read transposed ----
+  stamp(22);
+  {
+    u32x4 ah[F1M::B1K];  // the fc1 output gradient (bf16, zero past F1), broadcast over the A rows
+#pragma unroll
+    for (int q = 0; q < F1M::B1K; ++q) ah[q] = *reinterpret_cast<const u32x4*>(L.dh1b + 32 * q + 8 * g);
+#pragma unroll
+    for (int j = 0; j < (F1M::B1T + 15) / 16; ++j) {
+      const int tile = w + 16 * j;
+      if (tile < F1M::B1T) {  // wave-uniform: every lane runs the transposed reads
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < F1M::B1K; ++q) acc = mfma(ah[q], f1t_frag<F1, FLAT, S::F1S>(L.u.f1img, tile, q), acc);
+        const int c = 16 * tile + m;
+        if (g == 0 && c < FLAT) L.df[c] = acc[0];
+      }
     }
+  }
+  lbar();
+  stamp(5);
+
+  // ---- P10: the backward images (the fc1 image is dead): conv2 dgrad fragments; unpool2 -> the
+  //           conv2-output gradient images, all four cells of a pool window written (the value at
+  //           the arg max, 0 elsewhere; channels past C2 zero); the zero border of the padded image,
+  //           the unread pad columns and the whole conv1-gradient image d1 (written sparsely in P11)
+  //           zeroed -- every store to a distinct address, so no barrier inside the phase
+  if (t < WID) reinterpret_cast<uint4*>(L.u.b.w2d)[t] = wid;
+  if (t < 16 * 25) {
+    const int oc = t / 25, cell = t - 25 * oc, py = cell / 5, pxx = cell - 5 * py;
+    const int code = oc < C2 ? (int)L.i2[t] : 4;
+    const uint16_t v = code < 4 ? f32_to_bf16(L.df[t]) : (uint16_t)0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int Y = 2 * py + (k >> 1), X = 2 * pxx + (k & 1);
+      const uint16_t o = k == code ? v : (uint16_t)0;
+      L.u.b.dch[((Y + 4) * DCHS + X + 4) * 16 + oc] = o;
+      L.u.b.dcc[(oc * 10 + Y) * DCCS + X] = o;
+    }
+  } else {
+    // border of dch: the 18 x DCHS pixels outside [4, 14) x [4, 14), 16 channels = 2 uint4 each
+    constexpr int NPIX = 18 * DCHS;
+    for (int e = t - 16 * 25; e < 2 * NPIX; e += kT - 16 * 25) {
+      const int pix = e >> 1, Y = pix / DCHS, X = pix - DCHS * Y;
+      if (Y < 4 || Y >= 14 || X < 4 || X >= 14)
+        reinterpret_cast<uint4*>(L.u.b.dch)[2 * pix + (e & 1)] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  {
+    // dcc columns 10 .. DCCS - 1 of its 160 rows (read up to column 15 by the conv2 wgrad)
+    static_assert(DCCS == 24, "dcc pad layout");
+    for (int e = t; e < 160 * 7; e += kT) {  // 7 u32 = columns 10 .. 23
+      const int r = e / 7, k = e - 7 * r;
+      reinterpret_cast<unsigned*>(L.u.b.dcc + r * DCCS + 10)[k] = 0u;
+    }
+    constexpr int D1Q = D::C1 * D1S * 2 / 16;
+    static_assert((D::C1 * D1S * 2) % 16 == 0, "d1 zero fill");
+    for (int e = t; e < D1Q; e += kT) reinterpret_cast<uint4*>(L.u.b.d1)[e] = make_uint4(0u, 0u, 0u, 0u);
   }
   lbar();
   stamp(6);
@@ -735,9 +801,9 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
     for (int s = 0; s < 15; ++s) {
       const int pp = 2 * s + (g >> 1), oc0 = 8 * (g & 1), kh = pp / 6, u = pp - 6 * kh;
-      u32x4 a = *reinterpret_cast<const u32x4*>(L.dch + ((pp < 30 ? (Y - kh + 4) * DCHS + 2 * xp + 5 - u : 0)) * 16 + oc0);
+      u32x4 a = *reinterpret_cast<const u32x4*>(L.u.b.dch + ((pp < 30 ? (Y - kh + 4) * DCHS + 2 * xp + 5 - u : 0)) * 16 + oc0);
       if (pp >= 30) a = u32x4{0u, 0u, 0u, 0u};
-      acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2d + (s * 64 + lane) * 8), acc);
+      acc = mfma(a, *reinterpret_cast<const u32x4*>(L.u.b.w2d + (s * 64 + lane) * 8), acc);
     }
     const int ic = m >> 1, dx = m & 1;
 #pragma unroll
@@ -748,7 +814,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
         const int code = L.i1[ic * 196 + pc];
         if (code < 4) {
           const int py = pc / 14, pxx = pc - 14 * py;
-          L.d1[ic * D1S + (2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(acc[r]);
+          L.u.b.d1[ic * D1S + (2 * py + (code >> 1)) * 32 + 2 * pxx + (code & 1)] = f32_to_bf16(acc[r]);
         }
       }
     }
@@ -769,7 +835,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
         for (int s = 0; s < 5; ++s) {
           const int y = 2 * s + (g >> 1), x0 = 8 * (g & 1);
-          const u32x4 bq = *reinterpret_cast<const u32x4*>(L.dcc + (m * 10 + y) * DCCS + x0);
+          const u32x4 bq = *reinterpret_cast<const u32x4*>(L.u.b.dcc + (m * 10 + y) * DCCS + x0);
           const uint16_t* rowp = L.p1c + ((valid ? ic : 0) * 14 + y + (valid ? kh : 0)) * P1CS + x0;
           const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp), hi = *reinterpret_cast<const u32x4*>(rowp + 8);
           u32x4 a = fshift<kw>(lo, hi);
@@ -805,7 +871,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     const bool valid = m < 15;
     const int x0 = 8 * g;
     const uint16_t* xrow = L.xc + ((valid ? c : 0) * 32 + (valid ? kh : 0)) * XCS + x0;
-    const uint16_t* drow = L.d1 + min(m, C1 - 1) * D1S + x0;
+    const uint16_t* drow = L.u.b.d1 + min(m, C1 - 1) * D1S + x0;
     constexpr u32x4 ONES = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bias row (m = 15, kw = 0)
     const u32x4 Z = {0u, 0u, 0u, 0u};
     f32x4 acc[5];
@@ -826,15 +892,15 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) L.scr[((w * 5 + kw) * 16 + 4 * g + r) * 16 + m] = acc[kw][r];
+      for (int r = 0; r < 4; ++r) L.u.b.scr[((w * 5 + kw) * 16 + 4 * g + r) * 16 + m] = acc[kw][r];
   }
   lbar();
   stamp(23);
   for (int e = t; e < 5 * 256; e += kT) {
     const int kw = e >> 8, i = (e >> 4) & 15, oc = e & 15;
-    float v = L.scr[e];
+    float v = L.u.b.scr[e];
 #pragma unroll
-    for (int p = 1; p < kP13W; ++p) v += L.scr[p * 1280 + e];
+    for (int p = 1; p < kP13W; ++p) v += L.u.b.scr[p * 1280 + e];
     if (oc < C1) {
       if (i < 15) slab[oc * 76 + (i / 5) * 25 + (i % 5) * 5 + kw] = v;
       else if (kw == 0) slab[oc * 76 + 75] = v;
@@ -1187,8 +1253,8 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
     int wv = blk * (kWgT / 64) + (t >> 6);
     wv = __builtin_amdgcn_readfirstlane(wv);
     if (wv < NW3) {
-      fc_wgrad<FLAT, F1>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], P.wimg ? P.wimg + kFc1T : nullptr,
-                         F1);
+      // (no transposed fc1 image: the per-sample kernel transposes fc1 in LDS)
+      fc_wgrad<FLAT, F1>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], nullptr, F1);
     } else if ((wv -= NW3) < NW4) {
       fc_wgrad<F1, F2>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
                        Fc<D>::P2T);
