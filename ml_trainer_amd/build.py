@@ -92,8 +92,11 @@ def _run(cmd):
 # lenet_mfma.hip: the max-memory-clause machine scheduler (loads grouped into clauses issued ahead
 # of their uses) measured 1-2 % faster on the latency-chain per-sample step than the default,
 # max-ilp and iterative-ilp strategies (profiles/ab_lenet_sched_r3.jsonl).
+# lenet_mfma.hip also preloads the leading scalar kernel arguments into SGPRs (the per-sample
+# kernel's first-load pointers: no s_load round trip of the kernarg segment before its first loads).
 FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
-              "lenet_mfma.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+              "lenet_mfma.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
+                                 "-mllvm", "-amdgpu-kernarg-preload-count=12"]}
 
 
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:

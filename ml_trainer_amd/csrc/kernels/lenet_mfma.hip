@@ -338,7 +338,13 @@ __device__ __forceinline__ void pool4(f32x4 a, float bias, float& pv, uint8_t& c
 // KS: the per-sample chain
 // ---------------------------------------------------------------------------
 template <class D>
-__global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A, LeNetOpt O, float inv_B) {
+// The pointers the first loads need lead the argument list as plain scalars: the file is built with
+// kernarg preloading (build.py), so they arrive in SGPRs with the wave instead of behind an s_load
+// of the kernarg segment (aggregates are never preloaded).
+__global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, int64_t* __restrict__ pmeta2,
+                                               const int64_t* __restrict__ pctrl, const uint16_t* __restrict__ pwimg,
+                                               int64_t* __restrict__ pmetaN, int mode, float inv_B, LeNetPtrs P,
+                                               LeNetAug A, LeNetOpt O) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC;
   using S = KsLds<D>;
   static_assert(offsetof(S, w2f) == offsetof(S, w1f) + 2 * kW2F, "forward fragment images must be contiguous");
@@ -373,17 +379,17 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   // straight-line and unconditional (ctrl / meta2 / stage2 are host-checked), ctrl first: the
   // only values needed before the others arrive (vmcnt retires in issue order)
   const bool aug = A.data != nullptr;
-  const int64_t step = sload(A.ctrl), sie = sload(A.ctrl + 1);
-  const int64_t mstep = sload(P.meta2 + 4 * b), mpos = sload(P.meta2 + 4 * b + 1), mtgt = sload(P.meta2 + 4 * b + 3);
-  uint4 sraw = reinterpret_cast<const uint4*>(P.stage2 + (int64_t)b * 3072)[min(t, 191)];
+  const int64_t step = sload(pctrl), sie = sload(pctrl + 1);
+  const int64_t mstep = sload(pmeta2 + 4 * b), mpos = sload(pmeta2 + 4 * b + 1), mtgt = sload(pmeta2 + 4 * b + 3);
+  uint4 sraw = reinterpret_cast<const uint4*>(pstage2 + (int64_t)b * 3072)[min(t, 191)];
   const bool stage_on = aug && w == 15;  // next-step staging wave (see P2)
   // (vector loads, issued before the bulk: scalar ones would be waited for by every LDS barrier's
   // lgkmcnt(0), and the staging decision they feed is taken in P2, off the critical path)
   longlong2 mN01 = make_longlong2(-1, -1);
   long long mN2 = -1;
   if (stage_on) {
-    mN01 = *reinterpret_cast<const longlong2*>(P.metaN + 4 * b);
-    mN2 = P.metaN[4 * b + 2];
+    mN01 = *reinterpret_cast<const longlong2*>(pmetaN + 4 * b);
+    mN2 = pmetaN[4 * b + 2];
   }
   float xin[3] = {0.f, 0.f, 0.f};
   if (!aug) {
@@ -392,7 +398,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   }
   // conv weight B-fragment images (bf16, packed by the optimizer / lenet_mpack): 24 KB, linear
   // (the forward fragments only: conv2's dgrad fragments follow in P3, off the critical path)
-  const uint4* wimg4 = reinterpret_cast<const uint4*>(P.wimg);
+  const uint4* wimg4 = reinterpret_cast<const uint4*>(pwimg);
   constexpr int WIF = kW2D / 8, WID = (kWimg - kW2D) / 8;  // uint4s: forward part, dgrad part
   static_assert(WIF <= kT && WID <= kT, "fragment image staging");
   const uint4 wi0 = wimg4[min(t, WIF - 1)];
@@ -536,12 +542,12 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
   if (w < 8) {
     // ---- role A: fc3 / fc2 dgrad ----
     u32x4 f3t[F1M::B3K], f2t[F1M::B2K];  // first needed first (vmcnt order)
-    if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, P.wimg + kFc3T, w);
+    if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, pwimg + kFc3T, w);
     if (mode & LENET_PROBE_NOF2) {
 #pragma unroll
       for (int q = 0; q < F1M::B2K; ++q) f2t[q] = u32x4{0u, 0u, 0u, 0u};
     } else if (w < F1M::B2T) {
-      frag_rows<F1M::B2K, P2T, F1, F2>(f2t, P.wimg + kFc2T, w);
+      frag_rows<F1M::B2K, P2T, F1, F2>(f2t, pwimg + kFc2T, w);
     }
     lbar();  // P3 (conv2)
     stamp(3);
@@ -663,7 +669,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
           if (4 * q + g < FLAT / 8) *reinterpret_cast<u32x4*>(dst + (4 * q + g) * 8) = f1w[q];
       }
     };
-    if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, P.wimg + kFc3F, 0);
+    if (w == F1M::W3F) frag_rows<F1M::K3, P3F, NC, F2>(f3w, pwimg + kFc3F, 0);
     if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // P4b: fc2 forward
       const int r = 16 * (w - F1M::W2F) + m;
       const float v = row_dot(f2w, L.h1b);
@@ -708,21 +714,21 @@ __global__ __launch_bounds__(kT) void lenet_ms(int mode, LeNetPtrs P, LeNetAug A
     stamp(20);
     if (stage_on) {  // wave 15: publish the next step's raw image + tags
       if (st1) {
-        uint4* dst = reinterpret_cast<uint4*>(P.stage2 + (int64_t)b * 3072);
+        uint4* dst = reinterpret_cast<uint4*>(pstage2 + (int64_t)b * 3072);
         dst[lane] = nraw0;
         dst[lane + 64] = nraw1;
         dst[lane + 128] = nraw2;
       }
       if (lane == 0) {
         if (st1) {
-          P.meta2[4 * b] = step + 1;
-          P.meta2[4 * b + 1] = pos1;
-          P.meta2[4 * b + 2] = idx1;
-          P.meta2[4 * b + 3] = ntgtv;
+          pmeta2[4 * b] = step + 1;
+          pmeta2[4 * b + 1] = pos1;
+          pmeta2[4 * b + 2] = idx1;
+          pmeta2[4 * b + 3] = ntgtv;
         }
-        P.metaN[4 * b] = step + 2;
-        P.metaN[4 * b + 1] = pos2;
-        P.metaN[4 * b + 2] = nperm2v;
+        pmetaN[4 * b] = step + 2;
+        pmetaN[4 * b + 1] = pos2;
+        pmetaN[4 * b + 2] = nperm2v;
       }
     }
     lbar();  // P6 (fc2 dgrad)
@@ -1294,11 +1300,24 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
   }
 }
 
+// (the per-block first loads' pointers lead the arguments: preloaded into SGPRs, see lenet_ms)
+__device__ __forceinline__ LeNetPtrs with_first(LeNetPtrs P, const float* slab1, const float* p2, const float* dh1,
+                                                const float* h1, const float* dh2) {
+  P.slab1 = const_cast<float*>(slab1);
+  P.p2 = const_cast<float*>(p2);
+  P.dh1 = const_cast<float*>(dh1);
+  P.h1 = const_cast<float*>(h1);
+  P.dh2 = const_cast<float*>(dh2);
+  return P;
+}
 template <class D>
-__global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl) {
+__global__ __launch_bounds__(kWgT) void lenet_mw(const float* __restrict__ pslab1, const float* __restrict__ pp2,
+                                                 const float* __restrict__ pdh1, const float* __restrict__ ph1,
+                                                 const float* __restrict__ pdh2, int mode, int B, LeNetPtrs P,
+                                                 LeNetOpt O, int64_t* __restrict__ ctrl) {
   unsigned long long t0 = 0;
   if (mode & LENET_TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-  mw_body<D, 0>(mode, P, O, B, ctrl, Xch<0>{});
+  mw_body<D, 0>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, Xch<0>{});
   // LENET_TRACE: 100 MHz wall clock per block (start) and per wave (end): P.trace slots 64 + 5 blk (+1 + wave)
   if ((mode & LENET_TRACE) && P.trace && blockIdx.x < 100) {
     unsigned long long* tr = reinterpret_cast<unsigned long long*>(P.trace) + 64 + 5 * blockIdx.x;
@@ -1310,8 +1329,10 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(int mode, LeNetPtrs P, LeNetOpt
 // the data-parallel batch-reduction kernel: lenet_mw + the xGMI exchange of every block's slice
 // (struct Xch) + the update, in one launch (WT = rank count; 1 = loopback)
 template <class D, int WT>
-__global__ __launch_bounds__(kWgT) void lenet_mwx(int mode, LeNetPtrs P, LeNetOpt O, int B, int64_t* __restrict__ ctrl,
-                                                  XgmiFused X) {
+__global__ __launch_bounds__(kWgT) void lenet_mwx(const float* __restrict__ pslab1, const float* __restrict__ pp2,
+                                                  const float* __restrict__ pdh1, const float* __restrict__ ph1,
+                                                  const float* __restrict__ pdh2, int mode, int B, LeNetPtrs P,
+                                                  LeNetOpt O, int64_t* __restrict__ ctrl, XgmiFused X) {
   __shared__ int failed;
   Xch<WT> xc;
   xc.X = &X;
@@ -1326,7 +1347,7 @@ __global__ __launch_bounds__(kWgT) void lenet_mwx(int mode, LeNetPtrs P, LeNetOp
   xc.seq = X.seqs[blockIdx.x] + 1;  // per-block launch counter: identical on every block and rank
   xc.p = (int)(xc.seq & 1);
   xc.scale = 1.f / (float)WT;
-  mw_body<D, WT>(mode, P, O, B, ctrl, xc);
+  mw_body<D, WT>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, xc);
 }
 
 // bf16 shadow of the flat parameters + the conv fragment image, from the fp32 masters (start of
@@ -1424,9 +1445,11 @@ template <class D>
 void run(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, hipStream_t st) {
   mode |= probe_bits();
   const float inv_B = 1.f / (float)B;
-  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
+  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, P.stage2, P.meta2, A.ctrl, P.wimg, P.metaN, mode, inv_B, P,
+                     A, O);
   const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
-  hipLaunchKernelGGL(lenet_mw<D>, dim3(nblk), dim3(kWgT), 0, st, mode, P, O, B, A.ctrl);
+  hipLaunchKernelGGL(lenet_mw<D>, dim3(nblk), dim3(kWgT), 0, st, P.slab1, P.p2, P.dh1, P.h1, P.dh2, mode, B, P, O,
+                     A.ctrl);
 }
 
 template <class D>
@@ -1437,11 +1460,13 @@ void run_dp(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetO
   if (X.cap < O.n) throw std::runtime_error("lenet dp step: transport region smaller than the parameters");
   mode |= probe_bits();
   const float inv_B = 1.f / (float)B;
-  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, mode, P, A, O, inv_B);
+  hipLaunchKernelGGL(lenet_ms<D>, dim3(B), dim3(kT), 0, st, P.stage2, P.meta2, A.ctrl, P.wimg, P.metaN, mode, inv_B, P,
+                     A, O);
   const int m = mode | LENET_OPT;
 #define MLT_MWX(WV)                                                                                      \
   case WV:                                                                                               \
-    hipLaunchKernelGGL((lenet_mwx<D, WV>), dim3(nblk), dim3(kWgT), 0, st, m, P, O, B, A.ctrl, X); \
+    hipLaunchKernelGGL((lenet_mwx<D, WV>), dim3(nblk), dim3(kWgT), 0, st, P.slab1, P.p2, P.dh1, P.h1, P.dh2, m, B, \
+                       P, O, A.ctrl, X);                                                                          \
     break;
   switch (X.W) {
     MLT_MWX(1)
