@@ -961,11 +961,12 @@ struct Ctx {
   float lr, t;
 };
 
+template <int K>
 __device__ __forceinline__ void upd1(const LeNetOpt& O, const Ctx& c, uint16_t* shadow, int64_t i, float g, float p,
                                      float a, float s) {
   O.g[i] = g;
   if (!c.on) return;
-  opt_update(O.h, c.lr, c.t, p, g, a, s);
+  opt_update_k<K>(O.h, c.lr, c.t, p, g, a, s);
   O.p[i] = p;
   if (O.s1) O.s1[i] = a;
   if (O.s2) O.s2[i] = s;
@@ -1095,7 +1096,7 @@ __host__ __device__ constexpr int mw_fc_blocks() {
   return (mw_fc_waves<D>() + kWgT / 64 - 1) / (kWgT / 64);
 }
 
-template <int NIN, int NOUT, int WT>
+template <int NIN, int NOUT, int WT, int K>
 __device__ __forceinline__ void fc_wgrad(const Xch<WT>& xc, int tile, int B, const float* __restrict__ dY,
                                          const float* __restrict__ X, const LeNetOpt& O, const Ctx& c, uint16_t* shadow,
                                          int64_t offW, int64_t offb, uint16_t* __restrict__ timg, int tpitch,
@@ -1149,10 +1150,10 @@ __device__ __forceinline__ void fc_wgrad(const Xch<WT>& xc, int tile, int B, con
   if (wrow) {
     *reinterpret_cast<float4*>(O.g + iw) = gv;
     if (c.on) {
-      opt_update(O.h, c.lr, c.t, pw.x, gv.x, aw.x, sw.x);
-      opt_update(O.h, c.lr, c.t, pw.y, gv.y, aw.y, sw.y);
-      opt_update(O.h, c.lr, c.t, pw.z, gv.z, aw.z, sw.z);
-      opt_update(O.h, c.lr, c.t, pw.w, gv.w, aw.w, sw.w);
+      opt_update_k<K>(O.h, c.lr, c.t, pw.x, gv.x, aw.x, sw.x);
+      opt_update_k<K>(O.h, c.lr, c.t, pw.y, gv.y, aw.y, sw.y);
+      opt_update_k<K>(O.h, c.lr, c.t, pw.z, gv.z, aw.z, sw.z);
+      opt_update_k<K>(O.h, c.lr, c.t, pw.w, gv.w, aw.w, sw.w);
       *reinterpret_cast<float4*>(O.p + iw) = pw;
       if (O.s1) *reinterpret_cast<float4*>(O.s1 + iw) = aw;
       if (O.s2) *reinterpret_cast<float4*>(O.s2 + iw) = sw;
@@ -1168,10 +1169,10 @@ __device__ __forceinline__ void fc_wgrad(const Xch<WT>& xc, int tile, int B, con
         *reinterpret_cast<uint2*>(fimg + j * fpitch + c0) = make_uint2(pack2(h0, h1), pack2(h2, h3));
     }
   }
-  if (brow) upd1(O, c, shadow, ib, gb, pb, ab, sb);
+  if (brow) upd1<K>(O, c, shadow, ib, gb, pb, ab, sb);
 }
 
-template <class D, int WT>
+template <class D, int WT, int K>
 __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNetOpt& O, int B, int64_t* __restrict__ ctrl,
                                         const Xch<WT>& xc) {
   constexpr int C1 = D::C1, C2 = D::C2, F1 = D::F1, F2 = D::F2, NC = D::NC, FLAT = D::FLAT;
@@ -1227,7 +1228,7 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
     }
     O.g[dst] = gsum;
     if (c.on) {
-      opt_update(O.h, c.lr, c.t, p, gsum, a, s);
+      opt_update_k<K>(O.h, c.lr, c.t, p, gsum, a, s);
       O.p[dst] = p;
       if (O.s1) O.s1[dst] = a;
       if (O.s2) O.s2[dst] = s;
@@ -1260,12 +1261,12 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
     wv = __builtin_amdgcn_readfirstlane(wv);
     if (wv < NW3) {
       // (no transposed fc1 image: the per-sample kernel transposes fc1 in LDS)
-      fc_wgrad<FLAT, F1>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], nullptr, F1);
+      fc_wgrad<FLAT, F1, WT, K>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], nullptr, F1);
     } else if ((wv -= NW3) < NW4) {
-      fc_wgrad<F1, F2>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
+      fc_wgrad<F1, F2, WT, K>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
                        Fc<D>::P2T);
     } else if ((wv -= NW4) < NW5) {
-      fc_wgrad<F2, NC>(xc, wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9],
+      fc_wgrad<F2, NC, WT, K>(xc, wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9],
                        P.wimg ? P.wimg + kFc3T : nullptr, Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);
     } else if constexpr (Xch<WT>::on) {
       xc.sync();  // a wave without a tile still joins its block's exchange barriers
@@ -1300,6 +1301,20 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
   }
 }
 
+// the optimizer kind, once per block (uniform): each kind's body is contiguous code, so a launch
+// runs through one compact instruction footprint instead of all five kinds interleaved per update
+template <class D, int WT>
+__device__ __forceinline__ void mw_dispatch(int mode, const LeNetPtrs& P, const LeNetOpt& O, int B, int64_t* ctrl,
+                                            const Xch<WT>& xc) {
+  switch (O.h.kind) {
+    case OPT_ADAM: mw_body<D, WT, OPT_ADAM>(mode, P, O, B, ctrl, xc); break;
+    case OPT_ADAMW: mw_body<D, WT, OPT_ADAMW>(mode, P, O, B, ctrl, xc); break;
+    case OPT_ADAGRAD: mw_body<D, WT, OPT_ADAGRAD>(mode, P, O, B, ctrl, xc); break;
+    case OPT_ADAMAX: mw_body<D, WT, OPT_ADAMAX>(mode, P, O, B, ctrl, xc); break;
+    default: mw_body<D, WT, OPT_SGD>(mode, P, O, B, ctrl, xc); break;
+  }
+}
+
 // (the per-block first loads' pointers lead the arguments: preloaded into SGPRs, see lenet_ms)
 __device__ __forceinline__ LeNetPtrs with_first(LeNetPtrs P, const float* slab1, const float* p2, const float* dh1,
                                                 const float* h1, const float* dh2) {
@@ -1317,7 +1332,7 @@ __global__ __launch_bounds__(kWgT) void lenet_mw(const float* __restrict__ pslab
                                                  LeNetOpt O, int64_t* __restrict__ ctrl) {
   unsigned long long t0 = 0;
   if (mode & LENET_TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-  mw_body<D, 0>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, Xch<0>{});
+  mw_dispatch<D, 0>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, Xch<0>{});
   // LENET_TRACE: 100 MHz wall clock per block (start) and per wave (end): P.trace slots 64 + 5 blk (+1 + wave)
   if ((mode & LENET_TRACE) && P.trace && blockIdx.x < 100) {
     unsigned long long* tr = reinterpret_cast<unsigned long long*>(P.trace) + 64 + 5 * blockIdx.x;
@@ -1347,7 +1362,7 @@ __global__ __launch_bounds__(kWgT) void lenet_mwx(const float* __restrict__ psla
   xc.seq = X.seqs[blockIdx.x] + 1;  // per-block launch counter: identical on every block and rank
   xc.p = (int)(xc.seq & 1);
   xc.scale = 1.f / (float)WT;
-  mw_body<D, WT>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, xc);
+  mw_dispatch<D, WT>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, xc);
 }
 
 // bf16 shadow of the flat parameters + the conv fragment image, from the fp32 masters (start of
