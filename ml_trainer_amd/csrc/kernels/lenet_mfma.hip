@@ -214,6 +214,21 @@ __device__ __forceinline__ u32x4 f1t_frag(const uint16_t* img, int tile, int q) 
                (unsigned)(uint16_t)hi[2] | ((unsigned)(uint16_t)hi[3] << 16)};
 }
 
+// fc2 dgrad B fragment (as f1t_frag) from the XOR-swizzled fc2 image [F2][16 chunks] (KsLds::F2S)
+template <int F2, int F1>
+__device__ __forceinline__ u32x4 f2t_frag(const uint16_t* img, int tile, int q) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+  const int col = min(16 * tile + 4 * p, F1 - 4), c = col >> 3, e = col & 7;
+  const int r0 = min(32 * q + 8 * g + qq, F2 - 1), r1 = min(32 * q + 8 * g + qq + 4, F2 - 1);
+  auto pos = [](int r, int cc) { return r * 16 + (cc ^ (((r & 3) << 2) | ((r >> 2) & 3))); };
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + pos(r0, c) * 8 + e));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + pos(r1, c) * 8 + e));
+  return u32x4{(unsigned)(uint16_t)lo[0] | ((unsigned)(uint16_t)lo[1] << 16),
+               (unsigned)(uint16_t)lo[2] | ((unsigned)(uint16_t)lo[3] << 16),
+               (unsigned)(uint16_t)hi[0] | ((unsigned)(uint16_t)hi[1] << 16),
+               (unsigned)(uint16_t)hi[2] | ((unsigned)(uint16_t)hi[3] << 16)};
+}
+
 // The fc chain's wave schedule. Fragments (~150 KB per CU and step) are fetched where the issuing
 // waves are otherwise idle or light -- the vector memory path of a CU moves them at ~35 B/clk and a
 // wave stalls while its loads queue:
@@ -246,15 +261,24 @@ struct KsLds {
   // at chunks (r & 1) .. (r & 1) + FLAT/8 - 1 -- the one-chunk shift of odd rows makes the transposed
   // reads of the fc1 dgrad (ds_read_b64_tr_b16: 8 rows x 32 bytes per 32-lane half) conflict-free
   static constexpr int F1S = D::FLAT / 8 + 1;
-  // zero-filled at entry (one contiguous span): every image whose padding / untouched cells an
-  // MFMA fragment reads before P10
-  alignas(16) uint16_t p1h[14 * P1HS * 8];           // pooled conv1 [y][x][ic8]
-  alignas(16) uint16_t p1c[D::C1 * 14 * P1CS];       // pooled conv1 [ic][y][x]
-  // end of the zero span
-  alignas(16) uint16_t xh[32 * XHS * 4];             // input [Y][X][c4] (c = 3 zero; X >= 32 never read)
+  // fc2 weight image [F2 rows][16 chunks of 8 bf16]: chunk c of row r at position
+  // c ^ ((r & 3) << 2 | (r >> 2) & 3) (256-byte rows: conflict-free transposed reads)
+  static constexpr int F2S = 16;
+  static_assert(D::F1 <= 8 * F2S, "fc2 image rows");
+  alignas(16) uint16_t p1c[D::C1 * 14 * P1CS];       // pooled conv1 [ic][y][x] (zeroed at entry)
   alignas(16) uint16_t xc[3 * 32 * XCS];             // input [c][Y][X48] (X >= 32 zeroed separately)
-  alignas(16) uint16_t w1f[4 * 64 * 8];              // conv1 B fragments [kstep][lane][8]
-  alignas(16) uint16_t w2f[7 * 64 * 8];              // conv2 forward B fragments
+  // P0 .. P3 the input / conv-forward images; P4c .. P7 the fc2 weight image (written from the fc2
+  // forward's register fragments, read transposed by the fc2 dgrad)
+  union V {
+    struct Fw {
+      alignas(16) uint16_t p1h[14 * P1HS * 8];       // pooled conv1 [y][x][ic8] (zeroed at entry)
+      alignas(16) uint16_t xh[32 * XHS * 4];         // input [Y][X][c4] (c = 3 zero; X >= 32 never read)
+      alignas(16) uint16_t w1f[4 * 64 * 8];          // conv1 B fragments [kstep][lane][8]
+      alignas(16) uint16_t w2f[7 * 64 * 8];          // conv2 forward B fragments
+      alignas(16) uint8_t raw[3072];                 // this step's raw image (staged or gathered)
+    } f;
+    alignas(16) uint16_t f2img[D::F2 * F2S * 8];
+  } v;
   // bf16 A rows of the fc MFMAs (tails zero to the k-step multiple)
   alignas(16) uint16_t fb16[32 * F::K1];             // flattened pooled conv2 (fc1)
   alignas(16) uint16_t h1b[32 * F::K2];              // fc1 output (fc2)
@@ -272,7 +296,6 @@ struct KsLds {
   alignas(16) float f32[D::FLAT];                    // flattened pooled conv2, fp32 (stored for the fc1 wgrad)
   unsigned long long tr[32];                         // LENET_TRACE stamps
   double ce[2];                                      // this sample's (loss / B, hit / B)
-  alignas(16) uint8_t raw[3072];                     // this step's raw image (staged or gathered)
   float b1s[16], b2s[16];
   alignas(16) float fb[D::F1 + D::F2 + D::NC];       // fc biases
   uint8_t i1[D::C1 * 196];
@@ -347,7 +370,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
                                                LeNetAug A, LeNetOpt O) {
   constexpr int C1 = D::C1, C2 = D::C2, FLAT = D::FLAT, F1 = D::F1, F2 = D::F2, NC = D::NC;
   using S = KsLds<D>;
-  static_assert(offsetof(S, w2f) == offsetof(S, w1f) + 2 * kW2F, "forward fragment images must be contiguous");
+  static_assert(offsetof(typename S::V::Fw, w2f) == offsetof(typename S::V::Fw, w1f) + 2 * kW2F,
+                "forward fragment images must be contiguous");
   static_assert(sizeof(S) <= 160 * 1024, "LDS");
   __shared__ S L;
   // w is wave-uniform: readfirstlane makes the per-wave role branches scalar (uniform) branches,
@@ -428,11 +452,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
   const bool hit = aug && mstep == step && mpos == pos;  // block-uniform
   int64_t tgt = 0;
   {
-    // zero span [p1h .. d1 end) and the X >= 32 columns of xc
-    constexpr int ZB = (int)(offsetof(S, xh) - offsetof(S, p1h));
-    static_assert(ZB % 16 == 0, "zero span");
-    uint4* z = reinterpret_cast<uint4*>(L.p1h);
-    for (int e = t; e < ZB / 16; e += kT) z[e] = make_uint4(0u, 0u, 0u, 0u);
+    // zero the pooled-conv1 images p1h, p1c and the X >= 32 columns of xc
+    constexpr int ZH = (int)sizeof(L.v.f.p1h) / 16, ZC = (int)sizeof(L.p1c) / 16;
+    static_assert(sizeof(L.v.f.p1h) % 16 == 0 && sizeof(L.p1c) % 16 == 0, "zero spans");
+    for (int e = t; e < ZH + ZC; e += kT) {
+      uint4* z = e < ZH ? reinterpret_cast<uint4*>(L.v.f.p1h) + e : reinterpret_cast<uint4*>(L.p1c) + (e - ZH);
+      *z = make_uint4(0u, 0u, 0u, 0u);
+    }
     if (t < 3 * 32 * 2) reinterpret_cast<uint4*>(L.xc + (t >> 1) * XCS + 32)[t & 1] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 32 * F1M::K1 - FLAT) L.fb16[FLAT + t] = 0;
     if (t < 32 * F1M::K2 - F1) L.h1b[F1 + t] = 0;
@@ -440,7 +466,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
     if (t < 32 * F1M::B3K - NC) L.dlb[NC + t] = 0;
     if (t < 32 * F1M::B2K - F2) L.dh2b[F2 + t] = 0;
     if (t < 32 * F1M::B1K - F1) L.dh1b[F1 + t] = 0;
-    uint4* wl = reinterpret_cast<uint4*>(L.w1f);  // w1f | w2f | w2d are contiguous
+    uint4* wl = reinterpret_cast<uint4*>(L.v.f.w1f);  // w1f | w2f | w2d are contiguous
     if (t < WIF) wl[t] = wi0;
     if (t < NFB) L.fb[t] = fbv;
     if (t < 16) {
@@ -460,10 +486,10 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
       idx = idx < 0 ? 0 : (idx >= A.n ? A.n - 1 : idx);
       const uint4 graw = reinterpret_cast<const uint4*>(A.data + idx * 3072)[min(t, 191)];
       tgt = sload(P.dtargets + idx);
-      if (t < 192) reinterpret_cast<uint4*>(L.raw)[t] = graw;
+      if (t < 192) reinterpret_cast<uint4*>(L.v.f.raw)[t] = graw;
     } else {
       tgt = mtgt;
-      if (t < 192) reinterpret_cast<uint4*>(L.raw)[t] = sraw;
+      if (t < 192) reinterpret_cast<uint4*>(L.v.f.raw)[t] = sraw;
     }
     int ci, cj;
     bool fl;
@@ -471,13 +497,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
     lbar();
     stamp(17);
     float v[3];
-    aug_pixel(L.raw, Y0, X0, ci, cj, fl, A, v);
+    aug_pixel(L.v.f.raw, Y0, X0, ci, cj, fl, A, v);
     px = make_uint2(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), 0));
   } else {
     px = make_uint2(pack2(f32_to_bf16(xin[0]), f32_to_bf16(xin[1])), pack2(f32_to_bf16(xin[2]), 0));
     tgt = sload(P.targets + b);
   }
-  reinterpret_cast<uint2*>(L.xh)[Y0 * XHS + X0] = px;
+  reinterpret_cast<uint2*>(L.v.f.xh)[Y0 * XHS + X0] = px;
   L.xc[(0 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x & 0xffff);
   L.xc[(1 * 32 + Y0) * XCS + X0] = (uint16_t)(px.x >> 16);
   L.xc[(2 * 32 + Y0) * XCS + X0] = (uint16_t)(px.y & 0xffff);
@@ -492,7 +518,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
   {
     u32x4 bw[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) bw[s] = *reinterpret_cast<const u32x4*>(L.w1f + (s * 64 + lane) * 8);
+    for (int s = 0; s < 4; ++s) bw[s] = *reinterpret_cast<const u32x4*>(L.v.f.w1f + (s * 64 + lane) * 8);
     const int a = m >> 2, r = m & 3, dx = m & 1, oc = m >> 1;
     const float bias = L.b1s[min(oc, 15)];
     // tiles on waves 0 .. kC1W-1 only: the other waves spend this phase issuing the fc1 forward
@@ -504,7 +530,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int qq = 4 * s + g, kh = qq / 3, i = qq - 3 * kh;
-        u32x4 av = *reinterpret_cast<const u32x4*>(L.xh + ((qq < 15 ? (Y + kh) * XHS + 2 * pxx + 2 * i : 0)) * 4);
+        u32x4 av = *reinterpret_cast<const u32x4*>(L.v.f.xh + ((qq < 15 ? (Y + kh) * XHS + 2 * pxx + 2 * i : 0)) * 4);
         if (qq >= 15) av = u32x4{0u, 0u, 0u, 0u};
         acc = mfma(av, bw[s], acc);
       }
@@ -522,7 +548,7 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
       if (oc < C1 && cc < 196) {
         const int cy = cc / 14, cx = cc - 14 * cy;
         const uint16_t hv = f32_to_bf16(pv);
-        L.p1h[(cy * P1HS + cx) * 8 + oc] = hv;
+        L.v.f.p1h[(cy * P1HS + cx) * 8 + oc] = hv;
         L.p1c[(oc * 14 + cy) * P1CS + cx] = hv;
         L.i1[oc * 196 + cc] = code;
       }
@@ -541,14 +567,8 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
   // role's register-resident fragments share registers with the other's.
   if (w < 8) {
     // ---- role A: fc3 / fc2 dgrad ----
-    u32x4 f3t[F1M::B3K], f2t[F1M::B2K];  // first needed first (vmcnt order)
+    u32x4 f3t[F1M::B3K];
     if (w < F1M::B3T) frag_rows<F1M::B3K, P3T, F2, NC>(f3t, pwimg + kFc3T, w);
-    if (mode & LENET_PROBE_NOF2) {
-#pragma unroll
-      for (int q = 0; q < F1M::B2K; ++q) f2t[q] = u32x4{0u, 0u, 0u, 0u};
-    } else if (w < F1M::B2T) {
-      frag_rows<F1M::B2K, P2T, F1, F2>(f2t, pwimg + kFc2T, w);
-    }
     lbar();  // P3 (conv2)
     stamp(3);
     lbar();  // P4a (fc1 forward)
@@ -568,9 +588,13 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
     }
     lbar();
     stamp(20);
-    if (w < F1M::B2T) {  // fc2 dgrad (x the fc1 ReLU mask)
+    if (w < F1M::B2T) {  // fc2 dgrad (x the fc1 ReLU mask), W2 read transposed from the fc2 image
       const int k = 16 * w + m;
-      const float v = row_dot(f2t, L.dh2b);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < F1M::B2K; ++q)
+        acc = mfma(*reinterpret_cast<const u32x4*>(L.dh2b + 32 * q + 8 * g), f2t_frag<F2, F1>(L.v.f2img, w, q), acc);
+      const float v = acc[0];
       if (g == 0 && k < F1) {
         const float d = L.sh1[k] > 0.f ? v : 0.f;
         L.sdh1[k] = d;
@@ -629,9 +653,9 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
 #pragma unroll
       for (int s = 0; s < 7; ++s) {
         const int tap = 4 * s + g, kh = tap / 5, kw = tap - 5 * kh;
-        u32x4 a = *reinterpret_cast<const u32x4*>(L.p1h + ((tap < 25 ? (y + kh) * P1HS + x + kw : 0)) * 8);
+        u32x4 a = *reinterpret_cast<const u32x4*>(L.v.f.p1h + ((tap < 25 ? (y + kh) * P1HS + x + kw : 0)) * 8);
         if (tap >= 25) a = u32x4{0u, 0u, 0u, 0u};
-        acc = mfma(a, *reinterpret_cast<const u32x4*>(L.w2f + (s * 64 + lane) * 8), acc);
+        acc = mfma(a, *reinterpret_cast<const u32x4*>(L.v.f.w2f + (s * 64 + lane) * 8), acc);
       }
       const int cc = 4 * wt + g, oc = m;
       float pv;
@@ -706,6 +730,17 @@ __global__ __launch_bounds__(kT) void lenet_ms(uint8_t* __restrict__ pstage2, in
       }
     } else if (w >= F1M::W1F) {
       put_f1img();
+    }
+    if (w >= F1M::W2F && w < F1M::W2F + F1M::T2) {  // the fc2 forward fragments -> the fc2 image
+      const int row = 16 * (w - F1M::W2F) + m;
+      if (row < F2) {
+#pragma unroll
+        for (int q = 0; q < F1M::K2; ++q) {
+          const int c = 4 * q + g;
+          if (c < F1 / 8)
+            *reinterpret_cast<u32x4*>(L.v.f2img + (row * S::F2S + (c ^ (((row & 3) << 2) | ((row >> 2) & 3)))) * 8) = f2w[q];
+        }
+      }
     }
     lbar();
     stamp(4);
@@ -1263,8 +1298,7 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
       // (no transposed fc1 image: the per-sample kernel transposes fc1 in LDS)
       fc_wgrad<FLAT, F1, WT, K>(xc, wv, B, P.dh1, P.p2, O, c, shadow, O.off[4], O.off[5], nullptr, F1);
     } else if ((wv -= NW3) < NW4) {
-      fc_wgrad<F1, F2, WT, K>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], P.wimg ? P.wimg + kFc2T : nullptr,
-                       Fc<D>::P2T);
+      fc_wgrad<F1, F2, WT, K>(xc, wv, B, P.dh2, P.h1, O, c, shadow, O.off[6], O.off[7], nullptr, Fc<D>::P2T);
     } else if ((wv -= NW4) < NW5) {
       fc_wgrad<F2, NC, WT, K>(xc, wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9],
                        P.wimg ? P.wimg + kFc3T : nullptr, Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: per-sample kernel variants, same box. Numerics first (every bf16 LeNet test on the in-tree
 # build), then alternated benches over ab/*.so: v0 = round-3 kernel, v1 = LDS fc1 image,
-# v2 = v1 + kernarg preload of the first-load pointers (KS), v3 = v2 + the same for KW, v4 = v3 + the optimizer kind dispatched once per KW block.
+# v3 = v1 + kernarg preload of the first-load pointers (KS and KW), v4 = v3 + the optimizer kind dispatched once per KW block, v5 = v4 + the LDS fc2 image.
 set -o pipefail
 O=gpurun_out/r4ab
 mkdir -p $O
