@@ -655,6 +655,22 @@ __device__ __forceinline__ void glds_tile(uint8_t* lds, const uint16_t* __restri
   }
 }
 
+// The same tile copy from a uniform row base (SGPRs) + a per-thread 32-bit byte offset computed
+// once per kernel (glds_off_row): the ring kernels' per-stage address math was ~45 VALU (64-bit
+// row * ld products for 5 DMAs) in a loop whose VALU issue bounds it; the SADDR form also costs
+// one VGPR per DMA instead of two. `wu` is the wave index as a scalar (readfirstlane), so the LDS
+// destinations (M0) need no per-DMA readfirstlane either. Full tiles only (no row clamp).
+__device__ __forceinline__ void glds_tile2(uint8_t* lds, const uint16_t* rowbase, uint32_t o0, uint32_t o1, int wu) {
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(rowbase);
+  __builtin_amdgcn_global_load_lds((const void*)(b + o0), (lds_void*)(lds + wu * 64 * 16), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((const void*)(b + o1), (lds_void*)(lds + (256 + wu * 64) * 16), 16, 0, 0);
+}
+// byte offset of this thread's DMA i of glds_tile(lds, g, ld, row0, 64, col0) from g + row0 * ld + col0
+__device__ __forceinline__ uint32_t glds_off_row(int64_t ld, int i) {
+  const int e = threadIdx.x + 256 * i, r = e >> 3, c = (e & 7) ^ (r & 7);
+  return (uint32_t)((r * ld + c * 8) * 2);
+}
+
 // ds_read_b64_tr_b16 as inline asm for the ring kernels: through the builtin, hipcc cannot tell
 // the read from the in-flight LDS-DMA writes and puts an s_waitcnt vmcnt(0) in front of it, which
 // drains the whole ring every step. The asm read is invisible to the compiler's waitcnt pass, so
@@ -750,8 +766,10 @@ __device__ __forceinline__ void block_colsum64(float (&v)[4][4], float* red, flo
     out[threadIdx.x] = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
 }
 
-template <int NK, int kRing>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t* __restrict__ qkv,
+// FULLT: S % 64 == 0 (every ring stage a whole tile: the clamped-row copy path is compiled out, which
+// keeps the 2-group kernel within 256 VGPRs)
+template <int NK, int kRing, bool FULLT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                  const uint16_t* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
@@ -786,10 +804,23 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
   }
   const float sl2 = scale * 1.4426950408889634f;
   const int nqb = (S + AB - 1) / AB;
-  // stage = 5 glds per thread: 2 (Q) + 2 (dO) + 1 (waves 0/2: LSE row, waves 1/3: delta row)
+  // stage = 5 glds per thread: 2 (Q) + 2 (dO) + 1 (waves 0/2: LSE row, waves 1/3: delta row);
+  // full stages from sources computed once (advance q0 rows per stage), the partial last one clamped
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const uint32_t oq0 = glds_off_row(ld, 0), oq1 = glds_off_row(ld, 1);
+  const uint32_t oo0 = glds_off_row((int64_t)D, 0), oo1 = glds_off_row((int64_t)D, 1);
+  const uint32_t ol = (uint32_t)lane * ((wu & 1) ? (uint32_t)H * 4u : 4u);  // this lane's LSE / delta entry
   auto issue = [&](int slot, int qb) {
     uint8_t* st = smem + slot * STAGE;
     const int q0 = qb * AB, nv = min(AB, S - q0);
+    if constexpr (FULLT) {
+      glds_tile2(st, qkv + (base + q0) * ld + h * AH, oq0, oq1, wu);
+      glds_tile2(st + kTile, dout + (base + q0) * (int64_t)D + h * AH, oo0, oo1, wu);
+      const float* rb = (wu & 1) ? delta + (base + q0) * H + h : lse + ((int64_t)b * H + h) * S + q0;
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint8_t*>(rb) + ol),
+                                       (lds_void*)(st + 2 * kTile + (wu & 1) * AB * 4), 4, 0, 0);
+      return;
+    }
     glds_tile(st, qkv, ld, base + q0, nv, h * AH);
     glds_tile(st + kTile, dout, (int64_t)D, base + q0, nv, h * AH);
     const int qq = q0 + min(lane, nv - 1);
@@ -975,7 +1006,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_ring_kernel(const uint16_t*
 // The dQ ring kernel runs FIRST and computes delta = rowsum(dO * O) for its own queries in its
 // prologue (dO is in its registers anyway; O is one more 16-byte load per fragment), publishing it
 // for the dK/dV kernel that follows -- no separate delta pass over dO and O.
-template <int NQ, int kRing>
+template <int NQ, int kRing, bool FULLT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                const uint16_t* __restrict__ dout,
                                                                const uint16_t* __restrict__ out,
@@ -996,9 +1027,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
   const int len = lens ? lens[b] : S;
   const float sl2 = scale * 1.4426950408889634f;
   const int nkb = (len + AB - 1) / AB;
-  auto issue = [&](int slot, int kb) {
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const uint32_t ok0 = glds_off_row(ld, 0), ok1 = glds_off_row(ld, 1);
+  auto issue = [&](int slot, int kb) {  // (K and V: the same rows, D columns apart)
     uint8_t* st = smem + slot * STAGE;
     const int k0 = kb * AB, nv = min(AB, S - k0);
+    if constexpr (FULLT) {
+      const uint16_t* kr = qkv + (base + k0) * ld + D + h * AH;
+      glds_tile2(st, kr, ok0, ok1, wu);
+      glds_tile2(st + kTile, kr + D, ok0, ok1, wu);
+      return;
+    }
     glds_tile(st, qkv, ld, base + k0, nv, D + h * AH);
     glds_tile(st + kTile, qkv, ld, base + k0, nv, 2 * D + h * AH);
   };
@@ -1180,25 +1219,27 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   const int ring = rv ? atoi(rv) : 4;
   if (ring == 3 || ring == 4) {
     const bool k2 = attn_groups("MLT_ATTN_DKDV_GROUPS", S, 2) == 2, q2 = attn_groups("MLT_ATTN_DQ_GROUPS", S) == 2;
-#define MLT_RING_LAUNCH(RD)                                                                                         \
-  {                                                                                                                 \
-    if (q2)                                                                                                         \
-      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, out, lse, delta, lens,  \
-                         dqkv, S, H, scale, colpart_q);                                                             \
-    else                                                                                                            \
-      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, out, lse, delta, lens,  \
-                         dqkv, S, H, scale, colpart_q);                                                             \
-    if (k2)                                                                                                         \
-      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
-                         dqkv, S, H, scale, colpart_kv);                                                            \
-    else                                                                                                            \
-      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,    \
-                         dqkv, S, H, scale, colpart_kv);                                                            \
+#define MLT_RING_LAUNCH(RD, FL)                                                                                       \
+  {                                                                                                                   \
+    if (q2)                                                                                                           \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD, FL>), g2, dim3(256), 0, st, qkv, dout, out, lse, delta, lens, \
+                         dqkv, S, H, scale, colpart_q);                                                               \
+    else                                                                                                              \
+      hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD, FL>), g1, dim3(256), 0, st, qkv, dout, out, lse, delta, lens, \
+                         dqkv, S, H, scale, colpart_q);                                                               \
+    if (k2)                                                                                                           \
+      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD, FL>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,   \
+                         dqkv, S, H, scale, colpart_kv);                                                              \
+    else                                                                                                              \
+      hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD, FL>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,   \
+                         dqkv, S, H, scale, colpart_kv);                                                              \
   }
-    if (ring == 3)
-      MLT_RING_LAUNCH(3)
-    else
-      MLT_RING_LAUNCH(4)
+    const bool full = S % AB == 0;
+    if (ring == 3) {
+      if (full) MLT_RING_LAUNCH(3, true) else MLT_RING_LAUNCH(3, false)
+    } else {
+      if (full) MLT_RING_LAUNCH(4, true) else MLT_RING_LAUNCH(4, false)
+    }
 #undef MLT_RING_LAUNCH
     // partial rows actually written: B x (row blocks of the chosen group count)
     if (rows_kv) *rows_kv = B * ((S + (k2 ? 127 : 63)) / (k2 ? 128 : 64));
