@@ -1,4 +1,5 @@
 // Host side of the one-shot / two-shot xGMI all-reduce (kernels/allreduce.hip).
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -16,7 +17,7 @@ static void hcheck(hipError_t e, const char* what) {
 // (the t* / f* parts belong to the two-shot algorithm, ff to the fused LeNet step's exchange, which
 // shares `data`), every part 256-byte aligned
 struct RegionLayout {
-  size_t flags, t1, t2, f1, f2, ff, bytes;
+  size_t flags, t1, t2, f1, f2, ff, fe, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
@@ -28,7 +29,8 @@ static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t sl
   L.f1 = align256(L.t2 + tb);
   L.f2 = align256(L.f1 + fl);
   L.ff = align256(L.f2 + fl);
-  L.bytes = L.ff + (size_t)2 * XgmiAllReduce::kFusedBlocks * world * sizeof(uint64_t);
+  L.fe = align256(L.ff + (size_t)2 * XgmiAllReduce::kFusedBlocks * world * sizeof(uint64_t));
+  L.bytes = L.fe + 256;  // the device copy of the sticky error word (fused step)
   return L;
 }
 
@@ -96,6 +98,7 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
     P->f1[q] = reinterpret_cast<uint64_t*>(c + L.f1);
     P->f2[q] = reinterpret_cast<uint64_t*>(c + L.f2);
     ff_[q] = reinterpret_cast<uint64_t*>(c + L.ff);
+    if (q == rank_) derr_ = reinterpret_cast<unsigned*>(c + L.fe);
   }
   opened_ = true;
 }
@@ -123,6 +126,9 @@ XgmiFused XgmiAllReduce::fused_view() const {
   }
   X.seqs = fseqs_;
   X.err = err_;
+  X.derr = derr_;
+  const char* pv = std::getenv("MLT_XGMI_PROTO");
+  X.proto = pv ? (std::atoi(pv) & 3) : 0;
   X.cap = cap_;
   X.timeout = timeout_ms_ * 100000LL;
   X.rank = rank_;

@@ -97,6 +97,7 @@ class XgmiAllReduce {
   uint64_t* seqs_ = nullptr;
   uint64_t* fseqs_ = nullptr;
   uint64_t* ff_[8] = {nullptr};
+  unsigned* derr_ = nullptr;  // device copy of the error word (in the region)
   bool opened_ = false;
   int fault_ = 0;
   void* peers_host_ = nullptr;  // XgmiPeers

@@ -235,10 +235,15 @@ struct XgmiFused {
   float* data[kXgmiMaxRanks];      // per-rank [2][cap] fp32 (indexed by flat parameter offset)
   uint64_t* flags[kXgmiMaxRanks];  // per-rank [2][G][W]
   uint64_t* seqs;                  // [G] per-block launch counters (this rank)
-  unsigned* err;                   // sticky error word (host-mapped)
+  unsigned* err;                   // sticky error word (host-mapped: the host polls it)
+  unsigned* derr;                  // its device copy (uncached region memory: what the kernel reads)
   int64_t cap;
   long long timeout;               // ticks of the 100 MHz constant clock
   int rank, W, G, fault;
+  // protocol (A/B knob MLT_XGMI_PROTO): bit 0 = release / acquire fences around plain payload
+  // accesses (else system-scope sc0 sc1 payload and flag accesses, no fences); bit 1 = read the
+  // host-mapped error word at block start (else the device copy)
+  int proto;
 };
 // two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,

@@ -1033,10 +1033,43 @@ struct Xch {
   unsigned errv;
   float scale;
 
+  // payload accesses: with X->proto bit 0 plain (ordered by the release / acquire fences of sync),
+  // else system-scope relaxed atomics (global_load / store sc0 sc1: nothing of them stays in a
+  // cache of either GPU), 8 bytes each
   __device__ __forceinline__ float* mine() const { return X->data[X->rank] + p * X->cap; }
-  __device__ __forceinline__ void put1(int64_t i, float v) const { mine()[i] = v; }
-  __device__ __forceinline__ void put4(int64_t i, float4 v) const { *reinterpret_cast<float4*>(mine() + i) = v; }
-  // all threads of the block, once
+  __device__ __forceinline__ bool fenced() const { return (X->proto & 1) != 0; }
+  __device__ __forceinline__ void st2(float* a, float x, float y) const {
+    if (fenced()) {
+      *reinterpret_cast<float2*>(a) = make_float2(x, y);
+    } else {
+      const uint64_t v = (uint64_t)__float_as_uint(x) | ((uint64_t)__float_as_uint(y) << 32);
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __device__ __forceinline__ float2 ld2(const float* a) const {
+    if (fenced()) return *reinterpret_cast<const float2*>(a);
+    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+  }
+  __device__ __forceinline__ float ld1(const float* a) const {
+    if (fenced()) return *a;
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  }
+  __device__ __forceinline__ void put1(int64_t i, float v) const {
+    if (fenced()) {
+      mine()[i] = v;
+    } else {
+      __hip_atomic_store(reinterpret_cast<unsigned*>(mine() + i), __float_as_uint(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __device__ __forceinline__ void put4(int64_t i, float4 v) const {
+    st2(mine() + i, v.x, v.y);
+    st2(mine() + i + 2, v.z, v.w);
+  }
+  // all threads of the block, once: every storing wave drains its payload stores (vmcnt(0)), the
+  // workgroup barrier, one flag store per peer (a release store in the fenced protocol), the polls
+  // of the own flag row (relaxed system loads; the fenced protocol adds one acquire fence after)
   __device__ __forceinline__ bool sync() const {
     const int t = threadIdx.x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
@@ -1050,12 +1083,16 @@ struct Xch {
         } else {
           if (!withhold) {
             uint64_t* f = X->flags[t] + ((int64_t)p * X->G + blk) * WT + X->rank;
-            __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (fenced())
+              __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+              __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           const uint64_t* f = X->flags[X->rank] + ((int64_t)p * X->G + blk) * WT + t;
           const long long t0 = wall_clock64();
           while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
             if (wall_clock64() - t0 > X->timeout) {  // 100 MHz constant clock
+              __hip_atomic_fetch_or(X->derr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               __hip_atomic_fetch_or(X->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               *failed = 1;
               break;
@@ -1064,8 +1101,10 @@ struct Xch {
           }
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: this CU's caches see the peers' stores
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (fenced()) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: this CU's caches see the peers' stores
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     __syncthreads();
     const bool ok = *failed == 0;
@@ -1077,7 +1116,7 @@ struct Xch {
   __device__ __forceinline__ float get1(int64_t i) const {
     float v[WT];
 #pragma unroll
-    for (int q = 0; q < WT; ++q) v[q] = X->data[q][p * X->cap + i];
+    for (int q = 0; q < WT; ++q) v[q] = ld1(X->data[q] + p * X->cap + i);
     __builtin_amdgcn_sched_barrier(0);
     float s = v[0];
 #pragma unroll
@@ -1087,17 +1126,20 @@ struct Xch {
     return s;
   }
   __device__ __forceinline__ float4 get4(int64_t i) const {
-    float4 v[WT];
+    float2 lo[WT], hi[WT];
 #pragma unroll
-    for (int q = 0; q < WT; ++q) v[q] = *reinterpret_cast<const float4*>(X->data[q] + p * X->cap + i);
+    for (int q = 0; q < WT; ++q) {
+      lo[q] = ld2(X->data[q] + p * X->cap + i);
+      hi[q] = ld2(X->data[q] + p * X->cap + i + 2);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    float4 s = v[0];
+    float4 s = make_float4(lo[0].x, lo[0].y, hi[0].x, hi[0].y);
 #pragma unroll
     for (int q = 1; q < WT; ++q) {
-      s.x += v[q].x;
-      s.y += v[q].y;
-      s.z += v[q].z;
-      s.w += v[q].w;
+      s.x += lo[q].x;
+      s.y += lo[q].y;
+      s.z += hi[q].x;
+      s.w += hi[q].y;
     }
     s.x *= scale;
     s.y *= scale;
@@ -1390,8 +1432,9 @@ __global__ __launch_bounds__(kWgT) void lenet_mwx(const float* __restrict__ psla
   xc.errv = 0u;
   if (threadIdx.x == 0) {
     failed = 0;
-    // in flight during the reduction; checked before this block publishes anything
-    xc.errv = __hip_atomic_load(X.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // in flight during the reduction; checked before this block publishes anything (the device copy
+    // in the region: a local read, not a PCIe round trip to the host-mapped word)
+    xc.errv = __hip_atomic_load((X.proto & 2) ? X.err : X.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   xc.seq = X.seqs[blockIdx.x] + 1;  // per-block launch counter: identical on every block and rank
   xc.p = (int)(xc.seq & 1);
