@@ -17,7 +17,7 @@ static void hcheck(hipError_t e, const char* what) {
 // (the t* / f* parts belong to the two-shot algorithm, ff to the fused LeNet step's exchange, which
 // shares `data`), every part 256-byte aligned
 struct RegionLayout {
-  size_t flags, t1, t2, f1, f2, ff, fe, bytes;
+  size_t flags, t1, t2, f1, f2, fg, fe, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
@@ -28,9 +28,9 @@ static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t sl
   L.t2 = align256(L.t1 + tb);
   L.f1 = align256(L.t2 + tb);
   L.f2 = align256(L.f1 + fl);
-  L.ff = align256(L.f2 + fl);
-  L.fe = align256(L.ff + (size_t)2 * XgmiAllReduce::kFusedBlocks * world * sizeof(uint64_t));
-  L.bytes = L.fe + 256;  // the device copy of the sticky error word (fused step)
+  L.fg = align256(L.f2 + fl);                                // fused step: [2][cap] granules
+  L.fe = align256(L.fg + (size_t)2 * cap * sizeof(uint64_t));  // fused step: device error word
+  L.bytes = L.fe + 256;
   return L;
 }
 
@@ -97,7 +97,7 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
     P->t2[q] = reinterpret_cast<float*>(c + L.t2);
     P->f1[q] = reinterpret_cast<uint64_t*>(c + L.f1);
     P->f2[q] = reinterpret_cast<uint64_t*>(c + L.f2);
-    ff_[q] = reinterpret_cast<uint64_t*>(c + L.ff);
+    fg_[q] = reinterpret_cast<uint64_t*>(c + L.fg);
     if (q == rank_) derr_ = reinterpret_cast<unsigned*>(c + L.fe);
   }
   opened_ = true;
@@ -120,15 +120,11 @@ XgmiFused XgmiAllReduce::fused_view() const {
   const XgmiPeers* P = static_cast<const XgmiPeers*>(peers_host_);
   XgmiFused X;
   std::memset(&X, 0, sizeof(X));
-  for (int q = 0; q < world_; ++q) {
-    X.data[q] = P->data[q];
-    X.flags[q] = ff_[q];
-  }
+  (void)P;
+  for (int q = 0; q < world_; ++q) X.gran[q] = fg_[q];
   X.seqs = fseqs_;
   X.err = err_;
   X.derr = derr_;
-  const char* pv = std::getenv("MLT_XGMI_PROTO");
-  X.proto = pv ? (std::atoi(pv) & 3) : 0;
   X.cap = cap_;
   X.timeout = timeout_ms_ * 100000LL;
   X.rank = rank_;

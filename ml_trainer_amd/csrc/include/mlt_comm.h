@@ -77,9 +77,9 @@ class XgmiAllReduce {
   // must use the same algorithm for a given call. Graphs keep the algorithm they were captured with.
   void set_algo(int a);
   int algo() const { return algo_; }
-  // the fused LeNet data-parallel step's view (kernels/lenet_mfma.hip): the data region, a flag
-  // area of its own ([2][kFusedBlocks][W]) and per-block counters of its own; timeout / fault as
-  // set now (graphs keep the values they were captured with). World size 1 = loopback.
+  // the fused LeNet data-parallel step's view (kernels/lenet_mfma.hip): a granule array of its own
+  // ([2][cap] x 8 bytes), per-block counters of its own, the device copy of the error word; timeout /
+  // fault as set now (graphs keep the values they were captured with). World size 1 = loopback.
   static constexpr int kFusedBlocks = 128;
   XgmiFused fused_view() const;
 
@@ -96,7 +96,7 @@ class XgmiAllReduce {
   long long timeout_ms_ = 2000;
   uint64_t* seqs_ = nullptr;
   uint64_t* fseqs_ = nullptr;
-  uint64_t* ff_[8] = {nullptr};
+  uint64_t* fg_[8] = {nullptr};
   unsigned* derr_ = nullptr;  // device copy of the error word (in the region)
   bool opened_ = false;
   int fault_ = 0;

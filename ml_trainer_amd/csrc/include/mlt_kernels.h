@@ -227,23 +227,19 @@ void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank,
                            uint64_t* seqs, float scale, unsigned* err, long long timeout_ticks,
                            const XgmiPostOpt* post, hipStream_t st, int fault = 0);
 // The fused bf16 LeNet data-parallel step's view of the transport (lenet_mfma.hip, lenet_mwx):
-// the batch-reduction kernel's block b publishes the gradient elements it produced into its own
-// rank's data region (parity p of step seq) and flags[q][(p * G + b) * W + rank] on every peer q,
-// waits for all W flags of (p, b), sums those elements over the W regions in rank order and applies
-// the update in the same launch. W = 1 is the loopback (the peer is this rank itself).
+// every gradient element the batch-reduction kernel produces is published as an 8-byte granule
+// {fp32 value, low 32 bits of the block's launch counter} into its rank's granule array (parity
+// p = seq & 1), written and read with single 8-byte system-scope accesses; a consumer lane polls the
+// W - 1 peers' granules of ITS elements until their tags match, sums in rank order and applies the
+// update in the same launch -- no flags, no barriers, one round trip. W = 1 is the loopback.
 struct XgmiFused {
-  float* data[kXgmiMaxRanks];      // per-rank [2][cap] fp32 (indexed by flat parameter offset)
-  uint64_t* flags[kXgmiMaxRanks];  // per-rank [2][G][W]
+  uint64_t* gran[kXgmiMaxRanks];   // per-rank [2][cap] granules (indexed by flat parameter offset)
   uint64_t* seqs;                  // [G] per-block launch counters (this rank)
   unsigned* err;                   // sticky error word (host-mapped: the host polls it)
-  unsigned* derr;                  // its device copy (uncached region memory: what the kernel reads)
+  unsigned* derr;                  // its device copy (what the kernel reads)
   int64_t cap;
   long long timeout;               // ticks of the 100 MHz constant clock
   int rank, W, G, fault;
-  // protocol (A/B knob MLT_XGMI_PROTO): bit 0 = release / acquire fences around plain payload
-  // accesses (else system-scope sc0 sc1 payload and flag accesses, no fences); bit 1 = read the
-  // host-mapped error word at block start (else the device copy)
-  int proto;
 };
 // two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,

@@ -1010,143 +1010,104 @@ __device__ __forceinline__ void upd1(const LeNetOpt& O, const Ctx& c, uint16_t* 
 
 // Data-parallel exchange inside the batch-reduction kernel (struct XgmiFused, WT ranks; WT = 0: off).
 // Every gradient element is produced by exactly one lane of one block, the same lane and block on
-// every rank, so block b's elements form its slice: the lane puts them into its rank's region at
-// their flat offsets (parity p of this launch), the block publishes (p, b) to every peer, waits for
-// all WT peers, and the lane sums its elements over the WT regions in rank order (the same order on
-// every rank: bit-identical replicas) before the update. Producer: payload stores -> every wave's
-// vmcnt(0) -> workgroup barrier -> one system-scope release store per peer flag. Consumer: relaxed
-// system-scope polls of the own flag row -> one system acquire fence (+ its vmcnt wait) ->
-// workgroup barrier -> plain loads. Parity reuse is safe as in allreduce.hip: a rank reaches launch
-// s + 2 (parity p again) only after every peer published s + 1, which each peer does only after its
-// launch s -- including the reads of parity p -- retired.
-// Failure: the sticky error word (read at block start, checked before publishing) stops this rank
-// from publishing anything once any launch timed out, so every peer times out too; a timed-out block
-// applies nothing. Blocks that did see all peers apply their slices (the job stops with
-// TransportError; resume restores identical replicas from the checkpoint).
+// every rank. The lane publishes each of its elements as one 8-byte granule {fp32 value, tag = low
+// 32 bits of the block's launch counter} into its rank's granule array (parity p of this launch) with
+// a single system-scope store (global_store sc0 sc1: written through, single-copy atomic -- value and
+// tag arrive together), then polls the WT - 1 peers' granules of the same elements with system-scope
+// loads until every tag matches, and sums in rank order (its own value from registers; the same
+// order on every rank: bit-identical replicas) before the update. No flags, no fences, no barriers:
+// the data is its own flag, so the exchange costs one store and one (remote) load round trip per
+// lane instead of store -> drain -> barrier -> flag -> poll -> barrier -> load. Parity reuse is safe
+// as in allreduce.hip: a rank reaches launch s + 2 (parity p again) only after it read every peer's
+// launch s + 1 granules, which a peer writes only after its launch s -- including its reads of parity
+// p -- retired. W = 1 (loopback) polls its own granules back, so the loopback pays the round trip a
+// peer would.
+// Failure: the sticky error word (device copy, read once per wave at launch start) stops this rank
+// from publishing anything once any launch timed out, so every peer times out too; a lane whose
+// poll timed out applies nothing (the job stops with TransportError; resume restores identical
+// replicas from the checkpoint).
 template <int WT>
 struct Xch {
   static constexpr bool on = WT > 0;
-  const XgmiFused* X;
-  int* failed;  // __shared__
-  int blk, p;
-  uint64_t seq;
-  unsigned errv;
+  // (plain copies: a dynamically indexed kernel-argument array would be spilled to scratch)
+  uint64_t* gr[WT > 0 ? WT : 1];  // this launch's parity half of every rank's granule array
+  uint64_t* mine;
+  unsigned* err;
+  unsigned* derr;
+  long long timeout;
+  int rank;
+  unsigned tag;
+  bool dead;      // wave-uniform
+  bool withhold;  // fault injection (tests)
   float scale;
 
-  // payload accesses: with X->proto bit 0 plain (ordered by the release / acquire fences of sync),
-  // else system-scope relaxed atomics (global_load / store sc0 sc1: nothing of them stays in a
-  // cache of either GPU), 8 bytes each
-  __device__ __forceinline__ float* mine() const { return X->data[X->rank] + p * X->cap; }
-  __device__ __forceinline__ bool fenced() const { return (X->proto & 1) != 0; }
-  __device__ __forceinline__ void st2(float* a, float x, float y) const {
-    if (fenced()) {
-      *reinterpret_cast<float2*>(a) = make_float2(x, y);
-    } else {
-      const uint64_t v = (uint64_t)__float_as_uint(x) | ((uint64_t)__float_as_uint(y) << 32);
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(a), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+  __device__ __forceinline__ void st(int64_t i, float v) const {
+    const uint64_t g = (uint64_t)__float_as_uint(v) | ((uint64_t)tag << 32);
+    __hip_atomic_store(mine + i, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __device__ __forceinline__ float2 ld2(const float* a) const {
-    if (fenced()) return *reinterpret_cast<const float2*>(a);
-    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
-  }
-  __device__ __forceinline__ float ld1(const float* a) const {
-    if (fenced()) return *a;
-    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  __device__ __forceinline__ uint64_t ld(int q, int64_t i) const {
+    return __hip_atomic_load(gr[q] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __device__ __forceinline__ void put1(int64_t i, float v) const {
-    if (fenced()) {
-      mine()[i] = v;
-    } else {
-      __hip_atomic_store(reinterpret_cast<unsigned*>(mine() + i), __float_as_uint(v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (!dead && !withhold) st(i, v);
   }
   __device__ __forceinline__ void put4(int64_t i, float4 v) const {
-    st2(mine() + i, v.x, v.y);
-    st2(mine() + i + 2, v.z, v.w);
+    if (!dead && !withhold) {
+      st(i, v.x);
+      st(i + 1, v.y);
+      st(i + 2, v.z);
+      st(i + 3, v.w);
+    }
   }
-  // all threads of the block, once: every storing wave drains its payload stores (vmcnt(0)), the
-  // workgroup barrier, one flag store per peer (a release store in the fenced protocol), the polls
-  // of the own flag row (relaxed system loads; the fenced protocol adds one acquire fence after)
-  __device__ __forceinline__ bool sync() const {
-    const int t = threadIdx.x;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
-    __syncthreads();
-    if (t < 64) {
-      const bool dead = __builtin_amdgcn_readfirstlane(errv) != 0u;  // lane 0's value
-      const bool withhold = X->fault == 1 && blk % (2 * WT) == X->rank;  // fault injection (tests)
-      if (t < WT) {
-        if (dead) {
-          *failed = 1;
-        } else {
-          if (!withhold) {
-            uint64_t* f = X->flags[t] + ((int64_t)p * X->G + blk) * WT + X->rank;
-            if (fenced())
-              __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            else
-              __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-          const uint64_t* f = X->flags[X->rank] + ((int64_t)p * X->G + blk) * WT + t;
-          const long long t0 = wall_clock64();
-          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-            if (wall_clock64() - t0 > X->timeout) {  // 100 MHz constant clock
-              __hip_atomic_fetch_or(X->derr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_fetch_or(X->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              *failed = 1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
+  static constexpr bool peer(int q, int rank) { return WT == 1 || q != rank; }
+  // N consecutive elements at i: every peer's granules, polled until all tags match (false: timed
+  // out -- the error words are set), summed in rank order with own[] in this rank's position, scaled;
+  // opaque to the compiler so that the optimizer's arithmetic cannot contract with the sum (bitwise
+  // equal to all-reduce -> separate update launch)
+  template <int N>
+  __device__ __forceinline__ bool get(int64_t i, const float* own, float* out) const {
+    if (dead) return false;
+    uint64_t g[WT][N];
+#pragma unroll
+    for (int q = 0; q < WT; ++q)
+#pragma unroll
+      for (int e = 0; e < N; ++e) g[q][e] = peer(q, rank) ? ld(q, i + e) : (uint64_t)tag << 32;
+    long long t0 = -1;
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int q = 0; q < WT; ++q)
+#pragma unroll
+        for (int e = 0; e < N; ++e) ready &= (unsigned)(g[q][e] >> 32) == tag;
+      if (ready) break;
+      const long long now = wall_clock64();  // 100 MHz constant clock
+      if (t0 < 0) {
+        t0 = now;
+      } else if (now - t0 > timeout) {
+        __hip_atomic_fetch_or(derr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
       }
-      if (fenced()) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: this CU's caches see the peers' stores
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int q = 0; q < WT; ++q)
+#pragma unroll
+        for (int e = 0; e < N; ++e)
+          if (peer(q, rank) && (unsigned)(g[q][e] >> 32) != tag) g[q][e] = ld(q, i + e);
+    }
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < WT; ++q) {
+        const float v = peer(q, rank) ? __uint_as_float((unsigned)g[q][e]) : own[e];
+        s = q == 0 ? v : s + v;
       }
+      s *= scale;
+      asm volatile("" : "+v"(s));
+      out[e] = s;
     }
-    __syncthreads();
-    const bool ok = *failed == 0;
-    if (ok && t == 0) X->seqs[blk] = seq;  // read again only by the next launch (stream order)
-    return ok;
-  }
-  // the sum over the ranks, in rank order, scaled; opaque to the compiler so that the optimizer's
-  // arithmetic cannot contract with it (bitwise equal to all-reduce -> separate update launch)
-  __device__ __forceinline__ float get1(int64_t i) const {
-    float v[WT];
-#pragma unroll
-    for (int q = 0; q < WT; ++q) v[q] = ld1(X->data[q] + p * X->cap + i);
-    __builtin_amdgcn_sched_barrier(0);
-    float s = v[0];
-#pragma unroll
-    for (int q = 1; q < WT; ++q) s += v[q];
-    s *= scale;
-    asm volatile("" : "+v"(s));
-    return s;
-  }
-  __device__ __forceinline__ float4 get4(int64_t i) const {
-    float2 lo[WT], hi[WT];
-#pragma unroll
-    for (int q = 0; q < WT; ++q) {
-      lo[q] = ld2(X->data[q] + p * X->cap + i);
-      hi[q] = ld2(X->data[q] + p * X->cap + i + 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    float4 s = make_float4(lo[0].x, lo[0].y, hi[0].x, hi[0].y);
-#pragma unroll
-    for (int q = 1; q < WT; ++q) {
-      s.x += lo[q].x;
-      s.y += lo[q].y;
-      s.z += hi[q].x;
-      s.w += hi[q].y;
-    }
-    s.x *= scale;
-    s.y *= scale;
-    s.z *= scale;
-    s.w *= scale;
-    asm volatile("" : "+v"(s.x), "+v"(s.y), "+v"(s.z), "+v"(s.w));
-    return s;
+    return true;
   }
 };
 
@@ -1218,11 +1179,18 @@ __device__ __forceinline__ void fc_wgrad(const Xch<WT>& xc, int tile, int B, con
   float4 gv = make_float4(acc[0], acc[1], acc[2], acc[3]);
   float gb = acc[0];
   if constexpr (Xch<WT>::on) {  // data-parallel: this lane's elements summed over the ranks
-    if (wrow) xc.put4(iw, gv);
-    if (brow) xc.put1(ib, gb);
-    if (!xc.sync()) return;
-    if (wrow) gv = xc.get4(iw);
-    if (brow) gb = xc.get1(ib);
+    if (wrow) {
+      xc.put4(iw, gv);
+      float o[4] = {gv.x, gv.y, gv.z, gv.w}, r[4];
+      if (!xc.template get<4>(iw, o, r)) return;
+      gv = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    if (brow) {
+      xc.put1(ib, gb);
+      float r;
+      if (!xc.template get<1>(ib, &gb, &r)) return;
+      gb = r;
+    }
   }
   if (wrow) {
     *reinterpret_cast<float4*>(O.g + iw) = gv;
@@ -1269,9 +1237,7 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
   if (blk < NBC) {
     const int e = blk * kWgT + t;
     const bool act = e < D::S1 + D::S2;
-    if constexpr (!Xch<WT>::on) {
-      if (!act) return;
-    }
+    if (!act) return;
     int soff = 0;
     int64_t dst = 0;
     if (!act) {
@@ -1299,9 +1265,11 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
       for (int u = 0; u < 32; ++u) gsum += b0 + u < B ? v[u] : 0.f;
     }
     if constexpr (Xch<WT>::on) {  // data-parallel: summed over the ranks
-      if (act) xc.put1(dst, gsum);
-      if (!xc.sync() || !act) return;
-      gsum = xc.get1(dst);
+      if (!act) return;
+      xc.put1(dst, gsum);
+      float r;
+      if (!xc.template get<1>(dst, &gsum, &r)) return;
+      gsum = r;
     }
     O.g[dst] = gsum;
     if (c.on) {
@@ -1344,8 +1312,6 @@ __device__ __forceinline__ void mw_body(int mode, const LeNetPtrs& P, const LeNe
     } else if ((wv -= NW4) < NW5) {
       fc_wgrad<F2, NC, WT, K>(xc, wv, B, P.dlogits, P.h2, O, c, shadow, O.off[8], O.off[9],
                        P.wimg ? P.wimg + kFc3T : nullptr, Fc<D>::P3T, P.wimg ? P.wimg + kFc3F : nullptr, Fc<D>::P3F);
-    } else if constexpr (Xch<WT>::on) {
-      xc.sync();  // a wave without a tile still joins its block's exchange barriers
     }
   } else {
     // loss / accuracy of the step in sample order (fixed tree): bitwise reproducible epoch stats.
@@ -1424,20 +1390,27 @@ __global__ __launch_bounds__(kWgT) void lenet_mwx(const float* __restrict__ psla
                                                   const float* __restrict__ pdh1, const float* __restrict__ ph1,
                                                   const float* __restrict__ pdh2, int mode, int B, LeNetPtrs P,
                                                   LeNetOpt O, int64_t* __restrict__ ctrl, XgmiFused X) {
-  __shared__ int failed;
   Xch<WT> xc;
-  xc.X = &X;
-  xc.failed = &failed;
-  xc.blk = blockIdx.x;
-  xc.errv = 0u;
-  if (threadIdx.x == 0) {
-    failed = 0;
-    // in flight during the reduction; checked before this block publishes anything (the device copy
-    // in the region: a local read, not a PCIe round trip to the host-mapped word)
-    xc.errv = __hip_atomic_load((X.proto & 2) ? X.err : X.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // per-block launch counter: identical on every block and rank; read again only by the next launch
+  const uint64_t seq = X.seqs[blockIdx.x] + 1;
+  if (threadIdx.x == 0) X.seqs[blockIdx.x] = seq;
+  xc.tag = (unsigned)seq;
+  const int64_t half = (int64_t)(seq & 1) * X.cap;
+  xc.mine = X.gran[0] + half;
+#pragma unroll
+  for (int q = 0; q < WT; ++q) {
+    xc.gr[q] = X.gran[q] + half;
+    if (q == X.rank) xc.mine = xc.gr[q];
   }
-  xc.seq = X.seqs[blockIdx.x] + 1;  // per-block launch counter: identical on every block and rank
-  xc.p = (int)(xc.seq & 1);
+  xc.err = X.err;
+  xc.derr = X.derr;
+  xc.timeout = X.timeout;
+  xc.rank = X.rank;
+  xc.withhold = X.fault == 1 && (int)(blockIdx.x % (2 * WT)) == X.rank;
+  // the device copy of the sticky error word (a local read, not a PCIe round trip to the host-mapped
+  // word), once per wave: in flight during the batch reduction
+  xc.dead = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(X.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
   xc.scale = 1.f / (float)WT;
   mw_dispatch<D, WT>(mode, with_first(P, pslab1, pp2, pdh1, ph1, pdh2), O, B, ctrl, xc);
 }
@@ -1548,7 +1521,7 @@ template <class D>
 void run_dp(int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O, const XgmiFused& X,
             hipStream_t st) {
   const int nblk = mw_conv_blocks<D>() + mw_fc_blocks<D>() + 1;
-  if (X.G < nblk) throw std::runtime_error("lenet dp step: transport flag rows < reduction blocks");
+  if (X.G < nblk) throw std::runtime_error("lenet dp step: transport block counters < reduction blocks");
   if (X.cap < O.n) throw std::runtime_error("lenet dp step: transport region smaller than the parameters");
   mode |= probe_bits();
   const float inv_B = 1.f / (float)B;
