@@ -21,6 +21,7 @@ p.add_argument("--a_mn", type=int, default=0)
 p.add_argument("--b_mn", type=int, default=0)
 p.add_argument("--cfgs", default="1,5")
 p.add_argument("--reps", type=int, default=5)
+p.add_argument("--torch", type=int, default=0, help="also run torch.matmul (hipBLASLt) this many times")
 a = p.parse_args()
 C = require_native()
 dev = torch.device("cuda", 0)
@@ -30,5 +31,9 @@ out = torch.empty(a.M, a.N, dtype=torch.bfloat16, device=dev)
 for cfg in [int(c) for c in a.cfgs.split(",")]:
     for _ in range(a.reps):
         C.gemm(A, B, out, bool(a.a_mn), bool(a.b_mn), cfg=cfg)
+At = A.t() if a.a_mn else A
+Bt = B if a.b_mn else B.t()
+for _ in range(a.torch):
+    torch.matmul(At, Bt, out=out)
 torch.cuda.synchronize()
 print("done")

@@ -102,4 +102,12 @@ template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
 void launch_gemm_persist(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                          int64_t ldc, const GemmEpi& e, int group_m, int max_blocks, hipStream_t st);
 
+// gemm_w4.hip (planner cfg 7): 4-wave 256x256x64 tile, generated-asm main loop, k-contiguous A,
+// B k-contiguous or (b_mn) n-contiguous
+bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes, const GemmEpi& e,
+                       bool b_mn);
+template <typename OutT>
+void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                    int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st);
+
 }  // namespace mlt

@@ -806,7 +806,7 @@ struct CfgDesc {
   int per_cu;    // resident blocks per CU
   double fixed;  // per-block fixed cost (prologue fill + epilogue), s
 };
-constexpr int kNumCfg = 7;
+constexpr int kNumCfg = 8;
 // cfg 5 (ping-pong) fitted to the 64K-token BERT shapes (profiles/gemm_bf16_64k_tokens.jsonl):
 // 8-10 % faster than cfg 1 at K = 2304-3072; since the 16-byte-store epilogue also 3-8 % faster
 // at K = 768 (profiles/gemm_epi16_64k_tokens.jsonl) -> a faster steady state, a small extra
@@ -817,7 +817,8 @@ const CfgDesc kCfg[kNumCfg] = {{128, 128, 0.62e15 / kCUs, 2, 1.0e-6},
                                {128, 256, 0.92e15 / kCUs, 1, 1.0e-6},
                                {256, 192, 1.05e15 / kCUs, 1, 1.0e-6},
                                {256, 256, 1.335e15 / kCUs, 1, 2.5e-6},   // 5: ping-pong
-                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6}};  // 6: persistent ping-pong (fill once)
+                               {256, 256, 1.335e15 / kCUs, 1, 5.6e-6},   // 6: persistent ping-pong (fill once)
+                               {256, 256, 1.335e15 / kCUs, 1, 2.5e-6}};  // 7: 4-wave asm main loop (gemm_w4.hip)
 
 // split-K combine override: -1 planner, 0 in-kernel, 1 external (env MLT_GEMM_SPLIT_EXT, or
 // set_gemm_split_mode() from tests / benchmarks)
@@ -875,7 +876,7 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
   if (force_cfg >= 0) {
     best_cfg = (force_cfg >= 1 && force_cfg < kNumCfg && big_ok) ? force_cfg : 0;
     if (best_cfg == 6 && !allow_persist) best_cfg = 1;
-    best_s = best_cfg ? (force_splits > 0 && best_cfg != 6 ? force_splits : 1) : 1;
+    best_s = best_cfg ? (force_splits > 0 && best_cfg < 6 ? force_splits : 1) : 1;
   } else if (big_ok) {
     double best = allow_legacy ? est_time(0, 1, M, N, K, 64, 1.0) : 1e30;
     const int nk = K / kstep;
@@ -886,7 +887,7 @@ GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int ks
         // shapes while the tile kernels stored 8 bytes per lane; with their 16-byte-store
         // epilogue the ping-pong tile beats it by 13-20 % there (profiles/gemm_epi16_64k_tokens.jsonl,
         // profiles/fp8_cfg_large_131k_tokens.jsonl), and at K >= 3072 it already lost by 8-11 %.
-        if (cfg == 6) break;
+        if (cfg >= 6) break;
         if (s > nk) break;
         const int ks = (nk + s - 1) / s;
         if ((int64_t)ks * (s - 1) >= nk) continue;  // no empty split
@@ -1007,6 +1008,20 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
       }
       launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
       break;
+    case 7:
+      // 4-wave asm main loop (gemm_w4.hip): bf16, k-contiguous A, full 256 tiles
+      if constexpr (!AM && F8A < 0 && (sizeof(OutT) == 2 || sizeof(OutT) == 4)) {
+        if (p.splits == 1 && gemm_w4_supported(M, N, K, lda, ldb, ldc, (int)sizeof(OutT), e, BNL)) {
+          static const int group_m = [] {
+            const char* v = getenv("MLT_GEMM_GROUP_M");
+            return v ? atoi(v) : kGroupM;
+          }();
+          launch_gemm_w4<OutT>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, BNL, st);
+          break;
+        }
+      }
+      launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
+      break;
     default: break;
   }
 }
@@ -1042,6 +1057,18 @@ void set_gemm_split_mode(int mode) { g_split_mode = mode; }
 
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
   (void)b_mn;
+  // the 4-wave asm kernel (cfg 7) takes every k-contiguous-A (forward / input-gradient) shape it
+  // covers: 3-17 % over the ping-pong tile on the BERT forward shapes, 98-101 % of hipBLASLt at
+  // 4096^3 / 8192^3 (profiles/r4/gemm_w4_*.jsonl). MLT_GEMM_W4=0 restores the fitted planner.
+  static const bool w4 = [] {
+    const char* v = getenv("MLT_GEMM_W4");
+    return !(v && atoi(v) == 0);
+  }();
+  if (w4 && force_cfg < 0 && force_splits <= 0 && a_mn == 0 && M % 256 == 0 && N % 256 == 0 && K % 128 == 0 &&
+      K >= 256) {
+    GemmPlan p{7, 1, K / 64, 0, 0};
+    return p;
+  }
   // the ping-pong kernel's fit covers the k-contiguous-A (forward / dgrad) shapes; weight
   // gradients (A = dY^T, mn-contiguous) stay on the 256-wide tiles with split-K
   return plan_tiles(M, N, K, force_cfg, force_splits, 64, true, a_mn == 0, a_mn == 0);

@@ -1,0 +1,261 @@
+// 4-wave 256x256x64 bf16 GEMM for gfx950 (planner cfg 7): C = A . B^T with A [M][K] k-contiguous and
+// B [N][K] (forward layout of a linear layer) or B [K][N] (b_mn: the input-gradient layout, read
+// through ds_read_b64_tr_b16), one output tile per 256-thread workgroup, ONE wave per SIMD holding
+// a 128 x 128 wave tile in 256 AGPR accumulators.
+//
+// Why this shape (rocprofv3 --pmc on the box, profiles/r4/gemm_pmc_*.jsonl): at 8192^3 hipBLASLt's
+// MT256x256x64 kernel runs 4 waves per workgroup and keeps the matrix cores busy 87.5 % of the
+// cycles (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 4 SIMDs)), while the 8-wave ping-pong
+// kernel (gemm_tile.hip, cfg 5: 2 waves per SIMD, 128 x 64 wave tiles, two barriers per 16-MFMA
+// phase) reaches 67 % -- its waves sit parked at barriers / waitcnts 26 % of their cycles. A 128 x
+// 128 wave tile reads 64 FLOP per LDS byte (43 for 128 x 64), and with one barrier per K-tile
+// (2,048 MFMA cycles per SIMD) the fill / drain of the barrier is amortised over 128 MFMAs.
+//
+// The main loop is generated asm (scripts/gen_gemm_w4.py -> gemm_w4_loop.inc): fixed fragment
+// registers v[0:127], accumulators a[0:255], DMA source pointers s[88:91]; fragment reads one per
+// MFMA gap of a phase's first half, the LDS-DMA pieces one per 4 MFMAs over the second phase, the
+// first K-tile's MFMAs start from C = 0. This file computes the per-lane addresses, runs the loop
+// and applies the fused epilogue from the accumulators through a per-wave LDS image (16-byte row
+// stores). MFMA operands are swapped (D = B_tile . A_tile^T): a lane holds 4 columns of one row.
+// Requirements (host-checked, else the caller falls back): M, N multiples of 256, K a multiple of
+// 128 and >= 256, 16-byte aligned rows, no split-K / accumulate / fp8 scales.
+#include "mlt_common.h"
+#include "mlt_gemm.h"
+#include "mlt_gemm_tile.h"
+#include "gemm_w4_loop.inc"
+
+namespace mlt {
+
+enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// LDS: two K-tile stages of 64 KB; after the loop, four per-wave 64 x 132 fp32 epilogue images
+__device__ __forceinline__ uint32_t pack2(uint16_t lo, uint16_t hi) { return (uint32_t)lo | ((uint32_t)hi << 16); }
+constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 * kW4Pitch * 4 : 131072;
+
+template <typename OutT, int EK, bool BN>
+__device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                             OutT* __restrict__ C, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                             const GemmEpi& epi, int id, int gm_, int tiles_m, int tiles_n,
+                                             uint8_t* smem) {
+  const int per_group = gm_ * tiles_n, grp = id / per_group, first_m = grp * gm_;
+  const int gsize = min(tiles_m - first_m, gm_), rr = id - grp * per_group;
+  const int m0 = (first_m + rr % gsize) * 256, n0 = (rr / gsize) * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_u8*)smem;
+
+  // fragment reads: lane (g, rl) of a 16-row block reads row rl, 16-B chunk kh*4 + g, stored at
+  // chunk ^ ((row >> 1) & 7) (rows 128 B apart; the XOR spreads a 16-lane group over all 64 banks)
+  const int g = lane >> 4, rl = lane & 15, sw = (rl >> 1) & 7;
+  auto raddr = [&](int stage, int isb, int kh) {
+    const int row = (isb ? wc : wr) * 128 + rl;
+    return lds0 + stage * 65536 + isb * 32768 + row * 128 + (((kh * 4 + g) ^ sw) << 4);
+  };
+  const uint32_t ra00 = raddr(0, 0, 0), ra01 = raddr(0, 0, 1), ra10 = raddr(1, 0, 0), ra11 = raddr(1, 0, 1);
+  const uint32_t rb00 = raddr(0, 1, 0), rb01 = raddr(0, 1, 1), rb10 = raddr(1, 1, 0), rb11 = raddr(1, 1, 1);
+  // DMA sources: wave w's p-th piece fills LDS rows (4p + w) * 8 .. + 7 (1 KB, lane-linear); lane
+  // L fetches row + (L >> 3), the global chunk that lands on position L & 7 under the swizzle
+  uint32_t ga[8], gb[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int r = (p * 4 + w) * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    ga[p] = (uint32_t)((r * lda + kc * 8) * 2);
+    if constexpr (!BN) {
+      gb[p] = (uint32_t)((r * ldb + kc * 8) * 2);
+    } else {  // B image [64 k][256 n]: 32 chunks per 512-B k-row, chunk ^ (2 (k & 3) + 8 ((k >> 3) & 1))
+      const int e = (p * 4 + w) * 64 + lane, kk = e >> 5;
+      const int c = (e & 31) ^ (((kk & 3) << 1) | (((kk >> 3) & 1) << 3));
+      gb[p] = (uint32_t)((kk * ldb + c * 8) * 2);
+    }
+  }
+  const uint64_t sa = (uint64_t)(uintptr_t)(A + (int64_t)m0 * lda * 2);
+  const uint32_t lw = __builtin_amdgcn_readfirstlane(lds0 + w * 1024);
+  int np = (K >> 7) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
+  if constexpr (!BN) {
+    const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * ldb * 2);
+    asm volatile(MLT_W4_LOOP_ASM
+                 : [np] "+s"(np)
+                 : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [ra00] "v"(ra00), [ra01] "v"(ra01), [ra10] "v"(ra10),
+                   [ra11] "v"(ra11), [rb00] "v"(rb00), [rb01] "v"(rb01), [rb10] "v"(rb10), [rb11] "v"(rb11),
+                   [ga0] "v"(ga[0]), [ga1] "v"(ga[1]), [ga2] "v"(ga[2]), [ga3] "v"(ga[3]), [ga4] "v"(ga[4]),
+                   [ga5] "v"(ga[5]), [ga6] "v"(ga[6]), [ga7] "v"(ga[7]), [gb0] "v"(gb[0]), [gb1] "v"(gb[1]),
+                   [gb2] "v"(gb[2]), [gb3] "v"(gb[3]), [gb4] "v"(gb[4]), [gb5] "v"(gb[5]), [gb6] "v"(gb[6]),
+                   [gb7] "v"(gb[7])
+                 : MLT_W4_CLOBBERS, "memory");
+  } else {
+    // transposed B fragment reads (as gemm_tile's tfrag_mn): lane (g, q = rl >> 2, p = rl & 3) reads
+    // k-rows kh*32 + 8g + q (+ 4) at column wc*128 + 16 j + 4p; with the swizzle the byte address is
+    // R + (32 j ^ X), R = row + column-pair + half, X = 16 * (2q + 8 (g & 1)) -- built in the asm
+    const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * 2);
+    const uint32_t bstep = (uint32_t)(64 * ldb * 2);
+    const int q = rl >> 2, pp = rl & 3;
+    const uint32_t rbr = lds0 + (8 * g + q) * 512 + wc * 256 + 16 * (pp >> 1) + 8 * (pp & 1);
+    const uint32_t rbx = (uint32_t)(32 * q + 128 * (g & 1));
+    asm volatile(MLT_W4_LOOP_ASM_BN
+                 : [np] "+s"(np)
+                 : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [bstep] "s"(bstep), [ra00] "v"(ra00), [ra01] "v"(ra01),
+                   [ra10] "v"(ra10), [ra11] "v"(ra11), [rbr] "v"(rbr), [rbx] "v"(rbx), [ga0] "v"(ga[0]),
+                   [ga1] "v"(ga[1]), [ga2] "v"(ga[2]), [ga3] "v"(ga[3]), [ga4] "v"(ga[4]), [ga5] "v"(ga[5]),
+                   [ga6] "v"(ga[6]), [ga7] "v"(ga[7]), [gb0] "v"(gb[0]), [gb1] "v"(gb[1]), [gb2] "v"(gb[2]),
+                   [gb3] "v"(gb[3]), [gb4] "v"(gb[4]), [gb5] "v"(gb[5]), [gb6] "v"(gb[6]), [gb7] "v"(gb[7])
+                 : MLT_W4_CLOBBERS_BN, "memory");
+  }
+
+  // ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct
+  // stores would be 64 x 8 bytes per lane in 32-byte row pieces (store-issue bound). Each wave
+  // instead writes its 128 x 128 fp32 tile to its own LDS image in two 64-row halves (pitch 132
+  // floats: the 16 rows of a fragment write land 4 banks apart) and reads it back as 8 consecutive
+  // columns per lane: 32 x 16-byte stores per lane (bf16), side operands as 16-byte loads.
+  __syncthreads();  // every wave is past its last read of the K-tile stages
+  constexpr int P = kW4Pitch;
+  float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
+  const float alpha = epi.alpha;
+  const int rsub = lane >> 4, cc = lane & 15;  // read side: row 4 * it + rsub, columns 8 cc .. + 7
+  const int gn = n0 + wc * 128 + 8 * cc;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+  if (epi.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(epi.bias + gn);
+    const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
+    bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x0, x1, x2, x3;
+        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
+        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
+    uint4 sd[16];
+    if constexpr (EK == W4_RES || EK == W4_DGELU) {  // the half's side operands first, then the stores
+      const uint16_t* sx = EK == W4_RES ? epi.res : epi.aux;
+      const int64_t ldx = EK == W4_RES ? epi.ldres : epi.ldaux;
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
+        sd[it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
+      const float4 lo = *reinterpret_cast<const float4*>(img + row * P + 8 * cc);
+      const float4 hi = *reinterpret_cast<const float4*>(img + row * P + 8 * cc + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
+      if constexpr (EK == W4_GELU) {  // keep the (bf16-rounded) pre-activation for the backward
+        uint16_t a[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[e] = f32_to_bf16(v[e]);
+          v[e] = gelu_f(bf16_to_f32(a[e]));
+        }
+        *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
+            make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
+      } else if constexpr (EK == W4_RES || EK == W4_DGELU) {
+        const uint32_t sw4[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
+          if constexpr (EK == W4_RES)
+            v[e] += x;
+          else
+            v[e] *= gelu_grad(x);
+        }
+      }
+      OutT* cp = C + (int64_t)gm * ldc + gn;
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        *reinterpret_cast<uint4*>(cp) =
+            make_uint4(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), f32_to_bf16(v[3])),
+                       pack2(f32_to_bf16(v[4]), f32_to_bf16(v[5])), pack2(f32_to_bf16(v[6]), f32_to_bf16(v[7])));
+      }
+    }
+    if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
+  }
+}
+
+// One tile per workgroup. (A persistent variant -- one workgroup per CU walking id, id + 256, ...,
+// the next tile's DMAs issued behind the previous epilogue's stores -- measured slower on the K =
+// 768 shapes and at 8192^3: 950 vs 988 TF (QKV), 1,531 vs 1,618 TF; with one workgroup per tile
+// the dispatcher plus the XCD remap keeps each XCD on one contiguous run of tile ids.)
+template <typename OutT, int EK, bool BN>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                         OutT* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                         int64_t ldb, int64_t ldc, GemmEpi epi, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tiles_m = M >> 8, tiles_n = N >> 8;
+  const int gm_ = group_m > 0 ? group_m : tiles_m;
+  gemm_w4_tile<OutT, EK, BN>(A, B, C, K, lda, ldb, ldc, epi, xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
+}
+
+template <typename OutT, int EK, bool BN>
+static void launch_w4_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+  constexpr int SMEM = kW4Smem;
+  auto kern = gemm_w4_kernel<OutT, EK, BN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  const int tiles = (M / 256) * (N / 256);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, group_m);
+}
+
+bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes, const GemmEpi& e,
+                       bool b_mn) {
+  auto al = [](const void* p, int64_t ld, int esz) {
+    return p == nullptr || ((((uintptr_t)p) % 16) == 0 && (ld * esz) % 16 == 0);
+  };
+  if (M % 256 || N % 256 || K % 128 || K < 256) return false;
+  if ((lda * 2) % 16 || (ldb * 2) % 16 || (ldc * out_bytes) % 16) return false;
+  if (lda * 2 * 256 > (int64_t)1 << 31 || ldb * 2 * 256 > (int64_t)1 << 31) return false;  // 32-bit DMA offsets
+  if (b_mn && (N % 8 || ldb < N)) return false;
+  if (e.accumulate || e.inv_scale_a || e.inv_scale_b || e.q_colpart || e.qt || e.mode == 3) return false;
+  if (!al(e.res, e.ldres, 2) || !al(e.aux, e.ldaux, 2) || (e.bias && ((uintptr_t)e.bias) % 16)) return false;
+  if (out_bytes == 4 && (e.mode != 0 || e.res)) return false;
+  if (e.mode != 0 && e.res) return false;
+  return true;
+}
+
+template <typename OutT, bool BN>
+static void launch_w4_bn(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+  if (e.mode == 1)
+    launch_w4_ek<OutT, W4_GELU, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else if (e.mode == 2)
+    launch_w4_ek<OutT, W4_DGELU, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else if (e.res)
+    launch_w4_ek<OutT, W4_RES, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else
+    launch_w4_ek<OutT, W4_PLAIN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+}
+
+template <typename OutT>
+void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                    int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st) {
+  if (b_mn)
+    launch_w4_bn<OutT, true>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else
+    launch_w4_bn<OutT, false>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+}
+
+template void launch_gemm_w4<uint16_t>(const uint8_t*, const uint8_t*, uint16_t*, int, int, int, int64_t, int64_t,
+                                       int64_t, const GemmEpi&, int, bool, hipStream_t);
+template void launch_gemm_w4<float>(const uint8_t*, const uint8_t*, float*, int, int, int, int64_t, int64_t, int64_t,
+                                    const GemmEpi&, int, bool, hipStream_t);
+
+}  // namespace mlt

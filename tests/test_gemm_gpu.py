@@ -289,3 +289,63 @@ def test_dgelu_colsum_fused(dev, b_mn, M, N, K):
     torch.testing.assert_close(cs, 2 * ref.sum(0), rtol=1e-3, atol=2e-4 * scale)
     with pytest.raises(RuntimeError):  # edge tiles cannot fuse the sums
         C.gemm(A[:M - 8], B, out[:M - 8], False, bool(b_mn), aux=aux[:M - 8], mode=2, colsum_out=cs)
+
+
+@pytest.mark.parametrize("b_mn", [0, 1])
+def test_w4_asm_kernel(dev, b_mn):
+    """Config 7 (4-wave 256x256x64 tile, generated-asm main loop, AGPR accumulators, LDS-staged
+    epilogue; B k-contiguous or n-contiguous through transposed LDS reads): every epilogue, bf16 and
+    fp32 outputs, a strided A (and B), more tiles than CUs; a shape outside its domain (N tail) falls
+    back to the ping-pong kernel."""
+    C = require_native()
+    M, N, K = 4096, 2304, 768  # 16 x 9 = 144 tiles, 6 K-tile pairs
+    g = torch.Generator().manual_seed(71 + b_mn)
+    A = _mk((M, K + 64), dev, g)[:, :K]
+    B = _mk((K, N + 128), dev, g)[:, :N] if b_mn else _mk((N, K), dev, g)
+    ref = _ref(A, B, 0, b_mn)
+    assert C.gemm_plan(False, bool(b_mn), M, N, K)[0] == 7
+    for out_dtype in (torch.bfloat16, torch.float32):
+        out = torch.empty(M, N, dtype=out_dtype, device=dev)
+        C.gemm(A, B, out, False, bool(b_mn), cfg=7)
+        tol = 2e-2 if out_dtype == torch.bfloat16 else 2e-3
+        torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * 8)
+    bias = torch.randn(N, device=dev)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, out, False, bool(b_mn), bias=bias, aux=aux, mode=1, cfg=7)
+    torch.testing.assert_close(aux.float(), ref + bias, rtol=2e-2, atol=0.15)
+    torch.testing.assert_close(out.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=0.15)
+    res = _mk((M, N), dev, g)
+    C.gemm(A, B, out, False, bool(b_mn), res=res, alpha=0.5, cfg=7)
+    torch.testing.assert_close(out.float(), 0.5 * ref + res.float(), rtol=2e-2, atol=0.15)
+    pre = _mk((M, N), dev, g)
+    C.gemm(A, B, out, False, bool(b_mn), aux=pre, mode=2, cfg=7)
+    x = pre.float()
+    dg = 0.5 * (1 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+    torch.testing.assert_close(out.float(), ref * dg, rtol=2e-2, atol=0.15)
+    # outside the 256-multiple domain -> the ping-pong fallback, same numbers
+    Bt = B[:, : N - 40] if b_mn else B[: N - 40]
+    out = torch.empty(M, N - 40, dtype=torch.float32, device=dev)
+    C.gemm(A, Bt, out, False, bool(b_mn), cfg=7)
+    torch.testing.assert_close(out, ref[:, : N - 40], rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("b_mn", [0, 1])
+def test_w4_asm_kernel_repeatable_full_chip(dev, b_mn):
+    """Repeated full-chip runs of config 7 are bit-identical and agree with config 1 to fp32 rounding
+    (K = 3072: 24 K-tiles through both LDS stages many times)."""
+    C = require_native()
+    M, N, K = 8192, 2304, 3072
+    g = torch.Generator().manual_seed(78 + b_mn)
+    A = _mk((M, K), dev, g)
+    B = _mk((K, N) if b_mn else (N, K), dev, g)
+    ref = torch.empty(M, N, device=dev)
+    C.gemm(A, B, ref, False, bool(b_mn), cfg=1)
+    first = None
+    for _ in range(4):
+        out = torch.full((M, N), float("nan"), device=dev)
+        C.gemm(A, B, out, False, bool(b_mn), cfg=7)
+        if first is None:
+            first = out.clone()
+        assert torch.equal(out, first)
+    torch.testing.assert_close(first, ref, rtol=1e-4, atol=1e-3)
