@@ -109,5 +109,11 @@ bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ld
 template <typename OutT>
 void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                     int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st);
+// ... and its fp8 form (block-scaled MFMA, unit scales; both operands k-contiguous bytes)
+bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
+                          const GemmEpi& e);
+template <typename OutT, int FA, int FB>
+void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                       int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st);
 
 }  // namespace mlt

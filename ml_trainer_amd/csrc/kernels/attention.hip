@@ -431,11 +431,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
     f32x4 p[NK][4], ds[NK][4];  // rows q = qt*16 + 4g + r, column = key (lane)
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
+      // dP accumulates onto -delta (the MFMA's C operand): dS = P * dP' (as the ring kernel)
+      const float4 d4 = *reinterpret_cast<const float4*>(&del_s[cur][qt * 16 + 4 * g]);
       f32x4 sv[NK], dp[NK];
 #pragma unroll
       for (int n = 0; n < NK; ++n) {
         sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{-d4.x, -d4.y, -d4.z, -d4.w};
       }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
@@ -447,8 +449,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
         }
       }
       const float4 l4 = *reinterpret_cast<const float4*>(&lse_s[cur][qt * 16 + 4 * g]);
-      const float4 d4 = *reinterpret_cast<const float4*>(&del_s[cur][qt * 16 + 4 * g]);
-      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+      const float lr[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
       for (int n = 0; n < NK; ++n)
 #pragma unroll
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __re
           const bool ok = key[n] < len && q0 + ql < S;
           const float pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
           p[n][qt][r] = pv;
-          ds[n][qt][r] = pv * (dp[n][r] - dr[r]);
+          ds[n][qt][r] = pv * dp[n][r];
         }
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS  (k = queries, two 32-query steps)
@@ -570,9 +571,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
     for (int kt = 0; kt < 4; ++kt) {
       f32x4 sv[NQ], dp[NQ];
 #pragma unroll
-      for (int n = 0; n < NQ; ++n) {
+      for (int n = 0; n < NQ; ++n) {  // dP accumulates onto -delta: dS = P * dP'
         sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = f32x4{-dl[n], -dl[n], -dl[n], -dl[n]};
       }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
         for (int r = 0; r < 4; ++r) {
           const int key = kb * AB + kt * 16 + 4 * g + r;
           const float pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
-          ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+          ds[n][kt][r] = pv * dp[n][r];
         }
     }
     // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
@@ -881,11 +882,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
       f32x4 pe[NK], dse[NK];  // the even qt of the current pair
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) {
+        // dP accumulates onto -delta (the MFMA's C operand), so dS = P * dP' needs no subtraction
+        const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
+        const f32x4 ndr = {-d4.x, -d4.y, -d4.z, -d4.w};
         f32x4 sv[NK], dp[NK];
 #pragma unroll
         for (int n = 0; n < NK; ++n) {
           sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-          dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[n] = ndr;
         }
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
@@ -897,8 +901,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
           }
         }
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
-        const float4 d4 = *reinterpret_cast<const float4*>(del_s + qt * 16 + 4 * g);
-        const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+        const float lr[4] = {l4.x, l4.y, l4.z, l4.w};
         f32x4 pc[NK], dsc[NK];
 #pragma unroll
         for (int n = 0; n < NK; ++n)
@@ -915,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
               pv = fast_exp2(ok ? sv[n][r] * sl2 - lr[r] : -INFINITY);
             }
             pc[n][r] = pv;
-            dsc[n][r] = pv * (dp[n][r] - dr[r]);
+            dsc[n][r] = pv * dp[n][r];
           }
 #pragma unroll
         for (int n = 0; n < NK; ++n) {
@@ -1107,9 +1110,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
       for (int kt = 0; kt < 4; ++kt) {
         f32x4 sv[NQ], dp[NQ];
 #pragma unroll
-        for (int n = 0; n < NQ; ++n) {
+        for (int n = 0; n < NQ; ++n) {  // dP accumulates onto -delta: dS = P * dP'
           sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-          dp[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[n] = f32x4{-dl[n], -dl[n], -dl[n], -dl[n]};
         }
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
@@ -1131,7 +1134,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
               const int key = kb * AB + kt * 16 + 4 * g + r;
               pv = fast_exp2(key < len ? sv[n][r] * sl2 - lq[n] : -INFINITY);
             }
-            ds[n][kt][r] = pv * (dp[n][r] - dl[n]);
+            ds[n][kt][r] = pv * dp[n][r];
           }
       }
     };

@@ -866,6 +866,10 @@ double est_time(int cfg, int splits, int M, int N, int K, int kstep, double spee
 // overrides). 4 measured >= 8 everywhere on MI355X (profiles/gemm_group_m_r2.txt: BERT-base b512
 // +1.0 %, fp8 large b512 +1.1 %, BERT-base b128 equal); 16 lost 2-3 % at b128 (ab_gemm_group_m.txt)
 constexpr int kGroupM = 4;
+// cfg 7 runs one 256 x 256 tile per workgroup and never splits K: below about one tile per CU the
+// split-K tiles win (the fp8 weight gradients of the `large` config: 16-256 tiles at K = 256K
+// tokens ran 1,064 -> 621 samples/s end to end when cfg 7 took them)
+constexpr int kW4MinTiles = 240;
 
 GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
                     bool allow_pp = true, bool allow_persist = true) {
@@ -1019,6 +1023,15 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
           launch_gemm_w4<OutT>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, BNL, st);
           break;
         }
+      } else if constexpr (!AM && !BNL && F8A >= 0 && (sizeof(OutT) == 2 || sizeof(OutT) == 4)) {
+        if (p.splits == 1 && gemm_w4_f8_supported(M, N, K, lda, ldb, ldc, (int)sizeof(OutT), e)) {
+          static const int group_m = [] {
+            const char* v = getenv("MLT_GEMM_GROUP_M");
+            return v ? atoi(v) : kGroupM;
+          }();
+          launch_gemm_w4_f8<OutT, F8A, F8B>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+          break;
+        }
       }
       launch_pp<AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
       break;
@@ -1064,8 +1077,9 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
     const char* v = getenv("MLT_GEMM_W4");
     return !(v && atoi(v) == 0);
   }();
+  // (only with enough tiles to fill the chip: few-tile / long-K shapes keep the split-K planner)
   if (w4 && force_cfg < 0 && force_splits <= 0 && a_mn == 0 && M % 256 == 0 && N % 256 == 0 && K % 128 == 0 &&
-      K >= 256) {
+      K >= 256 && (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
     GemmPlan p{7, 1, K / 64, 0, 0};
     return p;
   }
@@ -1075,6 +1089,17 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
 }
 
 GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {
+  // the 4-wave asm kernel's fp8 form (cfg 7) where it applies; MLT_GEMM_W4=0 / MLT_GEMM_W4F8=0 opt out
+  static const bool w4 = [] {
+    const char* v = getenv("MLT_GEMM_W4");
+    const char* v8 = getenv("MLT_GEMM_W4F8");
+    return !(v && atoi(v) == 0) && !(v8 && atoi(v8) == 0);
+  }();
+  if (w4 && force_cfg < 1 && force_splits <= 0 && M % 256 == 0 && N % 256 == 0 && K % 256 == 0 && K >= 512 &&
+      (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
+    GemmPlan p{7, 1, K / 128, 0, 0};
+    return p;
+  }
   GemmPlan p = plan_tiles(M, N, K, force_cfg < 1 ? -1 : force_cfg, force_splits, 128, false);
   if (p.cfg == 0) p.cfg = -1;  // not runnable (K % 128 != 0 or too small)
   return p;

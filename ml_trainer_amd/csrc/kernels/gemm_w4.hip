@@ -33,6 +33,95 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ uint32_t pack2(uint16_t lo, uint16_t hi) { return (uint32_t)lo | ((uint32_t)hi << 16); }
 constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 * kW4Pitch * 4 : 131072;
 
+// ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct
+// stores would be 64 x 8 bytes per lane in 32-byte row pieces (store-issue bound). Each wave
+// instead writes its 128 x 128 fp32 tile to its own LDS image in two 64-row halves (pitch 132
+// floats: the 16 rows of a fragment write land 4 banks apart) and reads it back as 8 consecutive
+// columns per lane: 32 x 16-byte stores per lane (bf16), side operands as 16-byte loads.
+template <typename OutT, int EK>
+__device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, const GemmEpi& epi, float alpha, int m0,
+                                            int n0, int w, int lane, uint8_t* smem) {
+  const int wr = w >> 1, wc = w & 1, g = lane >> 4, rl = lane & 15;
+  __syncthreads();  // every wave is past its last read of the K-tile stages
+  constexpr int P = kW4Pitch;
+  float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
+  const int rsub = lane >> 4, cc = lane & 15;  // read side: row 4 * it + rsub, columns 8 cc .. + 7
+  const int gn = n0 + wc * 128 + 8 * cc;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+  if (epi.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(epi.bias + gn);
+    const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
+    bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
+  }
+  // side operands (residual / dGELU pre-activation) of BOTH halves issued first: one HBM round trip
+  // under the image writes instead of one per half
+  uint4 sd[2][16];
+  if constexpr (EK == W4_RES || EK == W4_DGELU) {
+    const uint16_t* sx = EK == W4_RES ? epi.res : epi.aux;
+    const int64_t ldx = EK == W4_RES ? epi.ldres : epi.ldaux;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
+        sd[h][it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
+      }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x0, x1, x2, x3;
+        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
+        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
+      const float4 lo = *reinterpret_cast<const float4*>(img + row * P + 8 * cc);
+      const float4 hi = *reinterpret_cast<const float4*>(img + row * P + 8 * cc + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
+      if constexpr (EK == W4_GELU) {  // keep the (bf16-rounded) pre-activation for the backward
+        uint16_t a[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[e] = f32_to_bf16(v[e]);
+          v[e] = gelu_f(bf16_to_f32(a[e]));
+        }
+        *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
+            make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
+      } else if constexpr (EK == W4_RES || EK == W4_DGELU) {
+        const uint32_t sw4[4] = {sd[h][it].x, sd[h][it].y, sd[h][it].z, sd[h][it].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
+          if constexpr (EK == W4_RES)
+            v[e] += x;
+          else
+            v[e] *= gelu_grad(x);
+        }
+      }
+      OutT* cp = C + (int64_t)gm * ldc + gn;
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        *reinterpret_cast<uint4*>(cp) =
+            make_uint4(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), f32_to_bf16(v[3])),
+                       pack2(f32_to_bf16(v[4]), f32_to_bf16(v[5])), pack2(f32_to_bf16(v[6]), f32_to_bf16(v[7])));
+      }
+    }
+    if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
+  }
+}
+
 template <typename OutT, int EK, bool BN>
 __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                              OutT* __restrict__ C, int K, int64_t lda, int64_t ldb, int64_t ldc,
@@ -105,86 +194,67 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
                  : MLT_W4_CLOBBERS_BN, "memory");
   }
 
-  // ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct
-  // stores would be 64 x 8 bytes per lane in 32-byte row pieces (store-issue bound). Each wave
-  // instead writes its 128 x 128 fp32 tile to its own LDS image in two 64-row halves (pitch 132
-  // floats: the 16 rows of a fragment write land 4 banks apart) and reads it back as 8 consecutive
-  // columns per lane: 32 x 16-byte stores per lane (bf16), side operands as 16-byte loads.
-  __syncthreads();  // every wave is past its last read of the K-tile stages
-  constexpr int P = kW4Pitch;
-  float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
-  const float alpha = epi.alpha;
-  const int rsub = lane >> 4, cc = lane & 15;  // read side: row 4 * it + rsub, columns 8 cc .. + 7
-  const int gn = n0 + wc * 128 + 8 * cc;
-  float bs[8];
+  w4_epilogue<OutT, EK>(C, ldc, epi, epi.alpha, m0, n0, w, lane, smem);
+}
+
+// fp8 operands (OCP e4m3 = 0 / e5m2 = 1 each; A [M][K], B [N][K] bytes): the block-scaled MFMA with
+// unit scales, K-tile = 128 elements = the same 128-byte LDS rows; a fragment is the lane's 32
+// bytes (chunks 2g and 2g + 1 of its row). Main loop: MLT_W4F8_LOOP_ASM (scripts/gen_gemm_w4.py).
+template <typename OutT, int EK, int FA, int FB>
+__device__ __forceinline__ void gemm_w4f8_tile(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                               OutT* __restrict__ C, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                               const GemmEpi& epi, int id, int gm_, int tiles_m, int tiles_n,
+                                               uint8_t* smem) {
+  const int per_group = gm_ * tiles_n, grp = id / per_group, first_m = grp * gm_;
+  const int gsize = min(tiles_m - first_m, gm_), rr = id - grp * per_group;
+  const int m0 = (first_m + rr % gsize) * 256, n0 = (rr / gsize) * 256;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_u8*)smem;
+  const int g = lane >> 4, rl = lane & 15, sw = (rl >> 1) & 7;
+  auto raddr = [&](int stage, int isb, int hi) {
+    const int row = (isb ? wc : wr) * 128 + rl;
+    return lds0 + stage * 65536 + isb * 32768 + row * 128 + (((2 * g + hi) ^ sw) << 4);
+  };
+  const uint32_t raL0 = raddr(0, 0, 0), raH0 = raddr(0, 0, 1), raL1 = raddr(1, 0, 0), raH1 = raddr(1, 0, 1);
+  const uint32_t rbL0 = raddr(0, 1, 0), rbH0 = raddr(0, 1, 1), rbL1 = raddr(1, 1, 0), rbH1 = raddr(1, 1, 1);
+  uint32_t ga[8], gb[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
-  if (epi.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(epi.bias + gn);
-    const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
-    bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
+  for (int p = 0; p < 8; ++p) {
+    const int r = (p * 4 + w) * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    ga[p] = (uint32_t)(r * lda + kc * 16);
+    gb[p] = (uint32_t)(r * ldb + kc * 16);
   }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x0, x1, x2, x3;
-        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
-        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
-    uint4 sd[16];
-    if constexpr (EK == W4_RES || EK == W4_DGELU) {  // the half's side operands first, then the stores
-      const uint16_t* sx = EK == W4_RES ? epi.res : epi.aux;
-      const int64_t ldx = EK == W4_RES ? epi.ldres : epi.ldaux;
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
-        sd[it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
-      const float4 lo = *reinterpret_cast<const float4*>(img + row * P + 8 * cc);
-      const float4 hi = *reinterpret_cast<const float4*>(img + row * P + 8 * cc + 4);
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
-      if constexpr (EK == W4_GELU) {  // keep the (bf16-rounded) pre-activation for the backward
-        uint16_t a[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          a[e] = f32_to_bf16(v[e]);
-          v[e] = gelu_f(bf16_to_f32(a[e]));
-        }
-        *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
-            make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
-      } else if constexpr (EK == W4_RES || EK == W4_DGELU) {
-        const uint32_t sw4[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
-          if constexpr (EK == W4_RES)
-            v[e] += x;
-          else
-            v[e] *= gelu_grad(x);
-        }
-      }
-      OutT* cp = C + (int64_t)gm * ldc + gn;
-      if constexpr (sizeof(OutT) == 4) {
-        *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      } else {
-        *reinterpret_cast<uint4*>(cp) =
-            make_uint4(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), f32_to_bf16(v[3])),
-                       pack2(f32_to_bf16(v[4]), f32_to_bf16(v[5])), pack2(f32_to_bf16(v[6]), f32_to_bf16(v[7])));
-      }
-    }
-    if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
-  }
+  const uint64_t sa = (uint64_t)(uintptr_t)(A + (int64_t)m0 * lda);
+  const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * ldb);
+  const uint32_t lw = __builtin_amdgcn_readfirstlane(lds0 + w * 1024);
+  int np = (K >> 8) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
+  asm volatile(MLT_W4F8_LOOP_ASM
+               : [np] "+s"(np)
+               : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [raL0] "v"(raL0), [raH0] "v"(raH0), [raL1] "v"(raL1),
+                 [raH1] "v"(raH1), [rbL0] "v"(rbL0), [rbH0] "v"(rbH0), [rbL1] "v"(rbL1), [rbH1] "v"(rbH1),
+                 [ga0] "v"(ga[0]), [ga1] "v"(ga[1]), [ga2] "v"(ga[2]), [ga3] "v"(ga[3]), [ga4] "v"(ga[4]),
+                 [ga5] "v"(ga[5]), [ga6] "v"(ga[6]), [ga7] "v"(ga[7]), [gb0] "v"(gb[0]), [gb1] "v"(gb[1]),
+                 [gb2] "v"(gb[2]), [gb3] "v"(gb[3]), [gb4] "v"(gb[4]), [gb5] "v"(gb[5]), [gb6] "v"(gb[6]),
+                 [gb7] "v"(gb[7]), [fa] "n"(FA), [fb] "n"(FB)
+               : MLT_W4F8_CLOBBERS, "memory");
+  float alpha = epi.alpha;
+  if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
+  if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
+  w4_epilogue<OutT, EK>(C, ldc, epi, alpha, m0, n0, w, lane, smem);
+}
+
+template <typename OutT, int EK, int FA, int FB>
+__global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                           OutT* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                           int64_t ldb, int64_t ldc, GemmEpi epi, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tiles_m = M >> 8, tiles_n = N >> 8;
+  const int gm_ = group_m > 0 ? group_m : tiles_m;
+  gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C, K, lda, ldb, ldc, epi, xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m,
+                                   tiles_n, smem);
 }
 
 // One tile per workgroup. (A persistent variant -- one workgroup per CU walking id, id + 256, ...,
@@ -252,6 +322,56 @@ void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, i
   else
     launch_w4_bn<OutT, false>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
 }
+
+template <typename OutT, int EK, int FA, int FB>
+static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                           int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+  constexpr int SMEM = kW4Smem;
+  auto kern = gemm_w4f8_kernel<OutT, EK, FA, FB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((M / 256) * (N / 256)), dim3(256), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e,
+                     group_m);
+}
+template <typename OutT, int FA, int FB>
+void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                       int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+  if (e.mode == 1)
+    launch_w4f8_ek<OutT, W4_GELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else if (e.mode == 2)
+    launch_w4f8_ek<OutT, W4_DGELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else if (e.res)
+    launch_w4f8_ek<OutT, W4_RES, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else
+    launch_w4f8_ek<OutT, W4_PLAIN, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+}
+bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
+                          const GemmEpi& e) {
+  auto al = [](const void* p, int64_t ld, int esz) {
+    return p == nullptr || ((((uintptr_t)p) % 16) == 0 && (ld * esz) % 16 == 0);
+  };
+  if (M % 256 || N % 256 || K % 256 || K < 512) return false;
+  if (lda % 16 || ldb % 16 || (ldc * out_bytes) % 16) return false;
+  if (lda * 256 > (int64_t)1 << 31 || ldb * 256 > (int64_t)1 << 31) return false;
+  if (e.accumulate || e.q_colpart || e.qt || e.mode == 3) return false;
+  if (!al(e.res, e.ldres, 2) || !al(e.aux, e.ldaux, 2) || (e.bias && ((uintptr_t)e.bias) % 16)) return false;
+  if (out_bytes == 4 && (e.mode != 0 || e.res)) return false;
+  if (e.mode != 0 && e.res) return false;
+  return true;
+}
+#define MLT_W4F8_INST(OT, FA, FB)                                                                                   \
+  template void launch_gemm_w4_f8<OT, FA, FB>(const uint8_t*, const uint8_t*, OT*, int, int, int, int64_t, int64_t, \
+                                              int64_t, const GemmEpi&, int, hipStream_t);
+MLT_W4F8_INST(uint16_t, 0, 0)
+MLT_W4F8_INST(uint16_t, 1, 0)
+MLT_W4F8_INST(uint16_t, 0, 1)
+MLT_W4F8_INST(float, 0, 0)
+MLT_W4F8_INST(float, 1, 0)
+MLT_W4F8_INST(float, 0, 1)
+#undef MLT_W4F8_INST
 
 template void launch_gemm_w4<uint16_t>(const uint8_t*, const uint8_t*, uint16_t*, int, int, int, int64_t, int64_t,
                                        int64_t, const GemmEpi&, int, bool, hipStream_t);

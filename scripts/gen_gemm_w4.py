@@ -159,6 +159,82 @@ def build(bn=False):
     return out
 
 
+# ---- fp8 (block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, scales fixed at 1.0) ------------------
+# A K-tile is 128 fp8 = the same 128-byte LDS rows. Fragment = 32 bytes per lane (8 VGPRs, two
+# ds_read_b128 of chunks 2g and 2g + 1). Registers: A double-buffered v[0:63] / v[64:127], B
+# single-buffered v[128:191] and refilled column by column: 64 MFMAs per K-tile in column-major
+# order (j outer), so B_j is free 8 MFMAs after its first use; its next-tile copy is read 2 MFMAs
+# after its last use (no WAR on an MFMA source still in flight). The tile's barrier sits after the
+# refill of B_7 (read at MFMA 1 of the tile from the tile's own stage): from there the stage is
+# read out, so the DMAs of tile t + 2 go into it, and tile t + 1 (landed: vmcnt(0)) is readable.
+# 32 cycles per MFMA on one SIMD -> 2,048 cycles per K-tile of 128: twice the bf16 FLOP rate.
+def f8_frag(buf, idx):
+    base = {"A0": 0, "A1": 64, "B": 128}[buf] + 8 * idx
+    return base
+
+
+def f8_read(buf, idx, stage):
+    ab = "b" if buf == "B" else "a"
+    b = f8_frag(buf, idx)
+    return [f"ds_read_b128 v[{b}:{b + 3}], %[r{ab}L{stage}] offset:{idx * 2048}",
+            f"ds_read_b128 v[{b + 4}:{b + 7}], %[r{ab}H{stage}] offset:{idx * 2048}"]
+
+
+def f8_mfma(k, acur, zero_c):
+    j, i = k // 8, k % 8
+    c = "0" if zero_c else acc(i, j)
+    a, b = f8_frag(acur, i), f8_frag("B", j)
+    return (f"v_mfma_scale_f32_16x16x128_f8f6f4 {acc(i, j)}, v[{b}:{b + 7}], v[{a}:{a + 7}], {c}, v192, v192 "
+            "op_sel_hi:[0,0,0] cbsz:%[fb] blgp:%[fa]")
+
+
+def f8_tile(stage, acur, anext, out, zero_c=False, refill_b7=True, do_glds=True, do_reads=True):
+    ra = [r for idx in range(8) for r in f8_read(anext, idx, stage ^ 1)] if do_reads else []
+    for k in range(64):
+        out.append(f8_mfma(k, acur, zero_c))
+        if k == 1 and refill_b7:
+            out += f8_read("B", 7, stage)
+        if k == 2:
+            out += ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_barrier"]
+        if do_glds and k >= 3 and (k - 3) % 4 == 0:
+            out.extend(glds((k - 3) // 4, stage))
+        if do_reads:
+            if k >= 9 and (k - 9) % 8 == 0 and (k - 9) // 8 < 7:  # B_j of the next tile, j = 0..6
+                out += f8_read("B", (k - 9) // 8, stage ^ 1)
+            if 4 <= k <= 34 and k % 2 == 0:
+                out.append(ra[(k - 4) // 2])
+    if do_glds:
+        out += adv(False)
+    if do_reads:
+        out.append("s_waitcnt lgkmcnt(2)")  # all but B_6's two reads: the next tile's first MFMAs' operands
+
+
+def build_f8():
+    out = ["s_mov_b64 s[88:89], %[sa]", "s_mov_b64 s[90:91], %[sb]", "v_mov_b32 v192, 0x7f"]
+    for t in range(2):
+        for p in range(16):
+            out.extend(glds(p, t))
+        out += adv(False)
+    out += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    for idx in range(8):
+        out += f8_read("A0", idx, 0)
+    for idx in range(8):
+        out += f8_read("B", idx, 0)
+    out.append("s_waitcnt lgkmcnt(0)")
+    f8_tile(0, "A0", "A1", out, zero_c=True, refill_b7=False)
+    f8_tile(1, "A1", "A0", out)
+    out += ["s_cmp_eq_u32 %[np], 0", "s_cbranch_scc1 L_w4f8_last_%="]
+    out.append("L_w4f8_loop_%=:")
+    f8_tile(0, "A0", "A1", out)
+    f8_tile(1, "A1", "A0", out)
+    out += ["s_sub_u32 %[np], %[np], 1", "s_cmp_lg_u32 %[np], 0", "s_cbranch_scc1 L_w4f8_loop_%="]
+    out.append("L_w4f8_last_%=:")
+    f8_tile(0, "A0", "A1", out, do_glds=False)
+    f8_tile(1, "A1", "A0", out, do_glds=False, do_reads=False)
+    out += ["s_nop 15", "s_nop 15", "s_nop 15", "s_nop 7"]
+    return out
+
+
 def emit(f, name, lines):
     f.write(f"// {name}: {len(lines)} instructions\n#define {name} \\\n")
     for ln in lines:
@@ -177,6 +253,10 @@ def main():
         f.write(f"#define MLT_W4_CLOBBERS {clob}\n")
         clob_bn = clob + ", " + ", ".join(f'"v{r}"' for r in range(192, 208))
         f.write(f"#define MLT_W4_CLOBBERS_BN {clob_bn}\n")
+        emit(f, "MLT_W4F8_LOOP_ASM", build_f8())
+        clob_f8 = ", ".join(f'"v{r}"' for r in range(193)) + ", " + ", ".join(f'"a{r}"' for r in range(256))
+        clob_f8 += ', "s88", "s89", "s90", "s91", "m0", "scc"'
+        f.write(f"#define MLT_W4F8_CLOBBERS {clob_f8}\n")
         # the epilogue's accumulator reads: fragment f (compile-time after unrolling) -> 4 floats
         f.write("#define MLT_W4_READ_FRAG(f, x0, x1, x2, x3) \\\n  switch (f) { \\\n")
         for fr in range(64):

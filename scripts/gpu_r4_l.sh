@@ -12,3 +12,8 @@ for w in 1 0; do
   cp $f $O/bert_w$w.csv
   python3 scripts/kstats.py $O/bert_w$w.csv 7 14 | cut -c1-150
 done
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests -k "attn or attention" \
+  > $O/t_attn.log 2>&1 || { tail -30 $O/t_attn.log; exit 1; }
+tail -1 $O/t_attn.log
+for b in 512 512; do ATTN_B=$b timeout -k 10 120 python3 -u benchmarks/attn_bench.py >> $O/attn_bench.jsonl 2>$O/attn.err || exit 1; done
+cat $O/attn_bench.jsonl

@@ -257,3 +257,49 @@ def test_fp8_wgrad_bias_fused_and_fallback(dev):
     torch.testing.assert_close(db2, ref_db, rtol=1e-5, atol=1e-3)
     ref_dw = dy.float().t() @ x.float()
     assert ((dw2 - ref_dw).norm() / ref_dw.norm()) < 0.02 and ((dw - ref_dw).norm() / ref_dw.norm()) < 0.1
+
+
+@pytest.mark.parametrize("fmts", [(0, 0), (1, 0), (0, 1)])
+def test_gemm_f8_w4_asm(dev, fmts):
+    """Config 7 in fp8 (4-wave tile, generated-asm loop on v_mfma_scale_f32_16x16x128_f8f6f4 with unit
+    scales, A double-buffered / B column-refilled fragments): fp32 and bf16 outputs, bias + residual,
+    GELU with the pre-activation, dGELU; the planner picks it for 256-multiple shapes."""
+    C = require_native()
+    fa, fb = fmts
+    M, N, K = 1024, 768, 1536  # 12 tiles; 12 K-tiles of 128 (6 pairs: peeled + loop + last)
+    g = torch.Generator().manual_seed(300 + 10 * fa + fb)
+    A = _rand_f8((M, K), fa, g, dev, 4.0)
+    B = _rand_f8((N, K), fb, g, dev, 4.0)
+    # the planner takes cfg 7 when the tiles fill the chip, split-K tiles for few-tile long-K shapes
+    assert C.gemm_f8_plan(65536, 1024, 1024)[0] == 7
+    assert C.gemm_f8_plan(1024, 1024, 262144)[0] != 7
+    isa = torch.tensor([0.5], device=dev)
+    isb = torch.tensor([0.25], device=dev)
+    ref = (A.float() @ B.float().t()) * 0.125
+    out = torch.empty(M, N, dtype=torch.float32, device=dev)
+    C.gemm_f8(A, B, out, fa, fb, isa, isb, cfg=7)
+    torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-4 * ref.abs().max().item())
+    out5 = torch.empty_like(out)
+    C.gemm_f8(A, B, out5, fa, fb, isa, isb, cfg=5)
+    torch.testing.assert_close(out, out5, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    ob = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm_f8(A, B, ob, fa, fb, isa, isb, bias=bias, res=res, cfg=7)
+    torch.testing.assert_close(ob.float(), ref + bias + res.float(), rtol=1e-2, atol=0.5)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm_f8(A, B, ob, fa, fb, isa, isb, bias=bias, aux=aux, mode=1, cfg=7)
+    torch.testing.assert_close(aux.float(), ref + bias, rtol=1e-2, atol=0.5)
+    torch.testing.assert_close(ob.float(), torch.nn.functional.gelu(aux.float()), rtol=1e-2, atol=0.05)
+
+
+def test_gemm_f8_w4_identity_asymmetric(dev):
+    """Operand roles / fragment layout of the fp8 asm loop: A = I picks rows of B exactly."""
+    C = require_native()
+    M, N, K = 256, 256, 512
+    A = torch.eye(M, K).to(torch.float8_e4m3fn).to(dev)
+    B = ((torch.arange(N * K).view(N, K) % 13) - 6).float().to(torch.float8_e4m3fn).to(dev)
+    one = torch.ones(1, device=dev)
+    out = torch.empty(M, N, dtype=torch.float32, device=dev)
+    C.gemm_f8(A, B, out, 0, 0, one, one, cfg=7)
+    torch.testing.assert_close(out, B.float()[:, :M].t())

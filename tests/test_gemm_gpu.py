@@ -303,7 +303,8 @@ def test_w4_asm_kernel(dev, b_mn):
     A = _mk((M, K + 64), dev, g)[:, :K]
     B = _mk((K, N + 128), dev, g)[:, :N] if b_mn else _mk((N, K), dev, g)
     ref = _ref(A, B, 0, b_mn)
-    assert C.gemm_plan(False, bool(b_mn), M, N, K)[0] == 7
+    assert C.gemm_plan(False, bool(b_mn), 65536, N, K)[0] == 7  # planner: tiles fill the chip
+    assert C.gemm_plan(False, bool(b_mn), 1024, 1024, 65536)[0] != 7  # few tiles, long K: split-K
     for out_dtype in (torch.bfloat16, torch.float32):
         out = torch.empty(M, N, dtype=out_dtype, device=dev)
         C.gemm(A, B, out, False, bool(b_mn), cfg=7)
