@@ -109,6 +109,13 @@ bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ld
 template <typename OutT>
 void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                     int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st);
+// ... its weight-gradient layout (A [K][M], B [K][N]) with split-K raw partials ws[z][M][N]
+bool gemm_w4_wgrad_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
+                             const GemmEpi& e, int splits, int ksteps);
+template <typename OutT>
+void launch_gemm_w4_wgrad(const uint8_t* A, const uint8_t* B, OutT* C, float* ws, int M, int N, int K, int64_t lda,
+                          int64_t ldb, int64_t ldc, const GemmEpi& e, int group_m, int splits, int ksteps,
+                          hipStream_t st);
 // ... and its fp8 form (block-scaled MFMA, unit scales; both operands k-contiguous bytes)
 bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
                           const GemmEpi& e);

@@ -870,6 +870,8 @@ constexpr int kGroupM = 4;
 // split-K tiles win (the fp8 weight gradients of the `large` config: 16-256 tiles at K = 256K
 // tokens ran 1,064 -> 621 samples/s end to end when cfg 7 took them)
 constexpr int kW4MinTiles = 240;
+// one workgroup's 256 x 256 x 64 K-tile at ~1.4 PF / 256 CUs (planner model for the split choice)
+constexpr double kW4KtileSec = 2.0 * 256 * 256 * 64 / (1.4e15 / 256);
 
 GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
                     bool allow_pp = true, bool allow_persist = true) {
@@ -1023,6 +1025,19 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
           launch_gemm_w4<OutT>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, BNL, st);
           break;
         }
+      } else if constexpr (AM && BNL && F8A < 0 && (sizeof(OutT) == 2 || sizeof(OutT) == 4)) {
+        // weight gradients: both operands transposed in LDS, split-K raw partials (external reduce)
+        if (gemm_w4_wgrad_supported(M, N, K, lda, ldb, ldc, (int)sizeof(OutT), e, p.splits, p.ksteps) &&
+            (p.splits == 1 || (ws != nullptr && cnt == nullptr))) {
+          static const int group_m = [] {
+            const char* v = getenv("MLT_GEMM_GROUP_M");
+            return v ? atoi(v) : kGroupM;
+          }();
+          launch_gemm_w4_wgrad<OutT>(A, B, C, ws, M, N, K, lda, ldb, ldc, e, group_m, p.splits, p.ksteps, st);
+          break;
+        }
+        launch_tile<256, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
+        break;
       } else if constexpr (!AM && !BNL && F8A >= 0 && (sizeof(OutT) == 2 || sizeof(OutT) == 4)) {
         if (p.splits == 1 && gemm_w4_f8_supported(M, N, K, lda, ldb, ldc, (int)sizeof(OutT), e)) {
           static const int group_m = [] {
@@ -1082,6 +1097,33 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
       K >= 256 && (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
     GemmPlan p{7, 1, K / 64, 0, 0};
     return p;
+  }
+  // weight gradients (both operands mn-contiguous, few tiles, K = tokens): cfg 7 with split-K raw
+  // partials reduced by one grid-wide launch; splits from a rounds x K-steps + reduce-traffic model
+  if (w4 && force_cfg < 0 && force_splits <= 0 && a_mn == 1 && b_mn == 1 && M % 256 == 0 && N % 256 == 0 &&
+      K % 128 == 0 && K >= 256) {
+    const int tiles = (M / 256) * (N / 256), nk = K / 64;
+    double best = 1e30;
+    int bs = 0, bks = 0;
+    for (int S = 1; S <= 64; ++S) {
+      int ks = (nk + S - 1) / S;
+      ks += ks & 1;
+      if (ks < 4) break;
+      const int last = nk - (S - 1) * ks;
+      if (last < 4 || last % 2) continue;
+      const int64_t rounds = ((int64_t)tiles * S + kCUs - 1) / kCUs;
+      const double t = (double)rounds * ks * kW4KtileSec + (S > 1 ? (double)M * N * 4.0 * (S + 1) / 5.0e12 + 3.0e-6 : 0.0);
+      if (t < best) {
+        best = t;
+        bs = S;
+        bks = ks;
+      }
+    }
+    if (bs) {
+      GemmPlan p{7, bs, bks, bs > 1 ? (int64_t)bs * M * N : 0, 0};
+      p.ext = bs > 1 ? 1 : 0;
+      return p;
+    }
   }
   // the ping-pong kernel's fit covers the k-contiguous-A (forward / dgrad) shapes; weight
   // gradients (A = dY^T, mn-contiguous) stay on the 256-wide tiles with split-K

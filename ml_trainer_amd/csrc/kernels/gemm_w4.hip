@@ -122,10 +122,13 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
   }
 }
 
-template <typename OutT, int EK, bool BN>
+// AN / BN: A stored [K][M] / B stored [K][N] (mn-contiguous: weight-gradient / input-gradient
+// layouts, read through ds_read_b64_tr_b16); nkt = this workgroup's K-tiles (even, >= 4), kz = its
+// first K element (split-K)
+template <typename OutT, int EK, bool AN, bool BN>
 __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                             OutT* __restrict__ C, int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                             const GemmEpi& epi, int id, int gm_, int tiles_m, int tiles_n,
+                                             OutT* __restrict__ C, int nkt, int64_t kz, int64_t lda, int64_t ldb,
+                                             int64_t ldc, const GemmEpi& epi, int id, int gm_, int tiles_m, int tiles_n,
                                              uint8_t* smem) {
   const int per_group = gm_ * tiles_n, grp = id / per_group, first_m = grp * gm_;
   const int gsize = min(tiles_m - first_m, gm_), rr = id - grp * per_group;
@@ -145,27 +148,33 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
   };
   const uint32_t ra00 = raddr(0, 0, 0), ra01 = raddr(0, 0, 1), ra10 = raddr(1, 0, 0), ra11 = raddr(1, 0, 1);
   const uint32_t rb00 = raddr(0, 1, 0), rb01 = raddr(0, 1, 1), rb10 = raddr(1, 1, 0), rb11 = raddr(1, 1, 1);
-  // DMA sources: wave w's p-th piece fills LDS rows (4p + w) * 8 .. + 7 (1 KB, lane-linear); lane
-  // L fetches row + (L >> 3), the global chunk that lands on position L & 7 under the swizzle
+  // DMA sources: wave w's p-th piece fills 1 KB of the image (lane-linear). k-contiguous image
+  // [256 rows][128 B]: rows (4p + w) * 8 .. + 7, lane L fetches row + (L >> 3), the global chunk that
+  // lands on position L & 7 under the swizzle. mn-contiguous image [64 k][256 mn]: 32 chunks per
+  // 512-B k-row, chunk ^ (2 (k & 3) + 8 ((k >> 3) & 1)) (conflict-free transposed reads).
   uint32_t ga[8], gb[8];
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     const int r = (p * 4 + w) * 8 + (lane >> 3);
     const int kc = (lane & 7) ^ ((r >> 1) & 7);
-    ga[p] = (uint32_t)((r * lda + kc * 8) * 2);
-    if constexpr (!BN) {
-      gb[p] = (uint32_t)((r * ldb + kc * 8) * 2);
-    } else {  // B image [64 k][256 n]: 32 chunks per 512-B k-row, chunk ^ (2 (k & 3) + 8 ((k >> 3) & 1))
-      const int e = (p * 4 + w) * 64 + lane, kk = e >> 5;
-      const int c = (e & 31) ^ (((kk & 3) << 1) | (((kk >> 3) & 1) << 3));
-      gb[p] = (uint32_t)((kk * ldb + c * 8) * 2);
-    }
+    const int e = (p * 4 + w) * 64 + lane, kk = e >> 5;
+    const int c = (e & 31) ^ (((kk & 3) << 1) | (((kk >> 3) & 1) << 3));
+    ga[p] = AN ? (uint32_t)((kk * lda + c * 8) * 2) : (uint32_t)((r * lda + kc * 8) * 2);
+    gb[p] = BN ? (uint32_t)((kk * ldb + c * 8) * 2) : (uint32_t)((r * ldb + kc * 8) * 2);
   }
-  const uint64_t sa = (uint64_t)(uintptr_t)(A + (int64_t)m0 * lda * 2);
+  const uint64_t sa = (uint64_t)(uintptr_t)(A + (AN ? kz * lda + m0 : (int64_t)m0 * lda + kz) * 2);
+  const uint64_t sb = (uint64_t)(uintptr_t)(B + (BN ? kz * ldb + n0 : (int64_t)n0 * ldb + kz) * 2);
   const uint32_t lw = __builtin_amdgcn_readfirstlane(lds0 + w * 1024);
-  int np = (K >> 7) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
-  if constexpr (!BN) {
-    const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * ldb * 2);
+  int np = (nkt >> 1) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
+  // transposed fragment reads (as gemm_tile's tfrag_mn): lane (g, q = rl >> 2, p = rl & 3) reads
+  // k-rows kh*32 + 8g + q (+ 4) at column w{r,c}*128 + 16 j + 4p; with the swizzle the byte address is
+  // R + (32 j ^ X), R = row + column-pair + half, X = 16 * (2q + 8 (g & 1)) -- built in the asm
+  const int q = rl >> 2, pp = rl & 3;
+  const uint32_t rbx = (uint32_t)(32 * q + 128 * (g & 1));
+  const uint32_t rcol = lds0 + (8 * g + q) * 512 + 16 * (pp >> 1) + 8 * (pp & 1);
+  const uint32_t rbr = rcol + wc * 256, rar = rcol + wr * 256;
+  const uint32_t astep = (uint32_t)(64 * lda * 2), bstep = (uint32_t)(64 * ldb * 2);
+  if constexpr (!AN && !BN) {
     asm volatile(MLT_W4_LOOP_ASM
                  : [np] "+s"(np)
                  : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [ra00] "v"(ra00), [ra01] "v"(ra01), [ra10] "v"(ra10),
@@ -175,15 +184,7 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
                    [gb2] "v"(gb[2]), [gb3] "v"(gb[3]), [gb4] "v"(gb[4]), [gb5] "v"(gb[5]), [gb6] "v"(gb[6]),
                    [gb7] "v"(gb[7])
                  : MLT_W4_CLOBBERS, "memory");
-  } else {
-    // transposed B fragment reads (as gemm_tile's tfrag_mn): lane (g, q = rl >> 2, p = rl & 3) reads
-    // k-rows kh*32 + 8g + q (+ 4) at column wc*128 + 16 j + 4p; with the swizzle the byte address is
-    // R + (32 j ^ X), R = row + column-pair + half, X = 16 * (2q + 8 (g & 1)) -- built in the asm
-    const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * 2);
-    const uint32_t bstep = (uint32_t)(64 * ldb * 2);
-    const int q = rl >> 2, pp = rl & 3;
-    const uint32_t rbr = lds0 + (8 * g + q) * 512 + wc * 256 + 16 * (pp >> 1) + 8 * (pp & 1);
-    const uint32_t rbx = (uint32_t)(32 * q + 128 * (g & 1));
+  } else if constexpr (!AN) {
     asm volatile(MLT_W4_LOOP_ASM_BN
                  : [np] "+s"(np)
                  : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [bstep] "s"(bstep), [ra00] "v"(ra00), [ra01] "v"(ra01),
@@ -192,6 +193,16 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
                    [ga6] "v"(ga[6]), [ga7] "v"(ga[7]), [gb0] "v"(gb[0]), [gb1] "v"(gb[1]), [gb2] "v"(gb[2]),
                    [gb3] "v"(gb[3]), [gb4] "v"(gb[4]), [gb5] "v"(gb[5]), [gb6] "v"(gb[6]), [gb7] "v"(gb[7])
                  : MLT_W4_CLOBBERS_BN, "memory");
+  } else {
+    static_assert(BN, "mn-contiguous A is built with an mn-contiguous B (the weight-gradient layout)");
+    asm volatile(MLT_W4_LOOP_ASM_ANBN
+                 : [np] "+s"(np)
+                 : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [astep] "s"(astep), [bstep] "s"(bstep), [rar] "v"(rar),
+                   [rbr] "v"(rbr), [rbx] "v"(rbx), [ga0] "v"(ga[0]), [ga1] "v"(ga[1]), [ga2] "v"(ga[2]),
+                   [ga3] "v"(ga[3]), [ga4] "v"(ga[4]), [ga5] "v"(ga[5]), [ga6] "v"(ga[6]), [ga7] "v"(ga[7]),
+                   [gb0] "v"(gb[0]), [gb1] "v"(gb[1]), [gb2] "v"(gb[2]), [gb3] "v"(gb[3]), [gb4] "v"(gb[4]),
+                   [gb5] "v"(gb[5]), [gb6] "v"(gb[6]), [gb7] "v"(gb[7])
+                 : MLT_W4_CLOBBERS_ANBN, "memory");
   }
 
   w4_epilogue<OutT, EK>(C, ldc, epi, epi.alpha, m0, n0, w, lane, smem);
@@ -261,28 +272,57 @@ __global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __rest
 // the next tile's DMAs issued behind the previous epilogue's stores -- measured slower on the K =
 // 768 shapes and at 8192^3: 950 vs 988 TF (QKV), 1,531 vs 1,618 TF; with one workgroup per tile
 // the dispatcher plus the XCD remap keeps each XCD on one contiguous run of tile ids.)
-template <typename OutT, int EK, bool BN>
+template <typename OutT, int EK, bool AN, bool BN>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                         OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                         int64_t ldb, int64_t ldc, GemmEpi epi, int group_m) {
+                                                         OutT* __restrict__ C, int M, int N, int nk, int ksteps,
+                                                         int64_t lda, int64_t ldb, int64_t ldc, int64_t cstride,
+                                                         GemmEpi epi, int group_m) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = M >> 8, tiles_n = N >> 8;
   const int gm_ = group_m > 0 ? group_m : tiles_m;
-  gemm_w4_tile<OutT, EK, BN>(A, B, C, K, lda, ldb, ldc, epi, xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
+  // split z = blockIdx.y: K-tiles [z * ksteps, min(nk, (z + 1) * ksteps)), output slab z (cstride)
+  const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);
+  gemm_w4_tile<OutT, EK, AN, BN>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 64, lda, ldb, ldc, epi,
+                                 xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
 }
 
-template <typename OutT, int EK, bool BN>
+template <typename OutT, int EK, bool AN, bool BN>
 static void launch_w4_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+                         int64_t ldc, const GemmEpi& e, int group_m, int splits, int ksteps, int64_t cstride,
+                         hipStream_t st) {
   constexpr int SMEM = kW4Smem;
-  auto kern = gemm_w4_kernel<OutT, EK, BN>;
+  auto kern = gemm_w4_kernel<OutT, EK, AN, BN>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
   const int tiles = (M / 256) * (N / 256);
-  hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e, group_m);
+  hipLaunchKernelGGL(kern, dim3(tiles, splits), dim3(256), SMEM, st, A, B, C, M, N, K / 64, ksteps, lda, ldb, ldc,
+                     cstride, e, group_m);
+}
+
+template <typename OutT, bool AN, bool BN>
+static void launch_w4_bn(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+  const int nk = K / 64;
+  if (e.mode == 1)
+    launch_w4_ek<OutT, W4_GELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+  else if (e.mode == 2)
+    launch_w4_ek<OutT, W4_DGELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+  else if (e.res)
+    launch_w4_ek<OutT, W4_RES, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+  else
+    launch_w4_ek<OutT, W4_PLAIN, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+}
+
+template <typename OutT>
+void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                    int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st) {
+  if (b_mn)
+    launch_w4_bn<OutT, false, true>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  else
+    launch_w4_bn<OutT, false, false>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
 }
 
 bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes, const GemmEpi& e,
@@ -301,26 +341,32 @@ bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ld
   return true;
 }
 
-template <typename OutT, bool BN>
-static void launch_w4_bn(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
-  if (e.mode == 1)
-    launch_w4_ek<OutT, W4_GELU, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else if (e.mode == 2)
-    launch_w4_ek<OutT, W4_DGELU, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else if (e.res)
-    launch_w4_ek<OutT, W4_RES, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else
-    launch_w4_ek<OutT, W4_PLAIN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-}
-
+// weight-gradient layout (A [K][M], B [K][N]): split-K raw fp32 partials ws[z][M][N] (the caller's
+// split-reduce applies alpha / bias / accumulate), or (splits == 1) straight through the epilogue
 template <typename OutT>
-void launch_gemm_w4(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                    int64_t ldc, const GemmEpi& e, int group_m, bool b_mn, hipStream_t st) {
-  if (b_mn)
-    launch_w4_bn<OutT, true>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else
-    launch_w4_bn<OutT, false>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+void launch_gemm_w4_wgrad(const uint8_t* A, const uint8_t* B, OutT* C, float* ws, int M, int N, int K, int64_t lda,
+                          int64_t ldb, int64_t ldc, const GemmEpi& e, int group_m, int splits, int ksteps,
+                          hipStream_t st) {
+  if (splits > 1) {
+    GemmEpi raw{};
+    raw.alpha = 1.f;
+    launch_w4_ek<float, W4_PLAIN, true, true>(A, B, ws, M, N, K, lda, ldb, N, raw, group_m, splits, ksteps,
+                                              (int64_t)M * N, st);
+  } else {
+    launch_w4_bn<OutT, true, true>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  }
+}
+bool gemm_w4_wgrad_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
+                             const GemmEpi& e, int splits, int ksteps) {
+  const int nk = K / 64;
+  if (M % 256 || N % 256 || K % 64 || splits < 1 || ksteps % 2 || ksteps < 4) return false;
+  if ((int64_t)(splits - 1) * ksteps >= nk) return false;
+  const int last = nk - (splits - 1) * ksteps;
+  if (last % 2 || last < 4 || last > ksteps) return false;
+  if ((lda * 2) % 16 || (ldb * 2) % 16 || lda < M || ldb < N) return false;
+  if (lda * 2 * 64 > (int64_t)1 << 31 || ldb * 2 * 64 > (int64_t)1 << 31) return false;
+  if (splits > 1) return N % 4 == 0;  // the raw partials; the split-reduce handles the epilogue
+  return gemm_w4_supported(M, N, K, lda, ldb, ldc, out_bytes, e, true) && !e.accumulate;
 }
 
 template <typename OutT, int EK, int FA, int FB>
@@ -377,5 +423,9 @@ template void launch_gemm_w4<uint16_t>(const uint8_t*, const uint8_t*, uint16_t*
                                        int64_t, const GemmEpi&, int, bool, hipStream_t);
 template void launch_gemm_w4<float>(const uint8_t*, const uint8_t*, float*, int, int, int, int64_t, int64_t, int64_t,
                                     const GemmEpi&, int, bool, hipStream_t);
+template void launch_gemm_w4_wgrad<float>(const uint8_t*, const uint8_t*, float*, float*, int, int, int, int64_t,
+                                          int64_t, int64_t, const GemmEpi&, int, int, int, hipStream_t);
+template void launch_gemm_w4_wgrad<uint16_t>(const uint8_t*, const uint8_t*, uint16_t*, float*, int, int, int, int64_t,
+                                             int64_t, int64_t, const GemmEpi&, int, int, int, hipStream_t);
 
 }  // namespace mlt

@@ -47,23 +47,25 @@ def mfma(fset, k, zero_c=False):
     return f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {frag(fset, 'B', j)}, {frag(fset, 'A', i)}, {c}"
 
 
-def read(fset, idx, stage, kh, bn=False):
+def read(fset, idx, stage, kh, bn=False, an=False):
     """idx 0..7: A fragment idx, 8..15: B fragment idx - 8 (kh fragments of `stage`). With bn (B
     stored [k][n], n-contiguous: the dgrad layout) a B fragment is two ds_read_b64_tr_b16 (k rows
-    kh*32 + 8g + q and + 4) from the per-fragment lane address v[192 + 8 stage + j]."""
+    kh*32 + 8g + q and + 4) from the per-fragment lane address v[192 + 8 stage + j]; with an (A stored
+    [k][m]: the weight-gradient layout) the same for A from v[208 + 8 stage + i]."""
     ab = "A" if idx < 8 else "B"
     n = idx % 8
-    if ab == "B" and bn:
-        base = 64 * fset + 32 + 4 * n
-        off = B_OFF + kh * 16384
-        return [f"ds_read_b64_tr_b16 v[{base}:{base + 1}], v{192 + 8 * stage + n} offset:{off}",
-                f"ds_read_b64_tr_b16 v[{base + 2}:{base + 3}], v{192 + 8 * stage + n} offset:{off + 2048}"]
+    if (ab == "B" and bn) or (ab == "A" and an):
+        base = 64 * fset + (32 if ab == "B" else 0) + 4 * n
+        off = (B_OFF if ab == "B" else 0) + kh * 16384
+        areg = (192 if ab == "B" else 208) + 8 * stage + n
+        return [f"ds_read_b64_tr_b16 v[{base}:{base + 1}], v{areg} offset:{off}",
+                f"ds_read_b64_tr_b16 v[{base + 2}:{base + 3}], v{areg} offset:{off + 2048}"]
     reg = f"%[r{ab.lower()}{stage}{kh}]"
     return [f"ds_read_b128 {frag(fset, ab, n)}, {reg} offset:{n * 2048}"]
 
 
-def reads(fset, stage, kh, bn):
-    return [r for idx in range(16) for r in read(fset, idx, stage, kh, bn)]
+def reads(fset, stage, kh, bn, an=False):
+    return [r for idx in range(16) for r in read(fset, idx, stage, kh, bn, an)]
 
 
 def glds(p, stage):
@@ -75,19 +77,20 @@ def glds(p, stage):
     return [f"s_add_u32 m0, %[lw], {imm}", f"global_load_lds_dwordx4 %[g{ab}{q}], {sp}"]
 
 
-def adv(bn):
-    """advance the DMA sources by one K-tile: 128 B of a k-contiguous row; 64 rows of an n-contiguous B"""
+def adv(bn, an=False):
+    """advance the DMA sources by one K-tile: 128 B of a k-contiguous row; 64 rows of an mn-contiguous one"""
+    a = "%[astep]" if an else "128"
     b = "%[bstep]" if bn else "128"
-    return ["s_add_u32 s88, s88, 128", "s_addc_u32 s89, s89, 0", f"s_add_u32 s90, s90, {b}", "s_addc_u32 s91, s91, 0"]
+    return [f"s_add_u32 s88, s88, {a}", "s_addc_u32 s89, s89, 0", f"s_add_u32 s90, s90, {b}", "s_addc_u32 s91, s91, 0"]
 
 
-def phase_x(stage, out, bn, zero_c=False):
+def phase_x(stage, out, bn, zero_c=False, an=False):
     """64 MFMAs on F0; the tile's kh1 fragments -> F1, one read per MFMA gap from the start (16
-    ds_read_b128, or 8 + 16 transposed reads with bn)."""
-    rd = reads(1, stage, 1, bn)
+    ds_read_b128, 8 + 16 with transposed B, 32 with both transposed)."""
+    rd = reads(1, stage, 1, bn, an)
     for k in range(64):
         out.append(mfma(0, k, zero_c))
-        if bn:
+        if bn or an:
             if k < len(rd):
                 out.append(rd[k])
         elif k % 2 == 0 and k < 32:
@@ -99,61 +102,72 @@ def sync(out):
     out.append("s_barrier")
 
 
-def phase_y(stage, do_glds, do_reads, out, bn):
+def phase_y(stage, do_glds, do_reads, out, bn, an=False):
     """DMAs one per 4 MFMAs over the whole phase (each costs ~60 issue cycles beside the MFMAs, so
     bunching them in the first half stalled the MFMA stream: 1,494 vs 1,570 TF at 8192^3), reads
-    of the next tile's kh0 fragments one per odd MFMA gap."""
-    rd = reads(0, stage ^ 1, 0, bn) if do_reads else []
+    of the next tile's kh0 fragments one per odd MFMA gap (with both operands transposed, 32 reads:
+    the odd gaps below 48 and the gaps 2 mod 4 below 32, so the last lands well before the wait)."""
+    rd = reads(0, stage ^ 1, 0, bn, an) if do_reads else []
+    if an:
+        slots = sorted([k for k in range(1, 48, 2)] + [k for k in range(2, 32, 4)])
+    else:
+        slots = [k for k in range(1, 64, 2)]
+    at = {k: i for i, k in enumerate(slots)}
     for k in range(64):
         out.append(mfma(1, k))
         if do_glds and k % 4 == 0:
             out.extend(glds(k // 4, stage))
-        if k % 2 == 1 and k // 2 < len(rd):
-            out.append(rd[k // 2])
+        if k in at and at[k] < len(rd):
+            out.append(rd[at[k]])
     if do_glds:
-        out += adv(bn)
+        out += adv(bn, an)
     if do_reads:
         out.append("s_waitcnt lgkmcnt(0)")
 
 
-def build(bn=False):
+def build(bn=False, an=False):
     out = ["s_mov_b64 s[88:89], %[sa]", "s_mov_b64 s[90:91], %[sb]"]
     if bn:  # per-fragment transposed-read lane addresses: v[192 + j] = (32 j ^ X) + R, stage 1 + 64 KB
         for j in range(8):
             out.append(f"v_xor_b32 v{192 + j}, {32 * j}, %[rbx]")
             out.append(f"v_add_u32 v{192 + j}, v{192 + j}, %[rbr]")
             out.append(f"v_add_u32 v{200 + j}, 0x10000, v{192 + j}")
+    if an:  # the same for A (its own row / column base, the same XOR term)
+        for j in range(8):
+            out.append(f"v_xor_b32 v{208 + j}, {32 * j}, %[rbx]")
+            out.append(f"v_add_u32 v{208 + j}, v{208 + j}, %[rar]")
+            out.append(f"v_add_u32 v{216 + j}, 0x10000, v{208 + j}")
     # prologue: DMA tiles 0 / 1 into stages 0 / 1, F0 <- tile 0 kh0
     for t in range(2):
         for p in range(16):
             out.extend(glds(p, t))
-        out += adv(bn)
+        out += adv(bn, an)
     out.append("s_waitcnt vmcnt(16)")
     out.append("s_barrier")
-    out += reads(0, 0, 0, bn)
+    out += reads(0, 0, 0, bn, an)
     out.append("s_waitcnt lgkmcnt(0)")
     # first pair peeled (tile 0 starts from C = 0); np = nk / 2 - 2 more full pairs, then the last
-    phase_x(0, out, bn, zero_c=True)
+    phase_x(0, out, bn, zero_c=True, an=an)
     sync(out)
-    phase_y(0, True, True, out, bn)
-    phase_x(1, out, bn)
+    phase_y(0, True, True, out, bn, an)
+    phase_x(1, out, bn, an=an)
     sync(out)
-    phase_y(1, True, True, out, bn)
+    phase_y(1, True, True, out, bn, an)
     out += ["s_cmp_eq_u32 %[np], 0", "s_cbranch_scc1 L_w4_last_%="]
     out.append("L_w4_loop_%=:")
     for s in range(2):
-        phase_x(s, out, bn)
+        phase_x(s, out, bn, an=an)
         sync(out)
-        phase_y(s, True, True, out, bn)
+        phase_y(s, True, True, out, bn, an)
     out += ["s_sub_u32 %[np], %[np], 1", "s_cmp_lg_u32 %[np], 0", "s_cbranch_scc1 L_w4_loop_%="]
     out.append("L_w4_last_%=:")
     # last pair: no DMAs, no reads past the last tile
-    phase_x(0, out, bn)
+    phase_x(0, out, bn, an=an)
     sync(out)
-    phase_y(0, False, True, out, bn)
-    phase_x(1, out, bn)
+    phase_y(0, False, True, out, bn, an)
+    phase_x(1, out, bn, an=an)
     sync(out)
-    phase_y(1, False, False, out, bn)
+    phase_y(1, False, False, out, bn, an)
     # MFMA -> v_accvgpr_read hazard before the epilogue's reads
     out += ["s_nop 15", "s_nop 15", "s_nop 7"]
     return out
@@ -253,6 +267,9 @@ def main():
         f.write(f"#define MLT_W4_CLOBBERS {clob}\n")
         clob_bn = clob + ", " + ", ".join(f'"v{r}"' for r in range(192, 208))
         f.write(f"#define MLT_W4_CLOBBERS_BN {clob_bn}\n")
+        emit(f, "MLT_W4_LOOP_ASM_ANBN", build(bn=True, an=True))
+        clob_anbn = clob + ", " + ", ".join(f'"v{r}"' for r in range(192, 224))
+        f.write(f"#define MLT_W4_CLOBBERS_ANBN {clob_anbn}\n")
         emit(f, "MLT_W4F8_LOOP_ASM", build_f8())
         clob_f8 = ", ".join(f'"v{r}"' for r in range(193)) + ", " + ", ".join(f'"a{r}"' for r in range(256))
         clob_f8 += ', "s88", "s89", "s90", "s91", "m0", "scc"'

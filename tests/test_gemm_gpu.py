@@ -350,3 +350,30 @@ def test_w4_asm_kernel_repeatable_full_chip(dev, b_mn):
             first = out.clone()
         assert torch.equal(out, first)
     torch.testing.assert_close(first, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_w4_asm_wgrad_split_k(dev):
+    """Config 7 in the weight-gradient layout (A [K][M], B [K][N], both through transposed LDS reads)
+    with split-K raw partials + the external reduce (the planner's pick for few-tile long-K shapes),
+    fp32 accumulate and bf16 + bias outputs; a forced single split runs the epilogue in-kernel."""
+    C = require_native()
+    M, N, K = 768, 2304, 16384
+    g = torch.Generator().manual_seed(90)
+    A = _mk((K, M), dev, g)
+    B = _mk((K, N), dev, g)
+    ref = A.float().t() @ B.float()
+    plan = C.gemm_plan(True, True, M, N, K)
+    assert plan[0] == 7 and plan[1] > 1 and plan[4] == 1, plan
+    acc = torch.full((M, N), 0.25, device=dev)
+    C.gemm(A, B, acc, True, True, accumulate=True)
+    torch.testing.assert_close(acc, ref + 0.25, rtol=1e-4, atol=2e-3)
+    bias = torch.randn(N, device=dev)
+    o16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm(A, B, o16, True, True, bias=bias)
+    torch.testing.assert_close(o16.float(), ref + bias, rtol=2e-2, atol=0.2)
+    one = torch.empty(M, N, device=dev)
+    C.gemm(A, B, one, True, True, cfg=7)
+    torch.testing.assert_close(one, ref, rtol=1e-4, atol=2e-3)
+    ref1 = torch.empty(M, N, device=dev)
+    C.gemm(A, B, ref1, True, True, cfg=1)
+    torch.testing.assert_close(acc - 0.25, ref1, rtol=1e-5, atol=1e-3)
