@@ -391,12 +391,16 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
                     reinterpret_cast<uintptr_t>(ap) % 16 == 0,
                 "colsum_out needs M % 256 == 0, N % 256 == 0, K % 64 == 0 and 16-byte aligned rows of C / aux");
     check_dev(*colsum_out, "colsum_out", at::kFloat, N, 16);
-    cfg = 5;
+    // the 4-wave kernel (cfg 7) when the planner takes it (its epilogue writes the same per-64-row
+    // partials), else the ping-pong tile
+    if (cfg != 7 && !(cfg < 0 && plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, -1, 0).cfg == 7)) cfg = 5;
+    else cfg = 7;
     splits = 1;
     part = at::empty({M / 64 * N}, A.options().dtype(at::kFloat));
   }
   const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
-  TORCH_CHECK(!part.defined() || (plan.cfg == 5 && plan.splits == 1), "colsum_out: ping-pong plan expected");
+  TORCH_CHECK(!part.defined() || ((plan.cfg == 5 || plan.cfg == 7) && plan.splits == 1),
+              "colsum_out: ping-pong / 4-wave plan expected");
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, A.options().dtype(at::kFloat));
   launch_gemm_bf16(plan, a_mn, b_mn, C.scalar_type() == at::kFloat, bf16_ptr(A), bf16_ptr(B), C.data_ptr(), (int)M,

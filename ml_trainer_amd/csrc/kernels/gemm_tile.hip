@@ -870,8 +870,28 @@ constexpr int kGroupM = 4;
 // split-K tiles win (the fp8 weight gradients of the `large` config: 16-256 tiles at K = 256K
 // tokens ran 1,064 -> 621 samples/s end to end when cfg 7 took them)
 constexpr int kW4MinTiles = 240;
-// one workgroup's 256 x 256 x 64 K-tile at ~1.4 PF / 256 CUs (planner model for the split choice)
+// one workgroup's 256 x 256 x 64 K-tile at ~1.4 PF / 256 CUs (planner model for the split choice;
+// the fp8 K-tile of 128 takes the same cycles)
 constexpr double kW4KtileSec = 2.0 * 256 * 256 * 64 / (1.4e15 / 256);
+// split count for cfg 7 over nk K-tiles: rounds of workgroups x K-tiles each + the partials' traffic
+void w4_pick_splits(int tiles, int nk, int M, int N, int& bs, int& bks) {
+  double best = 1e30;
+  bs = bks = 0;
+  for (int S = 1; S <= 64; ++S) {
+    int ks = (nk + S - 1) / S;
+    ks += ks & 1;
+    if (ks < 4) break;
+    const int last = nk - (S - 1) * ks;
+    if (last < 4 || last % 2) continue;
+    const int64_t rounds = ((int64_t)tiles * S + kCUs - 1) / kCUs;
+    const double t = (double)rounds * ks * kW4KtileSec + (S > 1 ? (double)M * N * 4.0 * (S + 1) / 5.0e12 + 3.0e-6 : 0.0);
+    if (t < best) {
+      best = t;
+      bs = S;
+      bks = ks;
+    }
+  }
+}
 
 GemmPlan plan_tiles(int M, int N, int K, int force_cfg, int force_splits, int kstep, bool allow_legacy,
                     bool allow_pp = true, bool allow_persist = true) {
@@ -1039,12 +1059,17 @@ void launch_cfg(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, 
         launch_tile<256, 256, 2, AM, BNL, OutT, F8A, F8B>(p, A, B, C, M, N, K, lda, ldb, ldc, e, ws, cnt, st);
         break;
       } else if constexpr (!AM && !BNL && F8A >= 0 && (sizeof(OutT) == 2 || sizeof(OutT) == 4)) {
+        static const int group_m = [] {
+          const char* v = getenv("MLT_GEMM_GROUP_M");
+          return v ? atoi(v) : kGroupM;
+        }();
         if (p.splits == 1 && gemm_w4_f8_supported(M, N, K, lda, ldb, ldc, (int)sizeof(OutT), e)) {
-          static const int group_m = [] {
-            const char* v = getenv("MLT_GEMM_GROUP_M");
-            return v ? atoi(v) : kGroupM;
-          }();
           launch_gemm_w4_f8<OutT, F8A, F8B>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+          break;
+        }
+        if (p.splits > 1 && ws != nullptr && cnt == nullptr &&
+            gemm_w4_f8_splitk_supported(M, N, K, lda, ldb, p.splits, p.ksteps)) {
+          launch_gemm_w4_f8_splitk<F8A, F8B>(A, B, ws, M, N, K, lda, ldb, group_m, p.splits, p.ksteps, st);
           break;
         }
       }
@@ -1102,23 +1127,8 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
   // partials reduced by one grid-wide launch; splits from a rounds x K-steps + reduce-traffic model
   if (w4 && force_cfg < 0 && force_splits <= 0 && a_mn == 1 && b_mn == 1 && M % 256 == 0 && N % 256 == 0 &&
       K % 128 == 0 && K >= 256) {
-    const int tiles = (M / 256) * (N / 256), nk = K / 64;
-    double best = 1e30;
     int bs = 0, bks = 0;
-    for (int S = 1; S <= 64; ++S) {
-      int ks = (nk + S - 1) / S;
-      ks += ks & 1;
-      if (ks < 4) break;
-      const int last = nk - (S - 1) * ks;
-      if (last < 4 || last % 2) continue;
-      const int64_t rounds = ((int64_t)tiles * S + kCUs - 1) / kCUs;
-      const double t = (double)rounds * ks * kW4KtileSec + (S > 1 ? (double)M * N * 4.0 * (S + 1) / 5.0e12 + 3.0e-6 : 0.0);
-      if (t < best) {
-        best = t;
-        bs = S;
-        bks = ks;
-      }
-    }
+    w4_pick_splits((M / 256) * (N / 256), K / 64, M, N, bs, bks);
     if (bs) {
       GemmPlan p{7, bs, bks, bs > 1 ? (int64_t)bs * M * N : 0, 0};
       p.ext = bs > 1 ? 1 : 0;
@@ -1141,6 +1151,17 @@ GemmPlan plan_gemm_f8(int M, int N, int K, int force_cfg, int force_splits) {
       (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
     GemmPlan p{7, 1, K / 128, 0, 0};
     return p;
+  }
+  // few tiles, long K (the fp8 weight gradients): cfg 7 split-K raw partials + the external reduce
+  if (w4 && force_cfg < 1 && force_splits <= 0 && M % 256 == 0 && N % 256 == 0 && N % 4 == 0 && K % 256 == 0 &&
+      K >= 1024) {
+    int bs = 0, bks = 0;
+    w4_pick_splits((M / 256) * (N / 256), K / 128, M, N, bs, bks);
+    if (bs > 1) {
+      GemmPlan p{7, bs, bks, (int64_t)bs * M * N, 0};
+      p.ext = 1;
+      return p;
+    }
   }
   GemmPlan p = plan_tiles(M, N, K, force_cfg < 1 ? -1 : force_cfg, force_splits, 128, false);
   if (p.cfg == 0) p.cfg = -1;  // not runnable (K % 128 != 0 or too small)
@@ -1216,6 +1237,24 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
   e.q_amax = out_amax;
   e.q_colpart = colpart;
   e.q_fmt = out_fmt;
+  // cfg 7's q8 epilogue (gemm_w4.hip) where the 4-wave kernel applies (K a multiple of 256)
+  static const bool w4 = [] {
+    const char* v = getenv("MLT_GEMM_W4");
+    const char* v8 = getenv("MLT_GEMM_W4F8");
+    const char* vq = getenv("MLT_GEMM_W4Q8");
+    return !(v && atoi(v) == 0) && !(v8 && atoi(v8) == 0) && !(vq && atoi(vq) == 0);
+  }();
+  if (w4 && K % 256 == 0 && K >= 512 && lda % 16 == 0 && ldb % 16 == 0 && ldy % 16 == 0 && ldyt % 16 == 0 &&
+      (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
+    if (fmt_a == 0 && fmt_b == 0) {
+      launch_gemm_w4_f8_q<0, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st);
+      return;
+    }
+    if (fmt_a == 1 && fmt_b == 0) {
+      launch_gemm_w4_f8_q<1, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st);
+      return;
+    }
+  }
   GemmPlan p{5, 1, K / 128, 0, 0};
   if (fmt_a == 0 && fmt_b == 0)
     launch_pp<false, false, uint8_t, 0, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);

@@ -22,11 +22,12 @@
 #include "mlt_common.h"
 #include "mlt_gemm.h"
 #include "mlt_gemm_tile.h"
+#include "mlt_fp8.h"
 #include "gemm_w4_loop.inc"
 
 namespace mlt {
 
-enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
+enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3, W4_Q8 = 8 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // LDS: two K-tile stages of 64 KB; after the loop, four per-wave 64 x 132 fp32 epilogue images
@@ -40,7 +41,7 @@ constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 
 // columns per lane: 32 x 16-byte stores per lane (bf16), side operands as 16-byte loads.
 template <typename OutT, int EK>
 __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, const GemmEpi& epi, float alpha, int m0,
-                                            int n0, int w, int lane, uint8_t* smem) {
+                                            int n0, int N, int w, int lane, uint8_t* smem) {
   const int wr = w >> 1, wc = w & 1, g = lane >> 4, rl = lane & 15;
   __syncthreads();  // every wave is past its last read of the K-tile stages
   constexpr int P = kW4Pitch;
@@ -80,6 +81,9 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
+    float csum[8];  // dGELU + q_colpart: the half's column sums (bias gradient of the dGELU output)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
@@ -107,6 +111,10 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
           else
             v[e] *= gelu_grad(x);
         }
+        if constexpr (EK == W4_DGELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += v[e];
+        }
       }
       OutT* cp = C + (int64_t)gm * ldc + gn;
       if constexpr (sizeof(OutT) == 4) {
@@ -118,7 +126,140 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
                        pack2(f32_to_bf16(v[4]), f32_to_bf16(v[5])), pack2(f32_to_bf16(v[6]), f32_to_bf16(v[7])));
       }
     }
+    if constexpr (EK == W4_DGELU) {
+      if (epi.q_colpart) {  // the 4 lanes of a column group (rsub) hold 16 rows each: one 64-row block
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          csum[e] += __shfl_xor(csum[e], 16);
+          csum[e] += __shfl_xor(csum[e], 32);
+        }
+        if (rsub == 0) {
+          float* cp = epi.q_colpart + (int64_t)((m0 + wr * 128 + 64 * h) >> 6) * N + gn;
+          *reinterpret_cast<float4*>(cp) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+        }
+      }
+    }
     if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
+  }
+}
+
+// ---- quantising ("q8") epilogue of the fp8 form: the output as fp8 C [M][N] AND its transpose C^T
+// [N][M] (the consumer GEMM's k-contiguous operand), amax of the unscaled output, optionally the
+// column partial sums per 64-row block (the bias gradient) -- gemm_tile.hip's q8 semantics. Per
+// wave and 64-row half, through the fp32 LDS image: a row pass (8 columns per lane: bias, GELU with
+// the bf16 pre-activation saved / dGELU, amax, scale, one 8-byte fp8 store; the scaled values go
+// back into the image) and a column pass (2 adjacent columns per lane, 16 rows per ds_read_b64
+// sweep: 16-byte fp8 stores of C^T rows, the column sums).
+template <int MODE, int FMT>
+__device__ __forceinline__ void w4_epilogue_q8(uint8_t* __restrict__ C, int64_t ldc, const GemmEpi& epi, float alpha,
+                                               int m0, int n0, int N, int w, int lane, uint8_t* smem) {
+  const int wr = w >> 1, wc = w & 1, g = lane >> 4, rl = lane & 15;
+  __syncthreads();  // every wave is past its last read of the K-tile stages
+  constexpr int P = kW4Pitch;
+  float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
+  const float s = *epi.q_scale;
+  const int rsub = lane >> 4, cc = lane & 15;
+  const int gn = n0 + wc * 128 + 8 * cc;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+  if (epi.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(epi.bias + gn);
+    const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
+    bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
+  }
+  float amx = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x0, x1, x2, x3;
+        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
+        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint4 sd[16];
+    if constexpr (MODE == 2) {  // dGELU pre-activations of the half first
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
+        sd[it] = *reinterpret_cast<const uint4*>(epi.aux + (int64_t)gm * epi.ldaux + gn);
+      }
+    }
+    // row pass
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
+      float* ip = img + row * P + 8 * cc;
+      const float4 lo = *reinterpret_cast<const float4*>(ip);
+      const float4 hi = *reinterpret_cast<const float4*>(ip + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
+      if constexpr (MODE == 1) {  // GELU: save the bf16 pre-activation, activate its rounded value
+        *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) = pack_bf16x8(v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_f(bf16_to_f32(f32_to_bf16(v[e])));
+      } else if constexpr (MODE == 2) {
+        const uint32_t wv[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] *= gelu_grad(__uint_as_float(wv[q] << 16));
+          v[2 * q + 1] *= gelu_grad(__uint_as_float(wv[q] & 0xffff0000u));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        amx = fmaxf(amx, fabsf(v[e]));
+        v[e] *= s;  // the image keeps the SCALED values: the column pass only converts
+      }
+      *reinterpret_cast<float4*>(ip) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(ip + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      *reinterpret_cast<uint2*>(C + (int64_t)gm * ldc + gn) =
+          make_uint2(pack4_fp8<FMT>(v[0], v[1], v[2], v[3]), pack4_fp8<FMT>(v[4], v[5], v[6], v[7]));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // column pass: lane -> columns 2 lane, 2 lane + 1 of the wave's 128; 4 sweeps of 16 rows
+    const int gc = n0 + wc * 128 + 2 * lane, gm0 = m0 + wr * 128 + 64 * h;
+    float cs0 = 0.f, cs1 = 0.f;
+#pragma unroll
+    for (int sw4 = 0; sw4 < 4; ++sw4) {
+      float a[16], b[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float2 t = *reinterpret_cast<const float2*>(img + (16 * sw4 + r) * P + 2 * lane);
+        a[r] = t.x;
+        b[r] = t.y;
+      }
+      if (epi.q_colpart) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          cs0 += a[r];
+          cs1 += b[r];
+        }
+      }
+      uint32_t pa[4], pb[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pa[q] = pack4_fp8<FMT>(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+        pb[q] = pack4_fp8<FMT>(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+      }
+      *reinterpret_cast<uint4*>(epi.qt + (int64_t)gc * epi.ldqt + gm0 + 16 * sw4) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
+      *reinterpret_cast<uint4*>(epi.qt + (int64_t)(gc + 1) * epi.ldqt + gm0 + 16 * sw4) =
+          make_uint4(pb[0], pb[1], pb[2], pb[3]);
+    }
+    if (epi.q_colpart) {  // column sums of the unscaled output over this 64-row block
+      const float inv = __builtin_amdgcn_rcpf(s);
+      *reinterpret_cast<float2*>(epi.q_colpart + (int64_t)(gm0 >> 6) * N + gc) = make_float2(cs0 * inv, cs1 * inv);
+    }
+    if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
+  }
+  if (epi.q_amax) {
+    amx = wave_max(amx);
+    if (lane == 0) atomic_max_pos(epi.q_amax, amx);
   }
 }
 
@@ -205,7 +346,7 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
                  : MLT_W4_CLOBBERS_ANBN, "memory");
   }
 
-  w4_epilogue<OutT, EK>(C, ldc, epi, epi.alpha, m0, n0, w, lane, smem);
+  w4_epilogue<OutT, EK>(C, ldc, epi, epi.alpha, m0, n0, tiles_n * 256, w, lane, smem);
 }
 
 // fp8 operands (OCP e4m3 = 0 / e5m2 = 1 each; A [M][K], B [N][K] bytes): the block-scaled MFMA with
@@ -213,9 +354,9 @@ __device__ __forceinline__ void gemm_w4_tile(const uint8_t* __restrict__ A, cons
 // bytes (chunks 2g and 2g + 1 of its row). Main loop: MLT_W4F8_LOOP_ASM (scripts/gen_gemm_w4.py).
 template <typename OutT, int EK, int FA, int FB>
 __device__ __forceinline__ void gemm_w4f8_tile(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                               OutT* __restrict__ C, int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                               const GemmEpi& epi, int id, int gm_, int tiles_m, int tiles_n,
-                                               uint8_t* smem) {
+                                               OutT* __restrict__ C, int nkt, int64_t kz, int64_t lda, int64_t ldb,
+                                               int64_t ldc, const GemmEpi& epi, int id, int gm_, int tiles_m,
+                                               int tiles_n, uint8_t* smem) {
   const int per_group = gm_ * tiles_n, grp = id / per_group, first_m = grp * gm_;
   const int gsize = min(tiles_m - first_m, gm_), rr = id - grp * per_group;
   const int m0 = (first_m + rr % gsize) * 256, n0 = (rr / gsize) * 256;
@@ -238,10 +379,10 @@ __device__ __forceinline__ void gemm_w4f8_tile(const uint8_t* __restrict__ A, co
     ga[p] = (uint32_t)(r * lda + kc * 16);
     gb[p] = (uint32_t)(r * ldb + kc * 16);
   }
-  const uint64_t sa = (uint64_t)(uintptr_t)(A + (int64_t)m0 * lda);
-  const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * ldb);
+  const uint64_t sa = (uint64_t)(uintptr_t)(A + (int64_t)m0 * lda + kz);
+  const uint64_t sb = (uint64_t)(uintptr_t)(B + (int64_t)n0 * ldb + kz);
   const uint32_t lw = __builtin_amdgcn_readfirstlane(lds0 + w * 1024);
-  int np = (K >> 8) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
+  int np = (nkt >> 1) - 2;  // full K-tile pairs of the loop (the first and the last pair are peeled)
   asm volatile(MLT_W4F8_LOOP_ASM
                : [np] "+s"(np)
                : [sa] "s"(sa), [sb] "s"(sb), [lw] "s"(lw), [raL0] "v"(raL0), [raH0] "v"(raH0), [raL1] "v"(raL1),
@@ -254,18 +395,24 @@ __device__ __forceinline__ void gemm_w4f8_tile(const uint8_t* __restrict__ A, co
   float alpha = epi.alpha;
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
-  w4_epilogue<OutT, EK>(C, ldc, epi, alpha, m0, n0, w, lane, smem);
+  if constexpr (EK >= W4_Q8)  // EK = W4_Q8 + 3 * out fmt + mode
+    w4_epilogue_q8<(EK - W4_Q8) % 3, (EK - W4_Q8) / 3>(reinterpret_cast<uint8_t*>(C), ldc, epi, alpha, m0, n0,
+                                                        tiles_n * 256, w, lane, smem);
+  else
+    w4_epilogue<OutT, EK>(C, ldc, epi, alpha, m0, n0, tiles_n * 256, w, lane, smem);
 }
 
 template <typename OutT, int EK, int FA, int FB>
 __global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                           OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                           int64_t ldb, int64_t ldc, GemmEpi epi, int group_m) {
+                                                           OutT* __restrict__ C, int M, int N, int nk, int ksteps,
+                                                           int64_t lda, int64_t ldb, int64_t ldc, int64_t cstride,
+                                                           GemmEpi epi, int group_m) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = M >> 8, tiles_n = N >> 8;
   const int gm_ = group_m > 0 ? group_m : tiles_m;
-  gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C, K, lda, ldb, ldc, epi, xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m,
-                                   tiles_n, smem);
+  const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);  // split z (see gemm_w4_kernel)
+  gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 128, lda, ldb, ldc, epi,
+                                   xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
 }
 
 // One tile per workgroup. (A persistent variant -- one workgroup per CU walking id, id + 256, ...,
@@ -334,7 +481,8 @@ bool gemm_w4_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ld
   if ((lda * 2) % 16 || (ldb * 2) % 16 || (ldc * out_bytes) % 16) return false;
   if (lda * 2 * 256 > (int64_t)1 << 31 || ldb * 2 * 256 > (int64_t)1 << 31) return false;  // 32-bit DMA offsets
   if (b_mn && (N % 8 || ldb < N)) return false;
-  if (e.accumulate || e.inv_scale_a || e.inv_scale_b || e.q_colpart || e.qt || e.mode == 3) return false;
+  if (e.accumulate || e.inv_scale_a || e.inv_scale_b || e.qt || e.mode == 3) return false;
+  if (e.q_colpart && e.mode != 2) return false;  // column partials: the dGELU epilogue only
   if (!al(e.res, e.ldres, 2) || !al(e.aux, e.ldaux, 2) || (e.bias && ((uintptr_t)e.bias) % 16)) return false;
   if (out_bytes == 4 && (e.mode != 0 || e.res)) return false;
   if (e.mode != 0 && e.res) return false;
@@ -371,7 +519,8 @@ bool gemm_w4_wgrad_supported(int M, int N, int K, int64_t lda, int64_t ldb, int6
 
 template <typename OutT, int EK, int FA, int FB>
 static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                           int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
+                           int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st, int splits = 1, int ksteps = 0,
+                           int64_t cstride = 0) {
   constexpr int SMEM = kW4Smem;
   auto kern = gemm_w4f8_kernel<OutT, EK, FA, FB>;
   static bool attr_set = false;
@@ -379,8 +528,8 @@ static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, i
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((M / 256) * (N / 256)), dim3(256), SMEM, st, A, B, C, M, N, K, lda, ldb, ldc, e,
-                     group_m);
+  hipLaunchKernelGGL(kern, dim3((M / 256) * (N / 256), splits), dim3(256), SMEM, st, A, B, C, M, N, K / 128,
+                     ksteps > 0 ? ksteps : K / 128, lda, ldb, ldc, cstride, e, group_m);
 }
 template <typename OutT, int FA, int FB>
 void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
@@ -394,6 +543,49 @@ void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N
   else
     launch_w4f8_ek<OutT, W4_PLAIN, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
 }
+// split-K raw fp32 partials ws[z][M][N] (alpha, the fp8 inverse scales and the epilogue are the
+// split-reduce's): the fp8 weight gradients (few tiles, K = tokens)
+template <int FA, int FB>
+void launch_gemm_w4_f8_splitk(const uint8_t* A, const uint8_t* B, float* ws, int M, int N, int K, int64_t lda,
+                              int64_t ldb, int group_m, int splits, int ksteps, hipStream_t st) {
+  GemmEpi raw{};
+  raw.alpha = 1.f;
+  launch_w4f8_ek<float, W4_PLAIN, FA, FB>(A, B, ws, M, N, K, lda, ldb, N, raw, group_m, st, splits, ksteps,
+                                          (int64_t)M * N);
+}
+template void launch_gemm_w4_f8_splitk<0, 0>(const uint8_t*, const uint8_t*, float*, int, int, int, int64_t, int64_t,
+                                              int, int, int, hipStream_t);
+template void launch_gemm_w4_f8_splitk<1, 0>(const uint8_t*, const uint8_t*, float*, int, int, int, int64_t, int64_t,
+                                              int, int, int, hipStream_t);
+template void launch_gemm_w4_f8_splitk<0, 1>(const uint8_t*, const uint8_t*, float*, int, int, int, int64_t, int64_t,
+                                              int, int, int, hipStream_t);
+bool gemm_w4_f8_splitk_supported(int M, int N, int K, int64_t lda, int64_t ldb, int splits, int ksteps) {
+  const int nk = K / 128;
+  if (M % 256 || N % 256 || K % 128 || splits < 2 || ksteps % 2 || ksteps < 4 || N % 4) return false;
+  if ((int64_t)(splits - 1) * ksteps >= nk) return false;
+  const int last = nk - (splits - 1) * ksteps;
+  if (last % 2 || last < 4 || last > ksteps) return false;
+  if (lda % 16 || ldb % 16 || lda * 256 > (int64_t)1 << 31 || ldb * 256 > (int64_t)1 << 31) return false;
+  return true;
+}
+
+// the quantising epilogue (fp8 Y, Y^T, amax, column partials): Y / Yt as uint8, mode 0 / 1 / 2
+template <int FA, int FB>
+void launch_gemm_w4_f8_q(const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st) {
+#define MLT_W4Q8(MODE, FMT)                                                                                       \
+  if (e.mode == MODE && e.q_fmt == FMT) {                                                                         \
+    launch_w4f8_ek<uint8_t, W4_Q8 + 3 * FMT + MODE, FA, FB>(A, B, Y, M, N, K, lda, ldb, ldy, e, group_m, st);  \
+    return;                                                                                                       \
+  }
+  MLT_W4Q8(0, 0) MLT_W4Q8(1, 0) MLT_W4Q8(2, 0) MLT_W4Q8(0, 1) MLT_W4Q8(1, 1) MLT_W4Q8(2, 1)
+#undef MLT_W4Q8
+}
+template void launch_gemm_w4_f8_q<0, 0>(const uint8_t*, const uint8_t*, uint8_t*, int, int, int, int64_t, int64_t,
+                                        int64_t, const GemmEpi&, int, hipStream_t);
+template void launch_gemm_w4_f8_q<1, 0>(const uint8_t*, const uint8_t*, uint8_t*, int, int, int, int64_t, int64_t,
+                                        int64_t, const GemmEpi&, int, hipStream_t);
+
 bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
                           const GemmEpi& e) {
   auto al = [](const void* p, int64_t ld, int esz) {
@@ -402,7 +594,8 @@ bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t
   if (M % 256 || N % 256 || K % 256 || K < 512) return false;
   if (lda % 16 || ldb % 16 || (ldc * out_bytes) % 16) return false;
   if (lda * 256 > (int64_t)1 << 31 || ldb * 256 > (int64_t)1 << 31) return false;
-  if (e.accumulate || e.q_colpart || e.qt || e.mode == 3) return false;
+  if (e.accumulate || e.qt || e.mode == 3) return false;
+  if (e.q_colpart && e.mode != 2) return false;
   if (!al(e.res, e.ldres, 2) || !al(e.aux, e.ldaux, 2) || (e.bias && ((uintptr_t)e.bias) % 16)) return false;
   if (out_bytes == 4 && (e.mode != 0 || e.res)) return false;
   if (e.mode != 0 && e.res) return false;

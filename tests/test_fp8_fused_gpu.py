@@ -27,7 +27,8 @@ def _gelu_grad(x):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("shape", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024)])
+@pytest.mark.parametrize("shape", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024),
+                                   (8192, 2048, 512), (4096, 4096, 1024)])  # the last two: cfg 7 (>= 240 tiles)
 def test_gemm_f8_q_matches_fp32(dev, mode, shape):
     C = require_native()
     M, N, K = shape

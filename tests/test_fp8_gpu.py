@@ -272,7 +272,8 @@ def test_gemm_f8_w4_asm(dev, fmts):
     B = _rand_f8((N, K), fb, g, dev, 4.0)
     # the planner takes cfg 7 when the tiles fill the chip, split-K tiles for few-tile long-K shapes
     assert C.gemm_f8_plan(65536, 1024, 1024)[0] == 7
-    assert C.gemm_f8_plan(1024, 1024, 262144)[0] != 7
+    plan = C.gemm_f8_plan(1024, 1024, 262144)  # few tiles, long K: split-K partials (ext reduce)
+    assert plan[0] == 7 and plan[1] > 1 and plan[4] == 1, plan
     isa = torch.tensor([0.5], device=dev)
     isb = torch.tensor([0.25], device=dev)
     ref = (A.float() @ B.float().t()) * 0.125
@@ -303,3 +304,25 @@ def test_gemm_f8_w4_identity_asymmetric(dev):
     out = torch.empty(M, N, dtype=torch.float32, device=dev)
     C.gemm_f8(A, B, out, 0, 0, one, one, cfg=7)
     torch.testing.assert_close(out, B.float()[:, :M].t())
+
+
+def test_gemm_f8_w4_split_k(dev):
+    """cfg 7 fp8 with split-K raw partials and the external reduce (the fp8 weight-gradient path):
+    inverse scales, bias, fp32 accumulate and bf16 outputs against an fp32 reference."""
+    C = require_native()
+    M, N, K = 512, 768, 16384
+    plan = C.gemm_f8_plan(M, N, K)
+    assert plan[0] == 7 and plan[1] > 1 and plan[4] == 1, plan
+    g = torch.Generator().manual_seed(410)
+    A = _rand_f8((M, K), 1, g, dev, 2.0)
+    B = _rand_f8((N, K), 0, g, dev, 2.0)
+    isa = torch.tensor([0.5], device=dev)
+    isb = torch.tensor([0.25], device=dev)
+    ref = (A.float() @ B.float().t()) * 0.125
+    acc = torch.full((M, N), 0.5, device=dev)
+    C.gemm_f8(A, B, acc, 1, 0, isa, isb, accumulate=True)
+    torch.testing.assert_close(acc, ref + 0.5, rtol=2e-3, atol=2e-4 * ref.abs().max().item())
+    bias = torch.randn(N, device=dev)
+    ob = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C.gemm_f8(A, B, ob, 1, 0, isa, isb, bias=bias)
+    torch.testing.assert_close(ob.float(), ref + bias, rtol=1e-2, atol=0.5)

@@ -267,7 +267,8 @@ def test_persistent_kernel_repeatable_full_chip(dev):
 
 
 @pytest.mark.parametrize("b_mn", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 768)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 768),
+                                   (16384, 3072, 768)])  # the last: the 4-wave kernel's epilogue (cfg 7)
 def test_dgelu_colsum_fused(dev, b_mn, M, N, K):
     """dGELU epilogue with fused column sums (the bias gradient of the layer before the GELU):
     output and sums vs fp32 torch; set and accumulate modes."""
