@@ -1237,12 +1237,14 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
   e.q_amax = out_amax;
   e.q_colpart = colpart;
   e.q_fmt = out_fmt;
-  // cfg 7's q8 epilogue (gemm_w4.hip) where the 4-wave kernel applies (K a multiple of 256)
+  // cfg 7's q8 epilogue (gemm_w4.hip) only on request (MLT_GEMM_W4Q8=1): its GELU / fp8-pack VALU
+  // runs after the main loop with one wave per SIMD and measured slower than the ping-pong's in the
+  // fp8 `large` step (FFN1 forward 2.73 vs 2.43 ms, FFN2 dgrad 2.48 vs 2.33 ms per call at b512,
+  // profiles/r4/large_fp8_b512_kernel_stats_r4.csv)
   static const bool w4 = [] {
     const char* v = getenv("MLT_GEMM_W4");
-    const char* v8 = getenv("MLT_GEMM_W4F8");
     const char* vq = getenv("MLT_GEMM_W4Q8");
-    return !(v && atoi(v) == 0) && !(v8 && atoi(v8) == 0) && !(vq && atoi(vq) == 0);
+    return !(v && atoi(v) == 0) && (vq && atoi(vq) == 1);
   }();
   if (w4 && K % 256 == 0 && K >= 512 && lda % 16 == 0 && ldb % 16 == 0 && ldy % 16 == 0 && ldyt % 16 == 0 &&
       (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
