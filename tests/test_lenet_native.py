@@ -360,12 +360,17 @@ def test_pinned_prefetcher_overlaps_copy_and_compute(dev):
             pf.copy_to_device(k % d, bufs[k % d], nbytes)
             pf.acquire(k % d)
             pf.release(k % d)
+    # every time is the best of 3 trials: a shared box's PCIe / clock noise must not read as a
+    # missing overlap (the overlap itself is also traced: profiles/r4/prefetch_overlap_trace.txt)
+    def best(fn, k=3):
+        return min(timed(fn) for _ in range(k))
+
     timed(copies)
-    t_copy = timed(copies) / n
+    t_copy = best(copies) / n
     timed(lambda: compute(bufs[0], 4))
-    t_mm = timed(lambda: compute(bufs[0], 16)) / 16
+    t_mm = best(lambda: compute(bufs[0], 16)) / 16
     reps = max(4, int(round(t_copy / t_mm)))
-    t_comp = timed(lambda: [compute(bufs[k % d], reps) for k in range(n)]) / n
+    t_comp = best(lambda: [compute(bufs[k % d], reps) for k in range(n)]) / n
 
     def pipeline():
         for k in range(d - 1):
@@ -379,7 +384,7 @@ def test_pinned_prefetcher_overlaps_copy_and_compute(dev):
             compute(bufs[k % d], reps)
             pf.release(k % d)
     timed(pipeline)
-    t_pipe = timed(pipeline) / n
+    t_pipe = best(pipeline) / n
     ratio = t_pipe / max(t_copy, t_comp)
     assert 0.4 < t_copy / t_comp < 2.5, (t_copy, t_comp)  # both sides matter
     assert ratio < 1.15, (t_pipe, t_copy, t_comp)
