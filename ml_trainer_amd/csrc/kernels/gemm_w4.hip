@@ -415,10 +415,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __rest
                                    xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
 }
 
-// One tile per workgroup. (A persistent variant -- one workgroup per CU walking id, id + 256, ...,
-// the next tile's DMAs issued behind the previous epilogue's stores -- measured slower on the K =
-// 768 shapes and at 8192^3: 950 vs 988 TF (QKV), 1,531 vs 1,618 TF; with one workgroup per tile
-// the dispatcher plus the XCD remap keeps each XCD on one contiguous run of tile ids.)
+// Persistent by default: 256 workgroups (one per CU), XCD x walking ITS contiguous run of tile ids
+// (the run xcd_remap gives it in a one-tile-per-workgroup launch, so the L2 reuse pattern is kept),
+// the next tile's DMAs issued right behind the previous epilogue's stores: +0.5-2 % per shape,
+// BERT-base 2,925 / 2,932 -> 2,945 / 2,956 (profiles/r4/gemm_w4_persist_xcd_ab.jsonl). (A first
+// persistent version striding ids by 256 broke that locality and lost: QKV 950 vs 988 TF.)
+// MLT_W4_PERSIST=0: one tile per workgroup.
 template <typename OutT, int EK, bool AN, bool BN>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                          OutT* __restrict__ C, int M, int N, int nk, int ksteps,
@@ -429,8 +431,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint8_t* __restri
   const int gm_ = group_m > 0 ? group_m : tiles_m;
   // split z = blockIdx.y: K-tiles [z * ksteps, min(nk, (z + 1) * ksteps)), output slab z (cstride)
   const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);
-  gemm_w4_tile<OutT, EK, AN, BN>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 64, lda, ldb, ldc, epi,
-                                 xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
+  const int T = tiles_m * tiles_n, G = gridDim.x;
+  if (G >= T) {
+    gemm_w4_tile<OutT, EK, AN, BN>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 64, lda, ldb, ldc, epi,
+                                   xcd_remap(blockIdx.x, G), gm_, tiles_m, tiles_n, smem);
+    return;
+  }
+  // persistent (G = 256 = 8 XCDs x 32): XCD x walks its contiguous run of tile ids
+  const int x = blockIdx.x % 8, l = blockIdx.x / 8, per = G / 8, q = T / 8, r = T % 8;
+  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, end = start + q + (x < r ? 1 : 0);
+  for (int id = start + l; id < end; id += per) {
+    if (id != start + l) __syncthreads();  // the previous epilogue's LDS reads are done
+    gemm_w4_tile<OutT, EK, AN, BN>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 64, lda, ldb, ldc, epi, id,
+                                   gm_, tiles_m, tiles_n, smem);
+  }
 }
 
 template <typename OutT, int EK, bool AN, bool BN>
@@ -445,7 +459,12 @@ static void launch_w4_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int
     attr_set = true;
   }
   const int tiles = (M / 256) * (N / 256);
-  hipLaunchKernelGGL(kern, dim3(tiles, splits), dim3(256), SMEM, st, A, B, C, M, N, K / 64, ksteps, lda, ldb, ldc,
+  static const bool persist = [] {
+    const char* v = getenv("MLT_W4_PERSIST");
+    return !(v && atoi(v) == 0);
+  }();
+  const int grid = persist && splits == 1 && tiles > 256 ? 256 : tiles;
+  hipLaunchKernelGGL(kern, dim3(grid, splits), dim3(256), SMEM, st, A, B, C, M, N, K / 64, ksteps, lda, ldb, ldc,
                      cstride, e, group_m);
 }
 
