@@ -411,8 +411,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __rest
   const int tiles_m = M >> 8, tiles_n = N >> 8;
   const int gm_ = group_m > 0 ? group_m : tiles_m;
   const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);  // split z (see gemm_w4_kernel)
-  gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 128, lda, ldb, ldc, epi,
-                                   xcd_remap(blockIdx.x, gridDim.x), gm_, tiles_m, tiles_n, smem);
+  const int T = tiles_m * tiles_n, G = gridDim.x;
+  if (G >= T) {
+    gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 128, lda, ldb, ldc, epi,
+                                     xcd_remap(blockIdx.x, G), gm_, tiles_m, tiles_n, smem);
+    return;
+  }
+  // persistent: XCD x walks its contiguous run of tile ids (as gemm_w4_kernel)
+  const int x = blockIdx.x % 8, l = blockIdx.x / 8, per = G / 8, q = T / 8, r = T % 8;
+  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, end = start + q + (x < r ? 1 : 0);
+  for (int id = start + l; id < end; id += per) {
+    if (id != start + l) __syncthreads();
+    gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 128, lda, ldb, ldc, epi, id,
+                                     gm_, tiles_m, tiles_n, smem);
+  }
 }
 
 // Persistent by default: 256 workgroups (one per CU), XCD x walking ITS contiguous run of tile ids
@@ -547,7 +559,13 @@ static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, i
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((M / 256) * (N / 256), splits), dim3(256), SMEM, st, A, B, C, M, N, K / 128,
+  static const bool persist = [] {
+    const char* v = getenv("MLT_W4_PERSIST");
+    return !(v && atoi(v) == 0);
+  }();
+  const int tiles = (M / 256) * (N / 256);
+  const int grid = persist && splits == 1 && tiles > 256 ? 256 : tiles;
+  hipLaunchKernelGGL(kern, dim3(grid, splits), dim3(256), SMEM, st, A, B, C, M, N, K / 128,
                      ksteps > 0 ? ksteps : K / 128, lda, ldb, ldc, cstride, e, group_m);
 }
 template <typename OutT, int FA, int FB>
