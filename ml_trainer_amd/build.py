@@ -100,6 +100,11 @@ FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-ve
                                  "-mllvm", "-amdgpu-kernarg-preload-count=12"]}
 
 
+# kernels whose accumulators live in AGPRs owned by inline asm (gemm_w4.hip): the build also emits
+# their device asm and fails on any compiler-generated v_accvgpr_write (scripts/check_w4_agpr.py)
+AGPR_GUARDED = {"gemm_w4.hip"}
+
+
 def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
     import pybind11
     os.makedirs(BUILD_DIR, exist_ok=True)
@@ -118,6 +123,7 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
                        [os.path.join(CSRC, "bindings.cpp")])
     jobs_list = []
     objs = []
+    asm_checks = []
     for s in kernel_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
@@ -125,6 +131,10 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
                "-Wno-unused-result", *FILE_FLAGS.get(os.path.basename(s), [])]
         if force or _newer(s, o, hdrs, cmd):
             jobs_list.append(cmd)
+            if os.path.basename(s) in AGPR_GUARDED:  # + its device asm for the AGPR-spill guard
+                asm_checks.append(os.path.join(BUILD_DIR, os.path.basename(s) + ".s"))
+                jobs_list.append([HIPCC, "-S", s, "--cuda-device-only", "-o", asm_checks[-1], f"--offload-arch={ARCH}",
+                                  *opt, *common, *FILE_FLAGS.get(os.path.basename(s), [])])
     for s in host_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
@@ -144,6 +154,14 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
                 if verbose:
                     src = futs[f][2]
                     print(f"[mlt-build] {os.path.relpath(src, REPO_DIR)}  {dt:.1f}s", flush=True)
+    for a in asm_checks:  # asm-owned accumulators: no compiler spill may land in an AGPR
+        sys.path.insert(0, os.path.join(REPO_DIR, "scripts"))
+        from check_w4_agpr import check
+        counts, bad = check(open(a).read())
+        if bad:
+            raise RuntimeError(f"compiler AGPR writes in asm-owned-accumulator kernels ({a}): {bad}")
+        if verbose:
+            print(f"[mlt-build] {os.path.basename(a)}: {len(counts)} kernels, no compiler AGPR writes", flush=True)
     out = ext_path()
     if force or jobs_list or not os.path.exists(out):
         link = ["g++", "-shared", "-o", out, *objs, f"-L{tlib}", f"-Wl,-rpath,{tlib}",

@@ -119,9 +119,6 @@ void launch_gemm_w4_wgrad(const uint8_t* A, const uint8_t* B, OutT* C, float* ws
 // ... and its fp8 form (block-scaled MFMA, unit scales; both operands k-contiguous bytes)
 bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
                           const GemmEpi& e);
-template <int FA, int FB>
-void launch_gemm_w4_f8_q(const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st);
 bool gemm_w4_f8_splitk_supported(int M, int N, int K, int64_t lda, int64_t ldb, int splits, int ksteps);
 template <int FA, int FB>
 void launch_gemm_w4_f8_splitk(const uint8_t* A, const uint8_t* B, float* ws, int M, int N, int K, int64_t lda,

@@ -1237,26 +1237,9 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
   e.q_amax = out_amax;
   e.q_colpart = colpart;
   e.q_fmt = out_fmt;
-  // cfg 7's q8 epilogue (gemm_w4.hip) only on request (MLT_GEMM_W4Q8=1): its GELU / fp8-pack VALU
-  // runs after the main loop with one wave per SIMD and measured slower than the ping-pong's in the
-  // fp8 `large` step (FFN1 forward 2.73 vs 2.43 ms, FFN2 dgrad 2.48 vs 2.33 ms per call at b512,
-  // profiles/r4/large_fp8_b512_kernel_stats_r4.csv)
-  static const bool w4 = [] {
-    const char* v = getenv("MLT_GEMM_W4");
-    const char* vq = getenv("MLT_GEMM_W4Q8");
-    return !(v && atoi(v) == 0) && (vq && atoi(vq) == 1);
-  }();
-  if (w4 && K % 256 == 0 && K >= 512 && lda % 16 == 0 && ldb % 16 == 0 && ldy % 16 == 0 && ldyt % 16 == 0 &&
-      (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
-    if (fmt_a == 0 && fmt_b == 0) {
-      launch_gemm_w4_f8_q<0, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st);
-      return;
-    }
-    if (fmt_a == 1 && fmt_b == 0) {
-      launch_gemm_w4_f8_q<1, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st);
-      return;
-    }
-  }
+  // (the ping-pong kernel: a 4-wave form of this epilogue measured slower -- 2.73 vs 2.43 ms per
+  // FFN1 call in the fp8 `large` step, its GELU / fp8-pack VALU serialised behind the main loop --
+  // and needed more than 256 VGPRs; profiles/README.md, round 4)
   GemmPlan p{5, 1, K / 128, 0, 0};
   if (fmt_a == 0 && fmt_b == 0)
     launch_pp<false, false, uint8_t, 0, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);

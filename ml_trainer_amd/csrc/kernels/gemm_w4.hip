@@ -22,12 +22,11 @@
 #include "mlt_common.h"
 #include "mlt_gemm.h"
 #include "mlt_gemm_tile.h"
-#include "mlt_fp8.h"
 #include "gemm_w4_loop.inc"
 
 namespace mlt {
 
-enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3, W4_Q8 = 8 };
+enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // LDS: two K-tile stages of 64 KB; after the loop, four per-wave 64 x 132 fp32 epilogue images
@@ -56,19 +55,24 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
     const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
     bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
   }
-  // side operands (residual / dGELU pre-activation) of BOTH halves issued first: one HBM round trip
-  // under the image writes instead of one per half
-  uint4 sd[2][16];
-  if constexpr (EK == W4_RES || EK == W4_DGELU) {
+  // side operands: the residual of BOTH halves issued first (one HBM round trip under the image
+  // writes instead of one per half); the dGELU pre-activation per half -- with the column partials
+  // beside it, both halves' 128 registers would push the kernel past 256 VGPRs into spills to AGPRs,
+  // which hold the not-yet-read accumulators (scripts/check_w4_agpr.py guards every build)
+  constexpr int SH = EK == W4_RES ? 2 : 1;
+  uint4 sd[SH][16];
+  auto side_loads = [&](int h, uint4 (&dst)[16]) __attribute__((always_inline)) {
     const uint16_t* sx = EK == W4_RES ? epi.res : epi.aux;
     const int64_t ldx = EK == W4_RES ? epi.ldres : epi.ldaux;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
-        sd[h][it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
-      }
+    for (int it = 0; it < 16; ++it) {
+      const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
+      dst[it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
+    }
+  };
+  if constexpr (EK == W4_RES) {
+    side_loads(0, sd[0]);
+    side_loads(1, sd[SH - 1]);
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -80,6 +84,7 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
         *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
       }
+    if constexpr (EK == W4_DGELU) side_loads(h, sd[0]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
     float csum[8];  // dGELU + q_colpart: the half's column sums (bias gradient of the dGELU output)
 #pragma unroll
@@ -102,7 +107,8 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
             make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
       } else if constexpr (EK == W4_RES || EK == W4_DGELU) {
-        const uint32_t sw4[4] = {sd[h][it].x, sd[h][it].y, sd[h][it].z, sd[h][it].w};
+        const uint4 sv = sd[EK == W4_RES ? h : 0][it];
+        const uint32_t sw4[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float x = bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
@@ -141,125 +147,6 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
       }
     }
     if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
-  }
-}
-
-// ---- quantising ("q8") epilogue of the fp8 form: the output as fp8 C [M][N] AND its transpose C^T
-// [N][M] (the consumer GEMM's k-contiguous operand), amax of the unscaled output, optionally the
-// column partial sums per 64-row block (the bias gradient) -- gemm_tile.hip's q8 semantics. Per
-// wave and 64-row half, through the fp32 LDS image: a row pass (8 columns per lane: bias, GELU with
-// the bf16 pre-activation saved / dGELU, amax, scale, one 8-byte fp8 store; the scaled values go
-// back into the image) and a column pass (2 adjacent columns per lane, 16 rows per ds_read_b64
-// sweep: 16-byte fp8 stores of C^T rows, the column sums).
-template <int MODE, int FMT>
-__device__ __forceinline__ void w4_epilogue_q8(uint8_t* __restrict__ C, int64_t ldc, const GemmEpi& epi, float alpha,
-                                               int m0, int n0, int N, int w, int lane, uint8_t* smem) {
-  const int wr = w >> 1, wc = w & 1, g = lane >> 4, rl = lane & 15;
-  __syncthreads();  // every wave is past its last read of the K-tile stages
-  constexpr int P = kW4Pitch;
-  float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
-  const float s = *epi.q_scale;
-  const int rsub = lane >> 4, cc = lane & 15;
-  const int gn = n0 + wc * 128 + 8 * cc;
-  float bs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
-  if (epi.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(epi.bias + gn);
-    const float4 b1 = *reinterpret_cast<const float4*>(epi.bias + gn + 4);
-    bs[0] = b0.x, bs[1] = b0.y, bs[2] = b0.z, bs[3] = b0.w, bs[4] = b1.x, bs[5] = b1.y, bs[6] = b1.z, bs[7] = b1.w;
-  }
-  float amx = 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x0, x1, x2, x3;
-        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
-        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint4 sd[16];
-    if constexpr (MODE == 2) {  // dGELU pre-activations of the half first
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
-        sd[it] = *reinterpret_cast<const uint4*>(epi.aux + (int64_t)gm * epi.ldaux + gn);
-      }
-    }
-    // row pass
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
-      float* ip = img + row * P + 8 * cc;
-      const float4 lo = *reinterpret_cast<const float4*>(ip);
-      const float4 hi = *reinterpret_cast<const float4*>(ip + 4);
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
-      if constexpr (MODE == 1) {  // GELU: save the bf16 pre-activation, activate its rounded value
-        *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) = pack_bf16x8(v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_f(bf16_to_f32(f32_to_bf16(v[e])));
-      } else if constexpr (MODE == 2) {
-        const uint32_t wv[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[2 * q] *= gelu_grad(__uint_as_float(wv[q] << 16));
-          v[2 * q + 1] *= gelu_grad(__uint_as_float(wv[q] & 0xffff0000u));
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        amx = fmaxf(amx, fabsf(v[e]));
-        v[e] *= s;  // the image keeps the SCALED values: the column pass only converts
-      }
-      *reinterpret_cast<float4*>(ip) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(ip + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      *reinterpret_cast<uint2*>(C + (int64_t)gm * ldc + gn) =
-          make_uint2(pack4_fp8<FMT>(v[0], v[1], v[2], v[3]), pack4_fp8<FMT>(v[4], v[5], v[6], v[7]));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // column pass: lane -> columns 2 lane, 2 lane + 1 of the wave's 128; 4 sweeps of 16 rows
-    const int gc = n0 + wc * 128 + 2 * lane, gm0 = m0 + wr * 128 + 64 * h;
-    float cs0 = 0.f, cs1 = 0.f;
-#pragma unroll
-    for (int sw4 = 0; sw4 < 4; ++sw4) {
-      float a[16], b[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float2 t = *reinterpret_cast<const float2*>(img + (16 * sw4 + r) * P + 2 * lane);
-        a[r] = t.x;
-        b[r] = t.y;
-      }
-      if (epi.q_colpart) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          cs0 += a[r];
-          cs1 += b[r];
-        }
-      }
-      uint32_t pa[4], pb[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        pa[q] = pack4_fp8<FMT>(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
-        pb[q] = pack4_fp8<FMT>(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
-      }
-      *reinterpret_cast<uint4*>(epi.qt + (int64_t)gc * epi.ldqt + gm0 + 16 * sw4) = make_uint4(pa[0], pa[1], pa[2], pa[3]);
-      *reinterpret_cast<uint4*>(epi.qt + (int64_t)(gc + 1) * epi.ldqt + gm0 + 16 * sw4) =
-          make_uint4(pb[0], pb[1], pb[2], pb[3]);
-    }
-    if (epi.q_colpart) {  // column sums of the unscaled output over this 64-row block
-      const float inv = __builtin_amdgcn_rcpf(s);
-      *reinterpret_cast<float2*>(epi.q_colpart + (int64_t)(gm0 >> 6) * N + gc) = make_float2(cs0 * inv, cs1 * inv);
-    }
-    if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
-  }
-  if (epi.q_amax) {
-    amx = wave_max(amx);
-    if (lane == 0) atomic_max_pos(epi.q_amax, amx);
   }
 }
 
@@ -395,11 +282,7 @@ __device__ __forceinline__ void gemm_w4f8_tile(const uint8_t* __restrict__ A, co
   float alpha = epi.alpha;
   if (epi.inv_scale_a) alpha *= *epi.inv_scale_a;
   if (epi.inv_scale_b) alpha *= *epi.inv_scale_b;
-  if constexpr (EK >= W4_Q8)  // EK = W4_Q8 + 3 * out fmt + mode
-    w4_epilogue_q8<(EK - W4_Q8) % 3, (EK - W4_Q8) / 3>(reinterpret_cast<uint8_t*>(C), ldc, epi, alpha, m0, n0,
-                                                        tiles_n * 256, w, lane, smem);
-  else
-    w4_epilogue<OutT, EK>(C, ldc, epi, alpha, m0, n0, tiles_n * 256, w, lane, smem);
+  w4_epilogue<OutT, EK>(C, ldc, epi, alpha, m0, n0, tiles_n * 256, w, lane, smem);
 }
 
 template <typename OutT, int EK, int FA, int FB>
@@ -484,14 +367,18 @@ template <typename OutT, bool AN, bool BN>
 static void launch_w4_bn(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                          int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
   const int nk = K / 64;
-  if (e.mode == 1)
-    launch_w4_ek<OutT, W4_GELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
-  else if (e.mode == 2)
-    launch_w4_ek<OutT, W4_DGELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
-  else if (e.res)
-    launch_w4_ek<OutT, W4_RES, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
-  else
+  if constexpr (sizeof(OutT) == 4) {  // fp32 outputs: the plain epilogue only (host-checked)
     launch_w4_ek<OutT, W4_PLAIN, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+  } else {
+    if (e.mode == 1)
+      launch_w4_ek<OutT, W4_GELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+    else if (e.mode == 2)
+      launch_w4_ek<OutT, W4_DGELU, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+    else if (e.res)
+      launch_w4_ek<OutT, W4_RES, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+    else
+      launch_w4_ek<OutT, W4_PLAIN, AN, BN>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, 1, nk, 0, st);
+  }
 }
 
 template <typename OutT>
@@ -571,14 +458,18 @@ static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, i
 template <typename OutT, int FA, int FB>
 void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                        int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st) {
-  if (e.mode == 1)
-    launch_w4f8_ek<OutT, W4_GELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else if (e.mode == 2)
-    launch_w4f8_ek<OutT, W4_DGELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else if (e.res)
-    launch_w4f8_ek<OutT, W4_RES, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
-  else
+  if constexpr (sizeof(OutT) == 4) {  // fp32 outputs: the plain epilogue only (host-checked)
     launch_w4f8_ek<OutT, W4_PLAIN, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  } else {
+    if (e.mode == 1)
+      launch_w4f8_ek<OutT, W4_GELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+    else if (e.mode == 2)
+      launch_w4f8_ek<OutT, W4_DGELU, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+    else if (e.res)
+      launch_w4f8_ek<OutT, W4_RES, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+    else
+      launch_w4f8_ek<OutT, W4_PLAIN, FA, FB>(A, B, C, M, N, K, lda, ldb, ldc, e, group_m, st);
+  }
 }
 // split-K raw fp32 partials ws[z][M][N] (alpha, the fp8 inverse scales and the epilogue are the
 // split-reduce's): the fp8 weight gradients (few tiles, K = tokens)
@@ -605,23 +496,6 @@ bool gemm_w4_f8_splitk_supported(int M, int N, int K, int64_t lda, int64_t ldb, 
   if (lda % 16 || ldb % 16 || lda * 256 > (int64_t)1 << 31 || ldb * 256 > (int64_t)1 << 31) return false;
   return true;
 }
-
-// the quantising epilogue (fp8 Y, Y^T, amax, column partials): Y / Yt as uint8, mode 0 / 1 / 2
-template <int FA, int FB>
-void launch_gemm_w4_f8_q(const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st) {
-#define MLT_W4Q8(MODE, FMT)                                                                                       \
-  if (e.mode == MODE && e.q_fmt == FMT) {                                                                         \
-    launch_w4f8_ek<uint8_t, W4_Q8 + 3 * FMT + MODE, FA, FB>(A, B, Y, M, N, K, lda, ldb, ldy, e, group_m, st);  \
-    return;                                                                                                       \
-  }
-  MLT_W4Q8(0, 0) MLT_W4Q8(1, 0) MLT_W4Q8(2, 0) MLT_W4Q8(0, 1) MLT_W4Q8(1, 1) MLT_W4Q8(2, 1)
-#undef MLT_W4Q8
-}
-template void launch_gemm_w4_f8_q<0, 0>(const uint8_t*, const uint8_t*, uint8_t*, int, int, int, int64_t, int64_t,
-                                        int64_t, const GemmEpi&, int, hipStream_t);
-template void launch_gemm_w4_f8_q<1, 0>(const uint8_t*, const uint8_t*, uint8_t*, int, int, int, int64_t, int64_t,
-                                        int64_t, const GemmEpi&, int, hipStream_t);
 
 bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int out_bytes,
                           const GemmEpi& e) {

@@ -1,7 +1,6 @@
 """fp8 GEMM with a quantising epilogue (gemm_tile.hip q8_quadrant, C.gemm_f8_q) and the fused
 FFN path built on it (ops/fp8.py fwd_gelu_q / dgrad_gelu_q) vs plain torch fp32 references."""
 import math
-import os
 
 import pytest
 import torch
@@ -30,10 +29,7 @@ def _gelu_grad(x):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024),
                                    (8192, 2048, 512), (4096, 4096, 1024)])  # the last two: >= 240 tiles
-@pytest.mark.parametrize("w4q8", ["0", "1"])  # MLT_GEMM_W4Q8: the cfg 7 epilogue (read once per process)
-def test_gemm_f8_q_matches_fp32(dev, mode, shape, w4q8):
-    if w4q8 == "1" and os.environ.get("MLT_GEMM_W4Q8") != "1":
-        pytest.skip("run with MLT_GEMM_W4Q8=1 for the cfg 7 quantising epilogue")
+def test_gemm_f8_q_matches_fp32(dev, mode, shape):
     C = require_native()
     M, N, K = shape
     g = torch.Generator().manual_seed(M + N + K + mode)
