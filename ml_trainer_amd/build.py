@@ -105,7 +105,10 @@ FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-ve
 AGPR_GUARDED = {"gemm_w4.hip"}
 
 
-def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True) -> str:
+def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool = True, extra_flags=None,
+          out_path=None) -> str:
+    """extra_flags: {kernel file name: [flags]} on top of FILE_FLAGS; out_path: link elsewhere (A/B
+    variants of one kernel file; the objects are rebuilt for the in-tree flags on the next plain build)."""
     import pybind11
     os.makedirs(BUILD_DIR, exist_ok=True)
     tinc, tlib, abi = _torch_paths()
@@ -128,7 +131,8 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
         cmd = [HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common, "-munsafe-fp-atomics",
-               "-Wno-unused-result", *FILE_FLAGS.get(os.path.basename(s), [])]
+               "-Wno-unused-result", *FILE_FLAGS.get(os.path.basename(s), []),
+               *(extra_flags or {}).get(os.path.basename(s), [])]
         if force or _newer(s, o, hdrs, cmd):
             jobs_list.append(cmd)
             if os.path.basename(s) in AGPR_GUARDED:  # + its device asm for the AGPR-spill guard
@@ -162,7 +166,7 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
             raise RuntimeError(f"compiler AGPR writes in asm-owned-accumulator kernels ({a}): {bad}")
         if verbose:
             print(f"[mlt-build] {os.path.basename(a)}: {len(counts)} kernels, no compiler AGPR writes", flush=True)
-    out = ext_path()
+    out = out_path or ext_path()
     if force or jobs_list or not os.path.exists(out):
         link = ["g++", "-shared", "-o", out, *objs, f"-L{tlib}", f"-Wl,-rpath,{tlib}",
                 "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",

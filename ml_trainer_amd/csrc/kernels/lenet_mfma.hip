@@ -163,7 +163,10 @@ constexpr int DCCS = 24;         // [oc][Y][X] conv2-output grad: row stride (co
 constexpr int D1S = 28 * 32 + 16;  // [oc][Y][X32] unpooled conv1 grad: channel stride (conv1 wgrad B, 1-way vs 5)
 constexpr int kWgT = 256;        // KW threads
 constexpr int kP13W = 7;         // conv1 wgrad waves (28 output rows / 4 each)
-constexpr int kC1W = 8;          // conv1 forward waves (the fc1 forward waves 8-15 fetch weights meanwhile)
+#ifndef MLT_KC1W
+#define MLT_KC1W 8  // (build-time A/B knob)
+#endif
+constexpr int kC1W = MLT_KC1W;   // conv1 forward waves (the fc1 forward waves 8-15 fetch weights meanwhile)
 
 // ---------------------------------------------------------------------------
 // fc layers on the matrix cores: y = W x for ONE sample, its input row x (bf16 in LDS, zero past K
