@@ -52,6 +52,74 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return fmaf(x, 0.3989422804014327f * e, cdf);
 }
 
+// Two-wide forms for the VALU-bound GEMM epilogues (gemm_w4.hip): the same A&S 7.1.26 erf,
+// written on float2 so every non-transcendental step is one v_pk_fma_f32 / v_pk_mul_f32 for two
+// elements (the scalar forms above compile to ~19 single-element VALU ops + 2 transcendentals
+// per element; these to ~11 + 2). q = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2) = 0.5 poly(t) e^{-x^2/2}
+// (the 0.5 and 1/sqrt 2 folded into the constants), then
+//   gelu(x)  = x Phi(x) = relu(x) - |x| q
+//   gelu'(x) = Phi(x) + x phi(x),  Phi(x) = 0.5 + copysign(0.5 - q, x),  phi(x) = e^{-x^2/2} / sqrt(2 pi)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// packed round-to-nearest-even f32 x 2 -> bf16 x 2 (one v_cvt_pk_bf16_f32), element 0 in the low half
+__device__ __forceinline__ uint32_t cvt_pk_bf16(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ f32x2 unpack_bf16x2(uint32_t u) {
+  return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// q = Phi(-|x|) of N pairs, step by step across the pairs (N independent chains in source order:
+// a dependent packed op right behind its producer costs an s_nop on gfx950); also |x| and
+// e^{-x^2/2}
+template <int N>
+__device__ __forceinline__ void phi_tail2(const f32x2 (&x)[N], f32x2 (&ax)[N], f32x2 (&e)[N], f32x2 (&q)[N]) {
+  f32x2 t[N], h[N], arg[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) ax[i] = f32x2{fabsf(x[i].x), fabsf(x[i].y)};
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = pk_fma(ax[i], f32x2(0.3275911f * 0.70710678118654752f), f32x2(1.f));
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = f32x2{__builtin_amdgcn_rcpf(t[i].x), __builtin_amdgcn_rcpf(t[i].y)};
+#pragma unroll
+  for (int i = 0; i < N; ++i) arg[i] = x[i] * f32x2(-0.5f * 1.4426950408889634f);
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = pk_fma(t[i], f32x2(0.5f * 1.061405429f), f32x2(0.5f * -1.453152027f));
+#pragma unroll
+  for (int i = 0; i < N; ++i) arg[i] = arg[i] * x[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = pk_fma(t[i], h[i], f32x2(0.5f * 1.421413741f));
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = f32x2{__builtin_amdgcn_exp2f(arg[i].x), __builtin_amdgcn_exp2f(arg[i].y)};
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = pk_fma(t[i], h[i], f32x2(0.5f * -0.284496736f));
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = pk_fma(t[i], h[i], f32x2(0.5f * 0.254829592f));
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = t[i] * h[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = h[i] * e[i];
+}
+template <int N>
+__device__ __forceinline__ void gelu2(f32x2 (&x)[N]) {
+  f32x2 ax[N], e[N], q[N];
+  phi_tail2<N>(x, ax, e, q);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = pk_fma(-ax[i], q[i], (x[i] + ax[i]) * f32x2(0.5f));  // relu = (x + |x|) / 2
+}
+template <int N>
+__device__ __forceinline__ void gelu_grad2(f32x2 (&x)[N]) {
+  f32x2 ax[N], e[N], q[N];
+  phi_tail2<N>(x, ax, e, q);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const f32x2 r = f32x2(0.5f) - q[i];  // in [0, 0.5]: its sign bit is free for x's
+    q[i] = f32x2(0.5f) + f32x2{copysignf(r.x, x[i].x), copysignf(r.y, x[i].y)};
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = pk_fma(x[i] * f32x2(0.3989422804014327f), e[i], q[i]);
+}
+
 // Apply the epilogue to 4 consecutive columns gn..gn+3 of row gm (values already scaled by
 // alpha and biased) and store them. Columns >= N are skipped.
 template <typename OutT>

@@ -98,29 +98,34 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
       if constexpr (EK == W4_GELU) {  // keep the (bf16-rounded) pre-activation for the backward
-        uint16_t a[8];
+        uint32_t a[4];                // (two-wide GELU: this epilogue is VALU-bound, mlt_gemm.h)
+        f32x2 x2[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          a[e] = f32_to_bf16(v[e]);
-          v[e] = gelu_f(bf16_to_f32(a[e]));
+        for (int q2 = 0; q2 < 4; ++q2) {
+          a[q2] = cvt_pk_bf16(f32x2{v[2 * q2], v[2 * q2 + 1]});
+          x2[q2] = unpack_bf16x2(a[q2]);
         }
         *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
-            make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
-      } else if constexpr (EK == W4_RES || EK == W4_DGELU) {
-        const uint4 sv = sd[EK == W4_RES ? h : 0][it];
+            make_uint4(a[0], a[1], a[2], a[3]);
+        gelu2<4>(x2);
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) v[2 * q2] = x2[q2].x, v[2 * q2 + 1] = x2[q2].y;
+      } else if constexpr (EK == W4_DGELU) {
+        const uint4 sv = sd[0][it];
+        f32x2 x2[4] = {unpack_bf16x2(sv.x), unpack_bf16x2(sv.y), unpack_bf16x2(sv.z), unpack_bf16x2(sv.w)};
+        gelu_grad2<4>(x2);
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const f32x2 gv = f32x2{v[2 * q2], v[2 * q2 + 1]} * x2[q2];
+          v[2 * q2] = gv.x, v[2 * q2 + 1] = gv.y;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += v[e];
+      } else if constexpr (EK == W4_RES) {
+        const uint4 sv = sd[h][it];
         const uint32_t sw4[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
-          if constexpr (EK == W4_RES)
-            v[e] += x;
-          else
-            v[e] *= gelu_grad(x);
-        }
-        if constexpr (EK == W4_DGELU) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) csum[e] += v[e];
-        }
+        for (int e = 0; e < 8; ++e) v[e] += bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
       }
       OutT* cp = C + (int64_t)gm * ldc + gn;
       if constexpr (sizeof(OutT) == 4) {
@@ -128,8 +133,8 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
       } else {
         *reinterpret_cast<uint4*>(cp) =
-            make_uint4(pack2(f32_to_bf16(v[0]), f32_to_bf16(v[1])), pack2(f32_to_bf16(v[2]), f32_to_bf16(v[3])),
-                       pack2(f32_to_bf16(v[4]), f32_to_bf16(v[5])), pack2(f32_to_bf16(v[6]), f32_to_bf16(v[7])));
+            make_uint4(cvt_pk_bf16(f32x2{v[0], v[1]}), cvt_pk_bf16(f32x2{v[2], v[3]}),
+                       cvt_pk_bf16(f32x2{v[4], v[5]}), cvt_pk_bf16(f32x2{v[6], v[7]}));
       }
     }
     if constexpr (EK == W4_DGELU) {
