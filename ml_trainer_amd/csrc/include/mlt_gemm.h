@@ -31,25 +31,30 @@ struct GemmEpi {
   int q_fmt = 0;                   // 0 e4m3, 1 e5m2
 };
 
-// erf(z) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 output's ulp):
-// one v_rcp, one v_exp, five FMAs instead of the library erff; `ez2` returns e^{-z^2}, which
-// the GELU derivative reuses as its Gaussian density term.
-__device__ __forceinline__ float erf_fast(float z, float& ez2) {
-  const float a = fabsf(z);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-  const float poly =
-      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
-  ez2 = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-  return copysignf(fmaf(-poly, ez2, 1.f), z);
+// GELU and its derivative (erf by Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, far below the
+// bf16 output's ulp: one v_rcp and one v_exp instead of the library erff). These scalar forms are
+// the two-wide forms below operation for operation (v_pk_fma_f32 / v_pk_mul_f32 round each lane
+// exactly as v_fma_f32 / v_mul_f32), so every epilogue -- packed or not, in-kernel or split-K
+// reduce -- produces the same bits. q = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2).
+__device__ __forceinline__ float phi_tail(float x, float& ax, float& e) {
+  ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(ax, 0.3275911f * 0.70710678118654752f, 1.f));
+  float h = fmaf(t, 0.5f * 1.061405429f, 0.5f * -1.453152027f);
+  h = fmaf(t, h, 0.5f * 1.421413741f);
+  h = fmaf(t, h, 0.5f * -0.284496736f);
+  h = fmaf(t, h, 0.5f * 0.254829592f);
+  e = __builtin_amdgcn_exp2f((x * (-0.5f * 1.4426950408889634f)) * x);
+  return (t * h) * e;
 }
 __device__ __forceinline__ float gelu_f(float x) {
-  float e;
-  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f, e));
+  float ax, e;
+  const float q = phi_tail(x, ax, e);
+  return fmaf(-ax, q, (x + ax) * 0.5f);
 }
 __device__ __forceinline__ float gelu_grad(float x) {
-  float e;  // e = exp(-x^2 / 2)
-  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, e));
-  return fmaf(x, 0.3989422804014327f * e, cdf);
+  float ax, e;
+  const float q = phi_tail(x, ax, e);
+  return fmaf(x * 0.3989422804014327f, e, 0.5f + copysignf(0.5f - q, x));
 }
 
 // Two-wide forms for the VALU-bound GEMM epilogues (gemm_w4.hip): the same A&S 7.1.26 erf,
@@ -328,12 +333,8 @@ __device__ __forceinline__ bool epi_store8_ok(const GemmEpi& epi, const void* C,
 }
 
 __device__ __forceinline__ uint4 pack_bf16x8(const float (&v)[8]) {
-  uint4 o;
-  o.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-  o.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
-  o.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
-  o.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
-  return o;
+  return make_uint4(cvt_pk_bf16(f32x2{v[0], v[1]}), cvt_pk_bf16(f32x2{v[2], v[3]}), cvt_pk_bf16(f32x2{v[4], v[5]}),
+                    cvt_pk_bf16(f32x2{v[6], v[7]}));
 }
 
 template <int MODE, int EIT8, class RC8>
@@ -349,12 +350,10 @@ __device__ __forceinline__ void epi_store8_loop(uint16_t* __restrict__ C, int64_
     if constexpr (MODE == 1) {
       const uint4 pre = pack_bf16x8(v);
       *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) = pre;
-      const uint32_t w[4] = {pre.x, pre.y, pre.z, pre.w};
+      f32x2 x2[4] = {unpack_bf16x2(pre.x), unpack_bf16x2(pre.y), unpack_bf16x2(pre.z), unpack_bf16x2(pre.w)};
+      gelu2<4>(x2);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] = gelu_f(bf16_to_f32((uint16_t)(w[q] & 0xffff)));
-        v[2 * q + 1] = gelu_f(bf16_to_f32((uint16_t)(w[q] >> 16)));
-      }
+      for (int q = 0; q < 4; ++q) v[2 * q] = x2[q].x, v[2 * q + 1] = x2[q].y;
     } else if constexpr (MODE == 3) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = tanhf(v[q]);

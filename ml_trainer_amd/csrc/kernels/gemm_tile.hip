@@ -390,24 +390,32 @@ __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc
     const int gn = gn0 + c16;
     if (epi.mode == 1) {  // GELU: save the bf16 pre-activation, activate its rounded value
       uint16_t* ap = const_cast<uint16_t*>(epi.aux) + gm * epi.ldaux + gn;
-      float lo[8], hi[8];
+      uint32_t pr[8];  // (two-wide GELU, mlt_gemm.h)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        lo[q] = v[q];
-        hi[q] = v[8 + q];
+      for (int q = 0; q < 8; ++q) pr[q] = cvt_pk_bf16(f32x2{v[2 * q], v[2 * q + 1]});
+      reinterpret_cast<uint4*>(ap)[0] = make_uint4(pr[0], pr[1], pr[2], pr[3]);
+      reinterpret_cast<uint4*>(ap)[1] = make_uint4(pr[4], pr[5], pr[6], pr[7]);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        f32x2 x2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x2[q] = unpack_bf16x2(pr[4 * hh + q]);
+        gelu2<4>(x2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[8 * hh + 2 * q] = x2[q].x, v[8 * hh + 2 * q + 1] = x2[q].y;
       }
-      reinterpret_cast<uint4*>(ap)[0] = pack_bf16x8(lo);
-      reinterpret_cast<uint4*>(ap)[1] = pack_bf16x8(hi);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = gelu_f(bf16_to_f32(f32_to_bf16(v[q])));
     } else if (epi.mode == 2) {  // dGELU: times gelu'(pre-activation)
       const uint4* ap = reinterpret_cast<const uint4*>(epi.aux + gm * epi.ldaux + gn);
       const uint4 a0 = ap[0], a1 = ap[1];
       const uint32_t w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        v[2 * q] *= gelu_grad(__uint_as_float(w[q] << 16));
-        v[2 * q + 1] *= gelu_grad(__uint_as_float(w[q] & 0xffff0000u));
+      for (int hh = 0; hh < 2; ++hh) {
+        f32x2 x2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x2[q] = unpack_bf16x2(w[4 * hh + q]);
+        gelu_grad2<4>(x2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[8 * hh + 2 * q] *= x2[q].x, v[8 * hh + 2 * q + 1] *= x2[q].y;
       }
     }
 #pragma unroll
