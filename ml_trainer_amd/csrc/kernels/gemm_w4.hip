@@ -76,14 +76,12 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x0, x1, x2, x3;
-        MLT_W4_READ_FRAG(8 * (4 * h + i) + j, x0, x1, x2, x3);
-        *reinterpret_cast<float4*>(img + (16 * i + rl) * P + 16 * j + 4 * g) = make_float4(x0, x1, x2, x3);
-      }
+    // the half's 32 fragments -> image rows 16 i + rl, columns 16 j + 4 g (ds_write from the AGPRs)
+    const uint32_t va = (uint32_t)(uintptr_t)(lds_u8*)(smem + 4 * (w * 64 * P + rl * P + 4 * g));
+    if (h == 0)
+      asm volatile(MLT_W4_IMG_H0 ::[va] "v"(va) : "memory");
+    else
+      asm volatile(MLT_W4_IMG_H1 ::[va] "v"(va) : "memory");
     if constexpr (EK == W4_DGELU) side_loads(h, sd[0]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
     float csum[8];  // dGELU + q_colpart: the half's column sums (bias gradient of the dGELU output)

@@ -274,12 +274,18 @@ def main():
         clob_f8 = ", ".join(f'"v{r}"' for r in range(193)) + ", " + ", ".join(f'"a{r}"' for r in range(256))
         clob_f8 += ', "s88", "s89", "s90", "s91", "m0", "scc"'
         f.write(f"#define MLT_W4F8_CLOBBERS {clob_f8}\n")
-        # the epilogue's accumulator reads: fragment f (compile-time after unrolling) -> 4 floats
-        f.write("#define MLT_W4_READ_FRAG(f, x0, x1, x2, x3) \\\n  switch (f) { \\\n")
-        for fr in range(64):
-            regs = "\\n".join(f"v_accvgpr_read_b32 %{e}, a{4 * fr + e}" for e in range(4))
-            f.write(f'    case {fr}: asm volatile("{regs}" : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)); break; \\\n')
-        f.write("    default: break; \\\n  }\n")
+        # the epilogue's LDS image straight from the accumulators (ds_write takes AGPR data on gfx950:
+        # no v_accvgpr_read per element): half h = fragments 8 (4h + i) + j, lane-relative row 16 i,
+        # column 16 j of the 132-float-pitch image -> immediate offsets from one address register.
+        # Half 0 opens with 3 x s_nop 7 (24 wait states): the MFMA -> LDS-read-of-its-result hazard
+        # against the main loop's last MFMAs is not interlocked.
+        for h in range(2):
+            lines = ["s_nop 7", "s_nop 7", "s_nop 7"] if h == 0 else []
+            for i in range(4):
+                for j in range(8):
+                    fr = 8 * (4 * h + i) + j
+                    lines.append(f"ds_write_b128 %[va], a[{4 * fr}:{4 * fr + 3}] offset:{i * 16 * 132 * 4 + j * 64}")
+            emit(f, f"MLT_W4_IMG_H{h}", lines)
     print(f"wrote {OUT}")
 
 
