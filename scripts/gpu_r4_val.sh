@@ -19,7 +19,7 @@ timeout -k 10 180 python -u bench.py --batch 4 --no-fp32-companion > $O/lenet_b4
 tail -1 $O/lenet_b4.json | cut -c1-200
 timeout -k 10 300 python -u bench.py --model bert-base --steps 20 --warmup 5 > $O/bert.json 2>$O/b.err || { tail $O/b.err; exit 1; }
 tail -1 $O/bert.json | cut -c1-200
-timeout -k 10 400 python -u bench.py --model large --steps 6 --warmup 2 > $O/large.json 2>$O/b.err || { tail $O/b.err; exit 1; }
+timeout -k 10 400 python -u bench.py --model large --steps 20 --warmup 5 > $O/large.json 2>$O/b.err || { tail $O/b.err; exit 1; }
 tail -1 $O/large.json | cut -c1-200
 timeout -k 10 400 python -u bench.py --model large --steps 6 --warmup 2 --batch 256 > $O/large256.json 2>$O/b.err || { tail $O/b.err; exit 1; }
 tail -1 $O/large256.json | cut -c1-200
