@@ -1,4 +1,4 @@
-"""fp8 quantisation kernel throughput (cast with / without amax, cast-transpose)."""
+"""fp8 quantisation kernel throughput (cast with / without amax, amax alone, cast-transpose)."""
 import json
 import os
 import sys
@@ -27,15 +27,17 @@ def timeit(fn, iters=50):
 
 scale = torch.ones(1, device=dev)
 amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
-for shape in [(8192, 1024), (8192, 4096), (16384, 3072)]:
+for shape in [(8192, 1024), (8192, 4096), (16384, 3072), (262144, 1024)]:
     x = torch.randn(*shape, device=dev).to(torch.bfloat16)
     y = torch.empty(shape, dtype=torch.float8_e4m3fn, device=dev)
     n = x.numel()
     t_amax = timeit(lambda: C.fp8_cast(x, y, scale, amax, 0))
     t_noamax = timeit(lambda: C.fp8_cast(x, y, scale, None, 0))
+    t_amax_only = timeit(lambda: C.fp8_amax(x, amax))
     t_copy = timeit(lambda: y.view(torch.uint8).copy_(x.view(torch.uint8).view(-1)[:n].view(shape)))
     print(json.dumps({"shape": shape, "cast_amax_us": round(t_amax, 2), "cast_us": round(t_noamax, 2),
-                      "GBps": round(3 * n / t_noamax / 1e3, 1), "torch_u8_copy_us": round(t_copy, 2)}), flush=True)
+                      "GBps": round(3 * n / t_noamax / 1e3, 1),
+                      "amax_us": round(t_amax_only, 2), "amax_GBps": round(2 * n / t_amax_only / 1e3, 1), "torch_u8_copy_us": round(t_copy, 2)}), flush=True)
 w = torch.randn(4096, 1024, device=dev)
 w8 = torch.empty(4096, 1024, dtype=torch.float8_e4m3fn, device=dev)
 wt = torch.empty(1024, 4096, dtype=torch.float8_e4m3fn, device=dev)
