@@ -30,7 +30,8 @@ Usage:  python bench.py --gpus N --steps K --warmup W
 
 Timing: every hipGraph the K timed steps replay is captured and uploaded before the timed
 region (a capture counter is checked after it); wall time between barrier+synchronize pairs is
-reported, plus hipEvent device time per step in config.device_ms_per_step.
+reported. The LeNet timed region holds no hipEvent (two timing-event records cost ~30 us of wall
+time per region here); per-kernel device time comes from rocprofv3 (profiles/).
 
 BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgrad GEMMs with
 delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
@@ -385,17 +386,17 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     plan_w = list(lenet_plan(args.warmup, st_w, N, world, rank, per_gpu, spg, shard_indices))
     precapture(engine, plan_w, use_graph)
     precapture(engine, lenet_plan(args.steps, dict(st_w), N, world, rank, per_gpu, spg, shard_indices), use_graph)
+    # no hipEvent inside the timed region: two timing-event records cost ~30 us of wall time per
+    # region on this stack (21.1-21.9 vs 19.6-19.7 us/step at K=20,
+    # profiles/r4/lenet_timed_region_events_ab.jsonl); per-kernel device times come from rocprofv3
     run(args.warmup)
     captures_before = engine.captures
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0.record()
     samples = run(args.steps)
-    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -403,18 +404,15 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     elapsed = time.perf_counter() - t0
     if engine.captures != captures_before:
         raise RuntimeError("a hipGraph was captured inside the timed region")
-    device_s = ev0.elapsed_time(ev1) / 1e3
 
-    tot = torch.tensor([elapsed, float(samples), device_s], dtype=torch.float64,
+    tot = torch.tensor([elapsed, float(samples)], dtype=torch.float64,
                        device=dev if backend == "nccl" else torch.device("cpu"))
     if world > 1:
         t_max = tot[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         s_sum = tot[1:2].clone()
         dist.all_reduce(s_sum, op=dist.ReduceOp.SUM)
-        d_max = tot[2:3].clone()
-        dist.all_reduce(d_max, op=dist.ReduceOp.MAX)
-        elapsed, total_samples, device_s = float(t_max.item()), float(s_sum.item()), float(d_max.item())
+        elapsed, total_samples = float(t_max.item()), float(s_sum.item())
     else:
         total_samples = float(samples)
     # sanity: training actually ran (finite loss accumulated on device); transport healthy
@@ -455,7 +453,6 @@ def bench_lenet(args, world, rank, dev, backend, precision):
                    "hipgraph_steps": 0 if args.no_graph else spg,
                    "kernels_per_step": round(nodes / spg, 2) if nodes else None,
                    "ddp_comm": comm,
-                   "device_ms_per_step": round(device_s / args.steps * 1e3, 5),
                    "dp_transport": engine.dp_transport,
                    "comm_ranks": engine.comm.size if engine.comm is not None else None,
                    "transport_ms": getattr(engine, "transport_times_ms", None),
@@ -526,7 +523,6 @@ def main():
         comp = bench_lenet(args, world, rank, dev, backend, "fp32")
         out["config"]["fp32_samples_per_s"] = comp["value"]
         out["config"]["fp32_ms_per_step"] = comp["ms_per_step"]
-        out["config"]["fp32_device_ms_per_step"] = comp["config"]["device_ms_per_step"]
         out["config"]["fp32_vs_baseline"] = comp["vs_baseline"]
         out["config"]["fp32_dp_transport"] = comp["config"]["dp_transport"]
     _emit(out, rank, args)
