@@ -138,7 +138,8 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
             if os.path.basename(s) in AGPR_GUARDED:  # + its device asm for the AGPR-spill guard
                 asm_checks.append(os.path.join(BUILD_DIR, os.path.basename(s) + ".s"))
                 jobs_list.append([HIPCC, "-S", s, "--cuda-device-only", "-o", asm_checks[-1], f"--offload-arch={ARCH}",
-                                  *opt, *common, *FILE_FLAGS.get(os.path.basename(s), [])])
+                                  *opt, *common, *FILE_FLAGS.get(os.path.basename(s), []),
+                                  *(extra_flags or {}).get(os.path.basename(s), [])])
     for s in host_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
