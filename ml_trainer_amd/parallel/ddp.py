@@ -72,15 +72,22 @@ def allreduce_us(nbytes: float, world: int, alpha_us: Optional[float] = None, bu
     return a + 2.0 * (world - 1) / world * nbytes / (b * 1e3)  # GB/s = 1e3 bytes/us
 
 
+def _min_bucket_mb() -> float:
+    import os
+    return float(os.environ.get("MLT_DDP_MIN_BUCKET_MB", MIN_BUCKET_MB))
+
+
 def plan_buckets(grad_bytes: int, world: int, bwd_ms: Optional[float] = None, largest_param_bytes: int = 0,
                  alpha_us: Optional[float] = None, bus_gbps: Optional[float] = None):
     """Bucket caps (cap_mb, first_mb) from the alpha-beta model. Buckets launched during backward
     overlap it as long as the comm stream keeps up: n * ALPHA + beta * M <= T_bwd; what stays exposed
     is the last bucket's all-reduce (ALPHA + beta * C_last). So the cap is the SMALLEST that keeps
     the stream from falling behind -- C = M * ALPHA / (T_bwd - beta * M) -- clamped to
-    [4, 128] MB; a comm-bound step (beta * M >= T_bwd) gets the largest cap (fewest collectives).
-    The first bucket (the last layers' gradients, ready first) is small so that communication
-    starts early. Without a backward-time estimate: the defaults (32 / 4 MB)."""
+    [MIN, 128] MB (MIN = 4, MLT_DDP_MIN_BUCKET_MB); a comm-bound step (beta * M >= T_bwd) gets the
+    largest cap (fewest collectives). The first bucket (the last layers' gradients, ready first)
+    is the size at which the all-reduce stops being latency-bound -- beta * F = ALPHA, so smaller
+    would not start the wire earlier and larger would delay it -- clamped to [1 MB, cap].
+    Without a backward-time estimate: the defaults (32 / 4 MB)."""
     if world <= 1 or bwd_ms is None or bwd_ms <= 0:
         return DEFAULT_BUCKET_MB, DEFAULT_FIRST_BUCKET_MB
     a = allreduce_us(0, world, alpha_us, bus_gbps)  # alpha alone
@@ -91,8 +98,10 @@ def plan_buckets(grad_bytes: int, world: int, bwd_ms: Optional[float] = None, la
         cap = MAX_BUCKET_MB
     else:
         cap = grad_bytes * a / slack / mb
-    cap = min(MAX_BUCKET_MB, max(MIN_BUCKET_MB, cap))
-    first = min(cap, max(1.0, DEFAULT_FIRST_BUCKET_MB))
+    cap = min(MAX_BUCKET_MB, max(_min_bucket_mb(), cap))
+    beta_us_per_byte = total_us / grad_bytes if grad_bytes > 0 else 0.0
+    first = a / beta_us_per_byte / mb if beta_us_per_byte > 0 else DEFAULT_FIRST_BUCKET_MB
+    first = min(cap, max(min(1.0, cap), first))
     return cap, first
 
 
@@ -101,12 +110,17 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: Optional[float] = None, broadcast_parameters: bool = True,
                  mode: str = "overlap", flat: Optional[FlatParams] = None,
                  comm_dtype: Optional[torch.dtype] = None, timing: bool = False, comm=None,
-                 bwd_ms_hint: Optional[float] = None):
+                 bwd_ms_hint: Optional[float] = None, auto_plan: Optional[bool] = None):
         """``comm``: None = native RCCL communicator when the group is RCCL with W > 1 (else
         torch.distributed); False = always torch.distributed; a ``_C.Communicator`` = use that
         one (also at world size 1: the single-GPU rehearsal of the native collective path).
         ``bwd_ms_hint``: expected backward time; with no explicit caps the buckets are then sized
-        by the alpha-beta model (:func:`plan_buckets`)."""
+        by the alpha-beta model (:func:`plan_buckets`). ``auto_plan`` (default: on when neither
+        caps nor a hint are given, W > 1, overlap mode; MLT_DDP_AUTOPLAN=0 turns it off): the
+        second synchronised backward is timed (first gradient hook -> last gradient; device
+        events on GPU), the MAX over ranks is agreed at the next forward, and the buckets are
+        rebuilt ONCE from the alpha-beta model with that time (``bucket_plan["source"]`` =
+        "alpha-beta", ``"bwd_ms"`` the agreed time)."""
         super().__init__()
         if mode not in ("overlap", "manual"):
             raise ValueError("mode must be 'overlap' or 'manual'")
@@ -126,7 +140,16 @@ class DistributedDataParallel(nn.Module):
         esz = 2 if comm_dtype == torch.bfloat16 else self.flat.grad.element_size()
         plan_cap, plan_first = plan_buckets(self.flat.numel * esz, self.world_size, bwd_ms_hint)
         self.bucket_plan = {"cap_mb": bucket_cap_mb or plan_cap, "first_mb": first_bucket_mb or plan_first,
-                            "source": "explicit" if bucket_cap_mb else ("alpha-beta" if bwd_ms_hint else "default")}
+                            "source": "explicit" if bucket_cap_mb else ("alpha-beta" if bwd_ms_hint else "default"),
+                            "replans": 0}
+        import os
+        if auto_plan is None:
+            auto_plan = (bucket_cap_mb is None and first_bucket_mb is None and bwd_ms_hint is None
+                         and os.environ.get("MLT_DDP_AUTOPLAN", "1") != "0")
+        self._auto_plan = bool(auto_plan) and mode == "overlap" and self.world_size > 1
+        self._grad_bytes = self.flat.numel * esz
+        self._synced_bwd = 0     # synchronised backwards seen
+        self._bwd_t = None       # (start, end) of the timed backward: cuda events or host seconds
         self._bucket_cap = int(self.bucket_plan["cap_mb"] * 2 ** 20)
         self._first_cap = int(self.bucket_plan["first_mb"] * 2 ** 20)
         self._build_buckets()
@@ -279,6 +302,8 @@ class DistributedDataParallel(nn.Module):
             if not self._callback_queued:
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish)
                 self._callback_queued = True
+                if self._auto_plan and self._synced_bwd == 1 and self._bwd_t is None:
+                    self._bwd_t = [self._mark(), None]  # the second synced backward: timed
             b = self._param_bucket[i]
             self._pending[b] -= 1
             if self._pending[b] == 0 and not self._launched[b]:
@@ -286,7 +311,45 @@ class DistributedDataParallel(nn.Module):
                 self._works.append(self._reduce_bucket(b))
         return hook
 
+    def _mark(self):
+        if self.flat.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        import time
+        return time.perf_counter()
+
+    def _maybe_replan(self) -> None:
+        """At the forward after the timed backward: agree the backward time (MAX over ranks, so
+        every rank computes the same plan), then rebuild the buckets once from the alpha-beta model."""
+        if not self._auto_plan or self._bwd_t is None or self._bwd_t[1] is None:
+            return
+        t0, t1 = self._bwd_t
+        self._auto_plan = False
+        if isinstance(t0, float):
+            ms = (t1 - t0) * 1e3
+        else:
+            t1.synchronize()
+            ms = t0.elapsed_time(t1)
+        dev = self.flat.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        ms = float(t.item())
+        cap, first = plan_buckets(self._grad_bytes, self.world_size, ms)
+        self.bucket_plan = {"cap_mb": cap, "first_mb": first, "source": "alpha-beta", "bwd_ms": round(ms, 4),
+                            "replans": 1}
+        old = list(self._buckets)
+        self._bucket_cap = int(cap * 2 ** 20)
+        self._first_cap = int(first * 2 ** 20)
+        self._build_buckets()
+        if self._buckets != old:
+            self._pending = list(self._bucket_counts)
+            self._launched = [False] * len(self._buckets)
+
     def _finish(self) -> None:
+        if self._bwd_t is not None and self._bwd_t[1] is None:
+            self._bwd_t[1] = self._mark()  # backward compute done (before the last collectives)
+        self._synced_bwd += 1
         # buckets whose params got no gradient this step (unused params): reduce them now
         for b in range(len(self._buckets)):
             if not self._launched[b] and self._bucket_counts[b] > 0:
@@ -382,6 +445,8 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         if self.flat.rebind_params():
             pass  # something replaced p.data (e.g. .to()); views restored
+        if self._auto_plan and self._bwd_t is not None and self._bwd_t[1] is not None and torch.is_grad_enabled():
+            self._maybe_replan()
         if self.timing and self._comm_stream is not None and self.require_sync and torch.is_grad_enabled():
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()

@@ -31,8 +31,8 @@ for prec in bf16 fp32; do
   done
 done
 if [ "$ngpu" -ge 8 ]; then
-  # N = 8 transport A/B of the bf16 step under both batch semantics: the fused two-launch xGMI
-  # exchange (default), the four-launch step with the one-/two-shot vote (MLT_LENET_FUSED_DP=0),
+  # N = 8 transport A/B of the bf16 step under both batch semantics: the one-launch xGMI-fused
+  # step (default), the four-launch step with the one-/two-shot vote (MLT_LENET_FUSED_DP=0),
   # and RCCL forced (MLT_XGMI_AR=0)
   for scaling in weak reference; do
     for variant in fused fourlaunch rccl; do
@@ -49,9 +49,12 @@ if [ "$ngpu" -ge 8 ]; then
       tail -n 1 "$out"
     done
   done
-  # kernel trace of the 8-rank reference-semantics step (per-kernel time of every rank)
+  # kernel trace of the 8-rank reference-semantics step (per-kernel time of every rank): the
+  # launcher OUTSIDE the profiler, one rocprofv3 per rank with bench.py directly after its `--`
+  # (scripts/prof_rank.sh); bench.py sees WORLD_SIZE and does not self-launch
   mkdir -p gpurun_out/prof_n8
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n8 -o n8 -- \
+  timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+    --master-port 29537 --no-python scripts/prof_rank.sh gpurun_out/prof_n8 -- \
     python3 -u bench.py --gpus 8 --steps 500 --warmup 50 --scaling reference --no-fp32-companion \
     > gpurun_out/prof_n8/bench.log 2>&1 || echo "=== rocprofv3 N=8 trace failed (see gpurun_out/prof_n8/bench.log)"
   bash scripts/bucket_sweep.sh 8 10 && cat gpurun_out/bucket_sweep.jsonl >> "$out"

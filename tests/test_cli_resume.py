@@ -150,6 +150,24 @@ def test_fit_error_not_masked_by_checkpoint_error(tmp_path, monkeypatch):
         tr.fit()
 
 
+def test_fit_inside_except_block_raises_checkpoint_error(tmp_path, monkeypatch):
+    """A successful fit() called from inside a caller's except block (a retry handler) still raises
+    a failed final checkpoint write: the finally block tests its own success flag, not
+    sys.exc_info() (which would see the caller's handled exception)."""
+    tr_set, va_set = SyntheticCIFAR10(64, True, seed=1), SyntheticCIFAR10(32, False, seed=1)
+    tr = Trainer(MLModel("tiny"), datasets=(tr_set, va_set), epochs=1, batch_size=32, model_dir=str(tmp_path),
+                 options={"progress": False, "async_checkpoint": True})
+
+    def bad_wait():
+        raise OSError("disk gone")
+    monkeypatch.setattr(tr, "_checkpoint_wait", bad_wait)
+    with pytest.raises(OSError, match="disk gone"):
+        try:
+            raise KeyError("the caller's earlier, handled error")
+        except KeyError:
+            tr.fit()
+
+
 def test_watchdog_fires_and_beats():
     fired = []
     w = Watchdog(0.3, on_timeout=lambda: fired.append(1), poll_s=0.05).start()

@@ -256,3 +256,51 @@ def test_bucket_plan_alpha_beta():
     cap, _ = plan_buckets(440 * mb, 8, bwd_ms=2.9, alpha_us=25.0, bus_gbps=300.0)
     beta_m = t - 25.0
     assert abs(cap - min(MAX_BUCKET_MB, max(MIN_BUCKET_MB, 440 * 25.0 / (2900.0 - beta_m)))) < 1e-9
+
+
+def _autoplan_worker(rank, world, port, out_dir, auto, cap, first):
+    dist_env(rank, world, port)
+    # a cheap wire and a tiny minimum bucket: the planned layout differs from the 32 / 4 MB default
+    os.environ["MLT_DDP_MIN_BUCKET_MB"] = "0.0001"
+    os.environ["MLT_DDP_ALPHA_US"] = "0.05"
+    os.environ["MLT_DDP_BUS_GBPS"] = "1000"
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(5)
+    model = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(6)])
+    ddp = (DistributedDataParallel(model) if auto else
+           DistributedDataParallel(model, bucket_cap_mb=cap, first_bucket_mb=first))
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    g = torch.Generator().manual_seed(11 + rank)
+    layouts = []
+    for _ in range(5):
+        x = torch.randn(16, 64, generator=g)
+        opt.zero_grad(set_to_none=False)
+        ddp(x).pow(2).mean().backward()
+        opt.step()
+        layouts.append(list(ddp._buckets))
+    torch.save({"params": ddp.flat.data.clone(), "plan": ddp.bucket_plan, "layouts": layouts},
+               os.path.join(out_dir, f"{'a' if auto else 'f'}{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_autoplan_rebuckets_once_bitwise():
+    """DDP without explicit caps times its second synchronised backward, agrees the MAX over ranks at
+    the next forward and rebuilds its buckets ONCE from the alpha-beta model (bucket_plan source
+    'alpha-beta'); training is bitwise equal to fixed caps of the same layout, on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_autoplan_worker, args=(world, free_port(), d, True, None, None), nprocs=world, join=True)
+        a = [torch.load(os.path.join(d, f"a{r}.pt"), weights_only=True) for r in range(world)]
+        plan = a[0]["plan"]
+        assert plan["source"] == "alpha-beta" and plan["replans"] == 1 and plan["bwd_ms"] > 0
+        assert a[1]["plan"] == plan  # agreed: the same plan on every rank
+        lay = a[0]["layouts"]
+        assert lay[0] == lay[1] and lay[2] == lay[3] == lay[4]  # rebuilt once, before the 3rd step
+        assert lay[2] != lay[0] and len(lay[2]) > 1
+        mp.spawn(_autoplan_worker, args=(world, free_port(), d, False, plan["cap_mb"], plan["first_mb"]),
+                 nprocs=world, join=True)
+        f = [torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True) for r in range(world)]
+        assert f[0]["layouts"][0] == lay[2]
+        for r in range(world):
+            assert torch.equal(a[r]["params"], f[r]["params"])

@@ -25,3 +25,16 @@ def test_train_local_then_test(tmp_path):
         ["--model_path", os.path.join(out, "model.pth"), "--synthetic", "--n_val", "64"])
     # same checkpoint and val set; random crop/flip augmentation differs between the two passes
     assert abs(loss2 - loss) < 0.05 and 0.0 <= acc2 <= 1.0
+
+
+def test_distributed_example_runs_config3_bf16():
+    """examples/02 (the SageMaker-distributed flow) trains BASELINE config 3 -- the bf16 step --
+    unless PRECISION overrides it; main.py's own default stays the reference dtype (fp32)."""
+    import shlex
+    src = open(os.path.join(ROOT, "examples", "02_train_distributed.sh")).read()
+    cmd = " ".join(l.rstrip("\\") for l in src.splitlines() if not l.lstrip().startswith("#"))
+    toks = shlex.split(cmd.replace('"${PRECISION:-bf16}"', "bf16"), posix=True)
+    i = toks.index("--precision")
+    assert toks[i + 1] == "bf16"
+    import main
+    assert main.build_parser().parse_args([]).precision == "fp32"
