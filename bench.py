@@ -375,7 +375,10 @@ def bench_lenet(args, world, rank, dev, backend, precision):
                 engine.start_epoch(torch.as_tensor(ev[1], dtype=torch.int32))
             else:
                 _, b, k, per_graph = ev
-                engine.train_steps(b, k, use_graph=use_graph, steps_per_graph=per_graph)
+                # flush=False: a one-launch step's update runs at the head of the next step's launch
+                # (steady-state pipelining: K launches carry K steps and K updates); the last one
+                # is flushed after the timed region
+                engine.train_steps(b, k, use_graph=use_graph, steps_per_graph=per_graph, flush=False)
                 samples += b * k
         return samples
 
@@ -416,7 +419,10 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     else:
         total_samples = float(samples)
     # sanity: training actually ran (finite loss accumulated on device); transport healthy
+    engine.flush()
     loss_sum = float(engine.stats[0].item())
+    if engine.sync_error():
+        raise RuntimeError("one-launch step: an in-launch wait gave up (a block never became resident)")
     engine.check_transport()
     value = total_samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -452,6 +458,9 @@ def bench_lenet(args, world, rank, dev, backend, precision):
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
                    "hipgraph_steps": 0 if args.no_graph else spg,
                    "kernels_per_step": round(nodes / spg, 2) if nodes else None,
+                   "update": ("pipelined: step k's batch reductions / exchange / optimizer update run in "
+                              "step k+1's launch beside its sample blocks' input phase"
+                              if nodes and nodes == spg else "in-step"),
                    "ddp_comm": comm,
                    "dp_transport": engine.dp_transport,
                    "comm_ranks": engine.comm.size if engine.comm is not None else None,

@@ -98,6 +98,16 @@ def _run(cmd):
 FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
               "lenet_mfma.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
                                  "-mllvm", "-amdgpu-kernarg-preload-count=12"]}
+# translation units split off a kernel file for parallel compilation share its flags
+# (lenet_mfma_1l_w*.hip: the one-launch step's per-world-size instantiations of lenet_mfma.inc)
+FILE_ALIASES = {"lenet_mfma_1l_": "lenet_mfma.hip"}
+
+
+def _flag_key(name: str) -> str:
+    for prefix, key in FILE_ALIASES.items():
+        if name.startswith(prefix):
+            return key
+    return name
 
 
 # kernels whose accumulators live in AGPRs owned by inline asm (gemm_w4.hip): the build also emits
@@ -131,8 +141,8 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
         cmd = [HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common, "-munsafe-fp-atomics",
-               "-Wno-unused-result", *FILE_FLAGS.get(os.path.basename(s), []),
-               *(extra_flags or {}).get(os.path.basename(s), [])]
+               "-Wno-unused-result", *FILE_FLAGS.get(_flag_key(os.path.basename(s)), []),
+               *(extra_flags or {}).get(_flag_key(os.path.basename(s)), [])]
         if force or _newer(s, o, hdrs, cmd):
             jobs_list.append(cmd)
             if os.path.basename(s) in AGPR_GUARDED:  # + its device asm for the AGPR-spill guard

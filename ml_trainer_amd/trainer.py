@@ -12,9 +12,11 @@ the north star: ``train_step(batch)`` and ``evaluate(loader=None)``.
 Under that surface (MI355X-first):
 
 * **fused step engine** -- for the reference LeNet on a GPU the whole training
-  step (augmentation, fwd, CE, metrics, bwd, optimizer) runs as five native
-  kernels replayed as multi-step hipGraphs (``models/lenet_engine.py``): no
-  per-step host syncs (fix B12), no H2D copies (HBM-resident dataset);
+  step (augmentation, fwd, CE, metrics, bwd, optimizer) runs natively: bf16 as
+  ONE kernel per step (the previous step's update folded into the next step's
+  launch), fp32 as four, replayed as multi-step hipGraphs
+  (``models/lenet_engine.py``): no per-step host syncs (fix B12), no H2D copies
+  (HBM-resident dataset);
 * **generic path** -- any ``nn.Module``: native fused optimizer over a flat
   parameter buffer, native flat-bucket DDP with backward-overlapped RCCL
   all-reduce, pinned-host prefetch on a copy stream, on-device loss/metric
@@ -33,7 +35,6 @@ import json
 import math
 import os
 import random
-import sys
 import time
 import warnings
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -447,15 +448,15 @@ class Trainer:
         done = 0
         while done < full:
             k = min(spg, full - done)
-            eng.train_steps(B, k, use_graph=self.opts.use_graph, steps_per_graph=spg)
+            eng.train_steps(B, k, use_graph=self.opts.use_graph, steps_per_graph=spg, flush=False)
             done += k
             bar.update(k)
             if self._watchdog:
                 self._watchdog.beat()
         if last:
-            eng.train_steps(last, 1, use_graph=self.opts.use_graph, steps_per_graph=1)
+            eng.train_steps(last, 1, use_graph=self.opts.use_graph, steps_per_graph=1, flush=False)
             bar.update(1)
-        loss, acc = eng.read_stats(n)  # the ONE host sync of the epoch
+        loss, acc = eng.read_stats(n)  # the ONE host sync of the epoch (flushes the pending update)
         eng.check_transport()
         bar.set_postfix(loss=loss, metric=acc if self.metric else None)
         bar.close()
@@ -684,6 +685,7 @@ class Trainer:
         if self._watchdog:
             self._watchdog.start()
         self._in_fit = True
+        ok = False  # (not sys.exc_info(): a fit() called inside a caller's except block sees theirs)
         try:
             for epoch in range(self.start_epoch, self.epochs + 1):
                 logger.info(f"{'-' * 30} EPOCH {epoch} / {self.epochs} {'-' * 30}")
@@ -706,11 +708,12 @@ class Trainer:
                     logger.info(f"train loss: {self.train_losses[-1]}")
                     logger.info(f"valid loss: {self.val_losses[-1]}\n\n")
                 self._write_metrics(epoch)
+            ok = True
         finally:
             self._in_fit = False
             if self._watchdog:
                 self._watchdog.stop()
-            if sys.exc_info()[0] is None:
+            if ok:
                 self._checkpoint_wait()  # the last async model.pth is on disk when fit() returns
             else:
                 # training already failed: wait for the pending write, but let the ORIGINAL

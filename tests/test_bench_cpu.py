@@ -34,6 +34,9 @@ class _FakeCEngine:
     def run(self, mode, B):
         self.replayed.append((B, 1))
 
+    def flush(self):
+        pass
+
 
 class _FakeC:
     LENET_FWD, LENET_CE, LENET_BWD, LENET_OPT, LENET_REDUCE = 1, 2, 4, 8, 16
