@@ -1185,6 +1185,21 @@ class LeNetEngine {
     }
   }
   int pending() const { return pending_b_; }
+  // transport bring-up: the batch reductions of the current activation / slab buffers into the
+  // flat gradient (exchange = the fused xGMI exchange too), no update; stats and stepinfo[3] as a
+  // flush leaves them. Nothing may be pending.
+  void reduce_only(int B, bool exchange) {
+    TORCH_CHECK(pending_b_ == 0, "reduce_only: flush the pending step first");
+    TORCH_CHECK(prec_ == 1 && P_.stepinfo && O_.g, "reduce_only: bf16 engine with set_opt");
+    TORCH_CHECK(B > 0 && B <= max_b_, "reduce_only: batch");
+    if (exchange) {
+      TORCH_CHECK(xgmi_ != nullptr, "reduce_only: no xGMI transport");
+      const XgmiFused X = xgmi_->fused_view();
+      launch_lenet_mfma_flush(cfg_, B, P_, O_, &X, cur_stream(), false);
+    } else {
+      launch_lenet_mfma_flush(cfg_, B, P_, O_, nullptr, cur_stream(), false);
+    }
+  }
   void set_onelaunch(bool on) {
     flush();
     onelaunch_ = on;
@@ -1375,6 +1390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
   m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));
   m.def("lenet_mfma_kw_blocks", &lenet_mfma_kw_blocks, py::arg("cfg"));
+  m.def("lenet_mfma_xch_granules", &lenet_mfma_xch_granules, py::arg("cfg"));
   m.def("get_lenet_variant", &get_lenet_variant);
   m.def("fp8_cast", &fp8_cast, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("fmt") = 0);
@@ -1419,6 +1435,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &PyXgmi::open)
       .def("all_reduce", &PyXgmi::all_reduce, py::arg("tensor"), py::arg("average") = true)
       .def("error", &PyXgmi::error)
+      .def_property_readonly("world", [](PyXgmi& x) { return x.raw().world(); })
       .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms)
       .def_property("algo", &PyXgmi::algo, &PyXgmi::set_algo)
       .def_property("fault", &PyXgmi::fault, &PyXgmi::set_fault);
@@ -1449,6 +1466,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("replay", &LeNetEngine::replay)
       .def("invalidate_shadow", &LeNetEngine::invalidate_shadow)
       .def("flush", &LeNetEngine::flush)
+      .def("reduce_only", &LeNetEngine::reduce_only, py::arg("B"), py::arg("exchange"))
       .def_property_readonly("pending", &LeNetEngine::pending)
       .def_property("onelaunch", &LeNetEngine::onelaunch_enabled, &LeNetEngine::set_onelaunch)
       .def("graph_nodes", &LeNetEngine::graph_nodes)

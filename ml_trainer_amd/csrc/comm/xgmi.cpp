@@ -13,13 +13,14 @@ static void hcheck(hipError_t e, const char* what) {
 }
 
 // region: data [2][cap] | flags [2][G][W] | t1 [2][W][slot] | t2 [2][W][slot] | f1 [2][G][W] | f2 [2][G][W]
-//         | ff [2][kFusedBlocks][W]
+//         | fg [2][max(cap, kFusedGranules)] (the fused step's granules) | fe (its device error word)
 // (the t* / f* parts belong to the two-shot algorithm, ff to the fused LeNet step's exchange, which
 // shares `data`), every part 256-byte aligned
 struct RegionLayout {
   size_t flags, t1, t2, f1, f2, fg, fe, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+static int64_t fused_cap(int64_t cap) { return cap > XgmiAllReduce::kFusedGranules ? cap : XgmiAllReduce::kFusedGranules; }
 static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
   RegionLayout L;
   const size_t fl = (size_t)2 * blocks * world * sizeof(uint64_t), tb = (size_t)2 * world * slot * sizeof(float);
@@ -28,8 +29,8 @@ static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t sl
   L.t2 = align256(L.t1 + tb);
   L.f1 = align256(L.t2 + tb);
   L.f2 = align256(L.f1 + fl);
-  L.fg = align256(L.f2 + fl);                                // fused step: [2][cap] granules
-  L.fe = align256(L.fg + (size_t)2 * cap * sizeof(uint64_t));  // fused step: device error word
+  L.fg = align256(L.f2 + fl);                                           // fused step: [2][fcap] granules
+  L.fe = align256(L.fg + (size_t)2 * fused_cap(cap) * sizeof(uint64_t));  // fused step: device error word
   L.bytes = L.fe + 256;
   return L;
 }
@@ -125,7 +126,7 @@ XgmiFused XgmiAllReduce::fused_view() const {
   X.seqs = fseqs_;
   X.err = err_;
   X.derr = derr_;
-  X.cap = cap_;
+  X.cap = fused_cap(cap_);
   X.timeout = timeout_ms_ * 100000LL;
   X.rank = rank_;
   X.W = world_;

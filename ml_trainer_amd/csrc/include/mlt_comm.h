@@ -81,6 +81,9 @@ class XgmiAllReduce {
   // ([2][cap] x 8 bytes), per-block counters of its own, the device copy of the error word; timeout /
   // fault as set now (graphs keep the values they were captured with). World size 1 = loopback.
   static constexpr int kFusedBlocks = 128;
+  // granules per parity of the fused LeNet exchange (its own index space, lenet_mfma.inc
+  // xch_granules: conv elements + 256 lane-contiguous granules per fc weight-gradient wave)
+  static constexpr int64_t kFusedGranules = 1 << 17;
   XgmiFused fused_view() const;
 
  private:

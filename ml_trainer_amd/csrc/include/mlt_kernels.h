@@ -123,8 +123,10 @@ int lenet_mfma_wimg_elems();
 bool lenet_mfma_onelaunch_ok(int cfg, int B, int W);  // W = 0: no exchange
 void launch_lenet_mfma_onelaunch(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                                  unsigned long long* sync, const XgmiFused* X, hipStream_t stream);
+// opt = false: batch reductions (+ the exchange when X) into O.g only, no update (self-test / timing)
 void launch_lenet_mfma_flush(int cfg, int B, const LeNetPtrs& P, const LeNetOpt& O, const XgmiFused* X,
-                             hipStream_t stream);
+                             hipStream_t stream, bool opt = true);
+int64_t lenet_mfma_xch_granules(int cfg);  // granules per parity the fused exchange needs
 // shadow + wimg from the fp32 masters (O.p)
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);
 void set_lenet_variant(int v);  // 0 default (4 launches), 1 fully fused per-sample chain, 2 split conv2 / fc

@@ -21,12 +21,15 @@ void launch_lenet_mfma_onelaunch(int cfg, int mode, int B, const LeNetPtrs& P, c
   }
 }
 void launch_lenet_mfma_flush(int cfg, int B, const LeNetPtrs& P, const LeNetOpt& O, const XgmiFused* X,
-                             hipStream_t stream) {
+                             hipStream_t stream, bool opt) {
   if (B <= 0) return;
   if (cfg == LENET_TINY)
-    lm::flush<lm::DmTiny>(B, P, O, X, stream);
+    lm::flush<lm::DmTiny>(B, P, O, X, stream, opt);
   else
-    lm::flush<lm::DmDefault>(B, P, O, X, stream);
+    lm::flush<lm::DmDefault>(B, P, O, X, stream, opt);
+}
+int64_t lenet_mfma_xch_granules(int cfg) {
+  return cfg == LENET_TINY ? lm::xch_granules<lm::DmTiny>() : lm::xch_granules<lm::DmDefault>();
 }
 
 void launch_lenet_mfma_dp(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,

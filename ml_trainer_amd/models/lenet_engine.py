@@ -50,10 +50,15 @@ CIFAR_STD = (0.2023, 0.1994, 0.2010)
 
 
 def fused_dp_enabled() -> bool:
-    """bf16 + xGMI: fold the gradient exchange into the batch-reduction kernel (MLT_LENET_FUSED_DP=0:
-    the four-launch step, for A/B)."""
+    """bf16 + xGMI: fold the gradient exchange into the step (MLT_LENET_FUSED_DP=0: the four-launch
+    step, for A/B; 2: take the fused step whenever its self-test passes, without the timed vote)."""
     import os
     return os.environ.get("MLT_LENET_FUSED_DP", "1") != "0"
+
+
+def fused_dp_forced() -> bool:
+    import os
+    return os.environ.get("MLT_LENET_FUSED_DP", "1") == "2"
 
 
 class TransportError(RuntimeError):
@@ -104,8 +109,9 @@ class LeNetStepEngine:
         self.xgmi = None
         self.captures = 0  # hipGraphs captured so far (bench asserts none inside its timed region)
         self.dp_transport = "none" if self.world_size == 1 else "torch.distributed"
-        if self.world_size > 1:
-            self._setup_transport(process_group)
+        # the transport is chosen once the optimizer is known (its self-test / timing trial runs the
+        # engine's batch-reduction kernels, which need the flat-buffer layout of set_optimizer)
+        self._transport_pending = self.world_size > 1
         self.optimizer = None
         self.lr_table: Optional[torch.Tensor] = None
         self._use_table = False
@@ -143,13 +149,15 @@ class LeNetStepEngine:
             self.xgmi = x = None
         if self.comm is None and self.xgmi is None:
             return
+        fused_ok = False
         if x is not None and self.precision == "bf16" and fused_dp_enabled():
-            # bf16 over xGMI: exchange + update folded into the batch-reduction kernel (two
-            # launches per step, as at W = 1) -- no standalone collective to vote on
-            self.eng.set_xgmi(x)
-            self.eng.fused_dp = True
-            self.dp_transport = "xgmi-fused"
-            return
+            # bf16 over xGMI: the exchange can run inside the step (one launch per step), but only
+            # once its own protocol -- not just the one-/two-shot kernels -- proved bit-exact on
+            # this fabric, on every rank
+            fused_ok = self._fused_selftest(x, process_group)
+            if not fused_ok:
+                warnings.warn("fused xGMI exchange failed its self-test on some rank; using the "
+                              "four-launch data-parallel step")
         self.eng.fused_dp = False
         t = self.flat.grad.clone()
         cands = []
@@ -166,6 +174,13 @@ class LeNetStepEngine:
                 cands.append(("xgmi2", two))
         if self.comm is not None:
             cands.append(("rccl", lambda: self.comm.all_reduce(t, "avg")))
+        if fused_ok:
+            # the fused step's exchange (batch reductions + granule exchange, one launch) against the
+            # four-launch step's collective behind the same batch reductions
+            B = self.max_batch
+            self.eng.set_xgmi(x)
+            cands.append(("xgmi-fused", lambda: self.eng.reduce_only(B, True)))
+            cands.append(("reduce", lambda: self.eng.reduce_only(B, False)))
         times = {}
         for name, fn in cands:
             for _ in range(5):
@@ -179,7 +194,7 @@ class LeNetStepEngine:
             times[name] = s.elapsed_time(e) / 50
         # every rank votes with its own timings and health: the slowest rank decides (MAX), and
         # an xGMI error word raised on ANY rank during the trial rules the xGMI kernels out
-        names = ("xgmi", "xgmi2", "rccl")
+        names = ("xgmi", "xgmi2", "rccl", "xgmi-fused", "reduce")
         bad = 1.0 if (x is not None and x.error()) else 0.0
         coll_dev = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
         vote = torch.tensor([bad] + [times.get(k, float("inf")) for k in names], device=coll_dev)
@@ -188,9 +203,19 @@ class LeNetStepEngine:
         bad, agreed = v[0], dict(zip(names, v[1:]))
         if x is not None and bad != 0.0:
             warnings.warn("xGMI all-reduce failed its timing trial on some rank; using RCCL")
-            agreed["xgmi"] = agreed["xgmi2"] = float("inf")
+            agreed["xgmi"] = agreed["xgmi2"] = agreed["xgmi-fused"] = float("inf")
         self.transport_times_ms = {k: agreed[k] for k in names if k in times}
-        best = min(names, key=lambda k: agreed[k])
+        self.flat.grad.zero_()
+        self.stats.zero_()  # (the trial reductions accumulated their stats)
+        four = min(("xgmi", "xgmi2", "rccl"), key=lambda k: agreed[k])
+        if fused_ok and (fused_dp_forced() or agreed["xgmi-fused"] <= agreed["reduce"] + agreed[four]):
+            self.eng.set_comm(None)
+            self.eng.set_xgmi(x)
+            self.eng.fused_dp = True
+            self.dp_transport = "xgmi-fused"
+            return
+        self.eng.set_xgmi(None)
+        best = four
         if agreed[best] == float("inf"):  # only a failed xGMI and no RCCL: leave torch.distributed
             return
         if best == "rccl":
@@ -200,6 +225,56 @@ class LeNetStepEngine:
             x.algo = 0 if best == "xgmi" else 1
             self.eng.set_xgmi(x)
             self.dp_transport = "xgmi-oneshot" if best == "xgmi" else "xgmi-twoshot"
+
+    def _fused_selftest(self, x, process_group, rounds: int = 12) -> bool:
+        """Bring-up test of the fused step's exchange protocol on the real fabric (collective):
+        ``rounds`` back-to-back rounds, each with fresh random per-rank activations / slabs, of the
+        batch reductions alone (this rank's gradient) and of the batch reductions + granule exchange
+        (the lenet_mwx kernel the fused step's update blocks share), under GEMM load from a side
+        stream; every exchanged gradient word is compared with the host's RANK-ORDERED sum of every
+        rank's local gradient (what each rank's kernel computes), bitwise. MIN vote over ranks."""
+        import torch.distributed as dist
+        dev = self.device
+        W = dist.get_world_size(process_group)
+        rank = dist.get_rank(process_group)
+        B = self.max_batch
+        self.eng.set_xgmi(x)
+        names = ("slab1", "p2", "h1", "h2", "dh1", "dh2", "dlogits")
+        side = torch.cuda.Stream(dev)
+        a = torch.randn(2048, 2048, device=dev)
+        torch.cuda.synchronize(dev)
+        with torch.cuda.stream(side):  # uneven load on the chip while the exchanges run
+            for _ in range(8):
+                a = torch.tanh(a @ a * 1e-3)
+        gen = torch.Generator(device=dev)
+        local, got = [], []
+        for it in range(rounds):
+            gen.manual_seed(0x5EED + 7919 * rank + 104729 * it)
+            for nm in names:
+                self.bufs[nm].normal_(generator=gen)
+            self.eng.reduce_only(B, False)
+            local.append(self.flat.grad.clone())
+            self.eng.reduce_only(B, True)
+            got.append(self.flat.grad.clone())
+        torch.cuda.synchronize(dev)
+        coll_dev = dev if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+        mine = torch.stack(local).to(coll_dev)
+        parts = [torch.empty_like(mine) for _ in range(W)]
+        dist.all_gather(parts, mine, group=process_group)
+        ref = parts[0].cpu().clone()
+        for q in range(1, W):
+            ref = ref + parts[q].cpu()  # rank order, fp32: what the kernel sums
+        ref = ref * torch.tensor(1.0 / W, dtype=torch.float32)
+        ok = bool(torch.equal(ref, torch.stack(got).cpu())) and x.error() == 0
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
+        for nm in names:
+            self.bufs[nm].zero_()
+        self.flat.grad.zero_()
+        self.stats.zero_()
+        self.eng.set_xgmi(None)
+        self.fused_selftest_ok = int(flag.item()) == 1
+        return self.fused_selftest_ok
 
     def _poll_transport(self) -> None:
         """Non-blocking health check of the in-graph collective, run after every graph replay:
@@ -243,6 +318,9 @@ class LeNetStepEngine:
         self.eng.set_opt(self.flat.data, self.flat.grad, s1, s2, h["kind"], h["lr"], h["momentum"], h["dampening"],
                          h["weight_decay"], h["beta1"], h["beta2"], h["eps"], h["lr_decay"], h["grad_scale"],
                          h["nesterov"], h["maximize"], lr_t, self._use_table, self.offsets)
+        if self._transport_pending:  # collective: every rank sets its optimizer at the same point
+            self._transport_pending = False
+            self._setup_transport(self.pg)
 
     def set_dataset(self, data_u8: torch.Tensor, targets: torch.Tensor, batch_size: int, augment: bool = True,
                     pad: int = 4, flip: bool = True, mean: Sequence[float] = CIFAR_MEAN,

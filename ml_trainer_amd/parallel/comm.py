@@ -112,6 +112,14 @@ def create_xgmi_allreduce(process_group=None, capacity: int = 0, device: Optiona
     if one != 1:
         return None
     x.two_shot_ok = two == 1
+    # fault injection for the bring-up tests: MLT_XGMI_INJECT_FAULT="rank:code" sets x.fault = code
+    # on that rank after the one-/two-shot self-tests (2: the fused exchange publishes corrupted
+    # values -- its own self-test must then reject it on every rank)
+    inj = os.environ.get("MLT_XGMI_INJECT_FAULT", "")
+    if inj:
+        r, code = (int(v) for v in inj.split(":"))
+        if r == rank:
+            x.fault = code
     return x
 
 

@@ -192,8 +192,8 @@ def test_xgmi_allreduce_three_four_eight_ranks_one_gpu(world, algo):
 
 
 def _fused_dp_worker(rank, world, port, out_dir):
-    """bf16 LeNet data-parallel step over xGMI: the two-launch step (exchange folded into the
-    batch-reduction kernel) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
+    """bf16 LeNet data-parallel step over xGMI: the one-launch step (exchange in the update blocks
+    beside the next step's samples) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
     dist_env(rank, world, port)
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
@@ -238,15 +238,70 @@ def _fused_dp_worker(rank, world, port, out_dir):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_lenet_bf16_fused_dp_matches_four_launch(world):
-    """Two launches per data-parallel step, bitwise equal to the four-launch step and identical on
+    """One launch per data-parallel step, bitwise equal to the four-launch step and identical on
     every rank (W = 8: the node's size, as 8 processes on the box's one GPU)."""
     r = _run(_fused_dp_worker, world)
     assert len(r) == world
     for d in r:
         assert d["err1"] == 0 and d["err0"] == 0
         assert torch.equal(d["p1"], d["p0"]) and torch.equal(d["g1"], d["g0"])
-        assert d["nodes1"] == 6 and d["nodes0"] == 12, (d["nodes1"], d["nodes0"])
+        assert d["nodes1"] == 3 and d["nodes0"] == 12, (d["nodes1"], d["nodes0"])  # 1 vs 4 kernels per step
         assert torch.equal(d["p1"], r[0]["p1"])
+
+
+def _selftest_worker(rank, world, port, out_dir, inject):
+    """Transport bring-up of the bf16 engine at W = 2 (both ranks on the box's GPU): the fused
+    exchange's own self-test runs before it may carry a step; MLT_XGMI_INJECT_FAULT="0:2" makes
+    rank 0 publish corrupted values, which rank 1's check catches -- then EVERY rank rejects the
+    fused step (MIN vote) and trains on the four-launch step, replicas still identical."""
+    dist_env(rank, world, port)
+    os.environ["MLT_XGMI_ALLOW_GLOO"] = "1"
+    os.environ["MLT_XGMI_TIMEOUT_MS"] = "20000"
+    if inject:
+        os.environ["MLT_XGMI_INJECT_FAULT"] = "0:2"
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from ml_trainer_amd.models.lenet import MLModel
+    from ml_trainer_amd.models.lenet_engine import LeNetStepEngine
+    from ml_trainer_amd.ops.optim import build_optimizer
+    from ml_trainer_amd.parallel.sampler import shard_indices
+    from ml_trainer_amd.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = MLModel().to(dev)
+    flat = FlatParams(m.parameters())
+    opt = build_optimizer("sgd", m.parameters(), lr=1e-2, momentum=0.9, flat=flat)
+    eng = LeNetStepEngine(m, flat, max_batch=8, optimizer=opt, world_size=world, precision="bf16")
+    gd = torch.Generator().manual_seed(3)
+    N = 64 * world
+    data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
+    targets = torch.randint(0, 10, (N,), generator=gd)
+    eng.set_dataset(data, targets, batch_size=8)
+    eng.start_epoch(torch.as_tensor(shard_indices(N, world, rank, shuffle=True, seed=0, epoch=0), dtype=torch.int32))
+    eng.train_steps(8, 4, use_graph=True, steps_per_graph=2)
+    eng.check_transport()
+    torch.cuda.synchronize()
+    out = {"ok": getattr(eng, "fused_selftest_ok", None), "transport": eng.dp_transport,
+           "times": eng.transport_times_ms, "p": flat.data.cpu()}
+    torch.save(out, os.path.join(out_dir, f"s{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("inject", [False, True])
+def test_fused_exchange_selftest_and_fallback(inject):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_selftest_worker, args=(2, free_port(), d, inject), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"s{i}.pt"), weights_only=True) for i in range(2)]
+    for x in r:
+        assert x["ok"] is (not inject), x
+        if inject:
+            assert x["transport"] in ("xgmi-oneshot", "xgmi-twoshot"), x["transport"]
+        else:
+            assert x["transport"] in ("xgmi-fused", "xgmi-oneshot", "xgmi-twoshot"), x["transport"]
+            assert "xgmi-fused" in x["times"] and "reduce" in x["times"]
+    assert r[0]["transport"] == r[1]["transport"]
+    assert torch.equal(r[0]["p"], r[1]["p"])
 
 
 def _bert_zero_worker(rank, world, port, out_dir):

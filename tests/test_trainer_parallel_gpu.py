@@ -22,6 +22,7 @@ def _worker(rank, world, port, out_dir, precision):
     dist_env(rank, world, port)
     os.environ["MLT_SAME_DEVICE"] = "1"
     os.environ["MLT_XGMI_ALLOW_GLOO"] = "1"
+    os.environ["MLT_LENET_FUSED_DP"] = "2"  # the fused step once it passed its self-test (no timed vote)
     from ml_trainer_amd.data.cifar10 import SyntheticCIFAR10
     from ml_trainer_amd.data.transforms import Compose, Normalize, ToTensor
     from ml_trainer_amd.models.lenet import MLModel
@@ -82,6 +83,7 @@ def _fault_resume_worker(rank, world, port, out_dir):
     dist_env(rank, world, port)
     os.environ["MLT_SAME_DEVICE"] = "1"
     os.environ["MLT_XGMI_ALLOW_GLOO"] = "1"
+    os.environ["MLT_LENET_FUSED_DP"] = "2"  # the fused step once it passed its self-test (no timed vote)
     os.environ["MLT_XGMI_TIMEOUT_MS"] = "300"
     from ml_trainer_amd.data.cifar10 import SyntheticCIFAR10
     from ml_trainer_amd.data.transforms import Compose, Normalize, ToTensor
