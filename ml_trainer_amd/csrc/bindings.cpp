@@ -1009,9 +1009,15 @@ class LeNetEngine {
       TORCH_CHECK(P_.slab1 != nullptr && (int64_t)C1 * 640 >= lenet_mfma_slab_floats(cfg), "slab1 too small");
     }
     if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 2048).data_ptr<float>();
+    // next-step input prep in the batch-reduction kernel (MLT_LENET_PREP=0: off, for A/B)
+    const char* pe = std::getenv("MLT_LENET_PREP");
+    if (bufs.contains("prep") && bufs.contains("pmeta") && !(pe && std::string(pe) == "0")) {
+      P_.prep = get("prep", at::kByte, B * 8192).data_ptr<uint8_t>();
+      P_.pmeta = get("pmeta", at::kLong, B * 4).data_ptr<int64_t>();
+    }
     if (bufs.contains("sync"))
       sync_ = reinterpret_cast<unsigned long long*>(get("sync", at::kLong, 64).data_ptr<int64_t>());
-    if (const char* e = std::getenv("MLT_LENET_ONELAUNCH")) onelaunch_ = std::string(e) != "0";
+    if (const char* e = std::getenv("MLT_LENET_ONELAUNCH")) onelaunch_ = std::string(e) == "1";
     A_ = LeNetAug{};
     O_ = LeNetOpt{};
   }
@@ -1160,9 +1166,9 @@ class LeNetEngine {
     if (one) pending_b_ = B;
   }
 
-  // The bf16 step runs as ONE launch per step (lenet_mfma_1l_*: this step's samples + the previous
-  // step's update) when the whole grid fits the chip and the step is the fused single-rank one or the
-  // xGMI-fused data-parallel one at W in {1, 2, 4, 8}; MLT_LENET_ONELAUNCH=0 keeps the two-launch step
+  // With onelaunch_ the bf16 step runs as ONE launch per step (lenet_mfma_1l_*: this step's samples +
+  // the previous step's update) when the whole grid fits the chip and the step is the fused
+  // single-rank one or the xGMI-fused data-parallel one at W in {1, 2, 4, 8}
   bool onelaunch(int mode, int B) const {
     if (!onelaunch_ || !sync_ || prec_ != 1 || !(mode & LENET_BWD) || !A_.ctrl || !P_.stepinfo) return false;
     const bool local = (mode & LENET_OPT) && !(mode & LENET_REDUCE);
@@ -1331,7 +1337,9 @@ class LeNetEngine {
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
   std::map<int64_t, bool> one_graphs_;  // graph key -> holds one-launch steps
   unsigned long long* sync_ = nullptr;  // one-launch hand-off words ("sync" buffer)
-  bool onelaunch_ = true;
+  // the one-launch step is opt-in (MLT_LENET_ONELAUNCH=1 / .onelaunch): measured slower than the
+  // two-launch step with input prep (profiles/r5/lenet_onelaunch_*.jsonl)
+  bool onelaunch_ = false;
   int pending_b_ = 0;  // batch of the step whose update is still pending (0: none)
   int prec_ = 0;
   bool fused_dp_ = true;

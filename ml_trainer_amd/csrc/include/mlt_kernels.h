@@ -64,6 +64,11 @@ struct LeNetPtrs {
   uint16_t* shadow;          // bf16 copy of the flat fp32 parameters (fc weights are read from it)
   uint16_t* wimg;            // bf16 conv-weight MFMA fragment image (lenet_mfma_wimg_elems())
   float* trace;              // LENET_TRACE phase stamps (8-byte slots) or nullptr
+  // next-step inputs prepared by the batch-reduction kernel's prep blocks (nullptr: off): the
+  // augmented bf16 pixels [B][1024] x (c0, c1 | c2, 0) of the sample each block will compute next,
+  // tagged pmeta[B][4] = (global step, perm position, target, 0); -1 = empty
+  uint8_t* prep;
+  int64_t* pmeta;
 };
 
 struct LeNetAug {

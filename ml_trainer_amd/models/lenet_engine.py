@@ -354,7 +354,7 @@ class LeNetStepEngine:
             self.optimizer.lr_tensor(0)  # sync group lr -> device scalar
 
     def _reset_staging(self) -> None:
-        for k in ("stage_meta", "meta2", "metaN"):
+        for k in ("stage_meta", "meta2", "metaN", "pmeta"):
             self.bufs[k].fill_(-1)
 
     def flush(self) -> None:

@@ -151,10 +151,10 @@ def test_bf16_graph_equals_eager_bitwise(dev):
 
 @pytest.mark.gpu
 def test_bf16_staging_bitwise(dev):
-    """The per-sample kernel stages the next step's raw image two steps deep (metaN -> meta2);
-    a step uses it only on a tag match. Training with staging (graphs, two epochs, a partial last
-    batch) == training with every tag invalidated before each step, bit for bit; in steady state
-    every step of an epoch after the first two hits."""
+    """The batch-reduction kernel's prep blocks augment the next step's inputs (pixels + tags);
+    a step uses them only on a tag match. Training with prepared inputs (graphs, two epochs, a
+    partial last batch) == training with every tag invalidated before each step (the per-sample
+    kernel then gathers and augments itself), bit for bit."""
     data, targets = _toy_data(300, 7)
     runs = []
     for staged in (True, False):
@@ -167,11 +167,12 @@ def test_bf16_staging_bitwise(dev):
             if staged:
                 eng.train_steps(32, 9, use_graph=True, steps_per_graph=3)
                 torch.cuda.synchronize()
-                meta = eng.bufs["meta2"].view(-1, 4)[:12].cpu()
-                # the 9th step (in-epoch index 8) staged in-epoch step 9 (positions 288 + b)
+                meta = eng.bufs["pmeta"].view(-1, 4)[:12].cpu()
+                # the 9th step's (in-epoch index 8) batch-reduction kernel prepared in-epoch step 9
+                # (positions 288 + b): global step, position, target
+                assert meta[:, 0].tolist() == [ep * 10 + 9] * 12, meta
                 assert meta[:, 1].tolist() == list(range(288, 300)), meta
-                assert meta[:, 2].tolist() == perm[288:].tolist()
-                assert meta[:, 3].tolist() == targets[perm[288:]].tolist()
+                assert meta[:, 2].tolist() == targets[perm[288:]].tolist()
             else:
                 for _ in range(9):
                     eng._reset_staging()
@@ -284,10 +285,10 @@ def test_bf16_host_change_of_masters_is_packed(dev):
 @pytest.mark.gpu
 @pytest.mark.parametrize("opt", ["sgd", "adamw"])
 def test_bf16_fused_dp_loopback_matches_fused(dev, opt):
-    """The one-launch data-parallel step (update blocks: batch reductions -> publish granules into
-    the xGMI region -> poll -> rank-ordered sum -> update, beside the next step's sample blocks)
-    against the loopback transport (the only peer is this rank) == the fused single-rank step,
-    bitwise; and the graph holds one kernel per step."""
+    """The two-launch data-parallel step (lenet_mwx: batch reductions -> publish granules into the
+    xGMI region -> poll -> rank-ordered sum -> update, one launch) against the loopback transport
+    (the only peer is this rank) == the fused single-rank step, bitwise; and the graph holds two
+    kernels per step."""
     from ml_trainer_amd.parallel.comm import create_xgmi_loopback
     data, targets = _toy_data(256, 5)
     runs = []
@@ -305,7 +306,7 @@ def test_bf16_fused_dp_loopback_matches_fused(dev, opt):
         torch.cuda.synchronize()
         if dp:
             assert x.error() == 0
-            assert eng.eng.graph_nodes(eng._train_mode(), 32, 3) == 3  # ONE kernel per step
+            assert eng.eng.graph_nodes(eng._train_mode(), 32, 3) == 6  # 2 kernels x 3 steps
         runs.append((flat.data.clone(), flat.grad.clone(), eng.stats.clone(), eng.ctrl.clone()))
     for a, b in zip(runs[0], runs[1]):
         assert torch.equal(a, b)
@@ -424,6 +425,7 @@ def test_bf16_onelaunch_pending_update(dev):
     for n in (3, 4):
         m = _mk("default", 31).to(dev)
         eng, flat = _engine(m, "sgd", max_batch=32, lr=1e-2)
+        eng.eng.onelaunch = True
         eng.set_dataset(data, targets, batch_size=32)
         eng.start_epoch(torch.arange(256))
         eng.train_steps(32, n, use_graph=True, steps_per_graph=n, flush=(n == 3))

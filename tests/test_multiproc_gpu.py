@@ -192,8 +192,9 @@ def test_xgmi_allreduce_three_four_eight_ranks_one_gpu(world, algo):
 
 
 def _fused_dp_worker(rank, world, port, out_dir):
-    """bf16 LeNet data-parallel step over xGMI: the one-launch step (exchange in the update blocks
-    beside the next step's samples) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
+    """bf16 LeNet data-parallel step over xGMI: the two-launch step (exchange folded into the batch-
+    reduction kernel), the opt-in one-launch step (exchange in update blocks beside the next step's
+    samples) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
     dist_env(rank, world, port)
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
@@ -210,12 +211,13 @@ def _fused_dp_worker(rank, world, port, out_dir):
     N = 64 * world
     data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
     targets = torch.randint(0, 10, (N,), generator=gd)
-    for fused in (True, False):
+    for variant, fused, one in (("1", True, False), ("0", False, False), ("one", True, True)):
         torch.manual_seed(0)
         m = MLModel().to(dev)
         flat = FlatParams(m.parameters())
         opt = build_optimizer("adamw", m.parameters(), lr=1e-3, weight_decay=0.01, flat=flat)
         eng = LeNetStepEngine(m, flat, max_batch=8, optimizer=opt, world_size=world, precision="bf16")
+        eng.eng.onelaunch = one
         xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
         assert xe is not None
         xe.algo = 0
@@ -227,10 +229,10 @@ def _fused_dp_worker(rank, world, port, out_dir):
         eng.train_steps(8, 6, use_graph=True, steps_per_graph=3)
         eng.check_transport()
         torch.cuda.synchronize()
-        out[f"p{int(fused)}"] = flat.data.cpu()
-        out[f"g{int(fused)}"] = flat.grad.cpu()
-        out[f"nodes{int(fused)}"] = eng.eng.graph_nodes(eng._train_mode(), 8, 3)
-        out[f"err{int(fused)}"] = xe.error()
+        out[f"p{variant}"] = flat.data.cpu()
+        out[f"g{variant}"] = flat.grad.cpu()
+        out[f"nodes{variant}"] = eng.eng.graph_nodes(eng._train_mode(), 8, 3)
+        out[f"err{variant}"] = xe.error()
         dist.barrier()
     torch.save(out, os.path.join(out_dir, f"f{rank}.pt"))
     dist.destroy_process_group()
@@ -238,14 +240,16 @@ def _fused_dp_worker(rank, world, port, out_dir):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_lenet_bf16_fused_dp_matches_four_launch(world):
-    """One launch per data-parallel step, bitwise equal to the four-launch step and identical on
-    every rank (W = 8: the node's size, as 8 processes on the box's one GPU)."""
+    """Two launches per data-parallel step (and one with the opt-in one-launch step), bitwise equal to
+    the four-launch step and identical on every rank (W = 8: the node's size, as 8 processes on the
+    box's one GPU)."""
     r = _run(_fused_dp_worker, world)
     assert len(r) == world
     for d in r:
-        assert d["err1"] == 0 and d["err0"] == 0
+        assert d["err1"] == 0 and d["err0"] == 0 and d["errone"] == 0
         assert torch.equal(d["p1"], d["p0"]) and torch.equal(d["g1"], d["g0"])
-        assert d["nodes1"] == 3 and d["nodes0"] == 12, (d["nodes1"], d["nodes0"])  # 1 vs 4 kernels per step
+        assert torch.equal(d["pone"], d["p0"]) and torch.equal(d["gone"], d["g0"])
+        assert (d["nodesone"], d["nodes1"], d["nodes0"]) == (3, 6, 12)  # 1 / 2 / 4 kernels per step
         assert torch.equal(d["p1"], r[0]["p1"])
 
 

@@ -75,11 +75,14 @@ def test_trainer_is_parallel_two_ranks_matches_one(precision):
     assert rel < 1e-4, rel.item()
 
 
-def _fault_resume_worker(rank, world, port, out_dir):
+def _fault_resume_worker(rank, world, port, out_dir, asym=False):
     """Epoch 1 healthy (checkpointed: model.pth + trainer_state.pt), then the xGMI transport's fault
     injection makes epoch 2 fail with TransportError on EVERY rank -- after some gradient slices
     were applied on one rank and not the other (the fused exchange applies per slice). A fresh
-    Trainer(resume=True) must restore bit-identical replicas from the checkpoint and train on."""
+    Trainer(resume=True) must restore bit-identical replicas from the checkpoint and train on.
+    asym: only rank 0 withholds its granules (its peers' polls time out while its own succeed, so
+    rank 0 applies that step whole and rank 1 only partly -- the replicas silently diverge -- and
+    rank 1's sticky error then starves rank 0 on the next step): both must still raise."""
     dist_env(rank, world, port)
     os.environ["MLT_SAME_DEVICE"] = "1"
     os.environ["MLT_XGMI_ALLOW_GLOO"] = "1"
@@ -109,7 +112,8 @@ def _fault_resume_worker(rank, world, port, out_dir):
     ck = tr.flat.data.detach().cpu().clone()
     eng = tr._engine
     res = {"transport": eng.dp_transport}
-    eng.xgmi.fault = 1
+    if rank == 0 or not asym:
+        eng.xgmi.fault = 1
     eng.use_transport(xgmi=eng.xgmi)  # recapture with the fault live
     tr.epochs, tr.start_epoch = 2, 2
     try:
@@ -133,13 +137,16 @@ def _fault_resume_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_fused_dp_transport_error_then_resume_restores_replicas():
+@pytest.mark.parametrize("asym", [False, True])
+def test_fused_dp_transport_error_then_resume_restores_replicas(asym):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_fault_resume_worker, args=(2, free_port(), d), nprocs=2, join=True)
+        mp.spawn(_fault_resume_worker, args=(2, free_port(), d, asym), nprocs=2, join=True)
         r = [torch.load(os.path.join(d, f"q{i}.pt"), weights_only=False) for i in range(2)]
     assert r[0]["transport"] == "xgmi-fused"
     assert r[0]["raised"] and r[1]["raised"]
     assert r[0]["start_epoch"] == 2
+    if asym:
+        assert not torch.equal(r[0]["failed_p"], r[1]["failed_p"])  # diverged before the error surfaced
     for i in range(2):
         assert r[i]["diverged_from_ckpt"]  # the failed step was applied on the slices whose peers arrived
         assert torch.equal(r[i]["resumed_p"], r[i]["ckpt_p"])  # restored from model.pth exactly
