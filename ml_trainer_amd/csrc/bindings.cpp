@@ -398,7 +398,7 @@ void gemm(Tensor A, Tensor B, Tensor C, bool a_mn, bool b_mn, c10::optional<Tens
     splits = 1;
     part = at::empty({M / 64 * N}, A.options().dtype(at::kFloat));
   }
-  const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
+  const GemmPlan plan = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits, accumulate ? 1 : 0);
   TORCH_CHECK(!part.defined() || ((plan.cfg == 5 || plan.cfg == 7) && plan.splits == 1),
               "colsum_out: ping-pong / 4-wave plan expected");
   Tensor ws;
@@ -619,8 +619,8 @@ void fp8_update_scale(Tensor hist, Tensor amax, Tensor scale, Tensor inv_scale, 
                           cur_stream());
 }
 
-py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits) {
-  const GemmPlan p = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits);
+py::tuple gemm_plan(bool a_mn, bool b_mn, int64_t M, int64_t N, int64_t K, int cfg, int splits, bool accumulate) {
+  const GemmPlan p = plan_gemm_bf16(a_mn, b_mn, (int)M, (int)N, (int)K, cfg, splits, accumulate ? 1 : 0);
   return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);
 }
 
@@ -1410,7 +1410,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_update_scale", &fp8_update_scale, py::arg("hist"), py::arg("amax"), py::arg("scale"),
         py::arg("inv_scale"), py::arg("fmax"), py::arg("step"), py::arg("margin") = 0);
   m.def("gemm_plan", &gemm_plan, py::arg("a_mn"), py::arg("b_mn"), py::arg("M"), py::arg("N"), py::arg("K"),
-        py::arg("cfg") = -1, py::arg("splits") = 0);
+        py::arg("cfg") = -1, py::arg("splits") = 0, py::arg("accumulate") = false);
   m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd, py::arg("DY"), py::arg("X"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),

@@ -182,7 +182,8 @@ struct GemmPlan {
   int64_t cnt_ints;
   int ext = 0;  // split-K partials summed by a separate grid-wide reduce launch (else: last-arriver in-kernel)
 };
-GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits);
+GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits,
+                        int accumulate = 0);
 void set_gemm_split_mode(int mode);  // -1 planner, 0 in-kernel last-arriver, 1 external reduce
 void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,

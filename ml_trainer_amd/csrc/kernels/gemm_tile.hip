@@ -1116,8 +1116,10 @@ void launch_split_reduce(const GemmPlan& p, const float* ws, OutT* C, int M, int
 
 void set_gemm_split_mode(int mode) { g_split_mode = mode; }
 
-GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits) {
+GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits, int accumulate) {
   (void)b_mn;
+  // (the 4-wave kernel's in-kernel epilogue cannot accumulate into C: an accumulating GEMM takes it
+  // only with split-K partials, whose external reduce accumulates; otherwise the fitted planner)
   // the 4-wave asm kernel (cfg 7) takes every k-contiguous-A (forward / input-gradient) shape it
   // covers: 3-17 % over the ping-pong tile on the BERT forward shapes, 98-101 % of hipBLASLt at
   // 4096^3 / 8192^3 (profiles/r4/gemm_w4_*.jsonl). MLT_GEMM_W4=0 restores the fitted planner.
@@ -1126,8 +1128,8 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
     return !(v && atoi(v) == 0);
   }();
   // (only with enough tiles to fill the chip: few-tile / long-K shapes keep the split-K planner)
-  if (w4 && force_cfg < 0 && force_splits <= 0 && a_mn == 0 && M % 256 == 0 && N % 256 == 0 && K % 128 == 0 &&
-      K >= 256 && (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
+  if (w4 && !accumulate && force_cfg < 0 && force_splits <= 0 && a_mn == 0 && M % 256 == 0 && N % 256 == 0 &&
+      K % 128 == 0 && K >= 256 && (int64_t)(M / 256) * (N / 256) >= kW4MinTiles) {
     GemmPlan p{7, 1, K / 64, 0, 0};
     return p;
   }
@@ -1137,7 +1139,7 @@ GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, 
       K % 128 == 0 && K >= 256) {
     int bs = 0, bks = 0;
     w4_pick_splits((M / 256) * (N / 256), K / 64, M, N, bs, bks);
-    if (bs) {
+    if (bs > 1 || (bs == 1 && !accumulate)) {
       GemmPlan p{7, bs, bks, bs > 1 ? (int64_t)bs * M * N : 0, 0};
       p.ext = bs > 1 ? 1 : 0;
       return p;

@@ -378,3 +378,29 @@ def test_w4_asm_wgrad_split_k(dev):
     ref1 = torch.empty(M, N, device=dev)
     C.gemm(A, B, ref1, True, True, cfg=1)
     torch.testing.assert_close(acc - 0.25, ref1, rtol=1e-5, atol=1e-3)
+
+
+def test_w4_wgrad_accumulate_plan(dev):
+    """An ACCUMULATING weight gradient (A [K][M], B [K][N]) on a shape the 4-wave kernel would take
+    with a single split: that kernel's in-kernel epilogue cannot accumulate, so the planner (told
+    `accumulate`) picks the fitted split-K tile plan instead of handing the launch a cfg-7 plan; the
+    result is C + A^T B against fp32 torch. Multi-split cfg-7 plans keep accumulating in their reduce."""
+    C = require_native()
+    M, N, K = 2048, 2048, 512
+    assert C.gemm_plan(True, True, M, N, K)[:2] == (7, 1)
+    plan = C.gemm_plan(True, True, M, N, K, accumulate=True)
+    assert plan[0] != 7, plan
+    g = torch.Generator().manual_seed(91)
+    A = _mk((K, M), dev, g)
+    B = _mk((K, N), dev, g)
+    ref = A.float().t() @ B.float()
+    acc = torch.full((M, N), -0.5, device=dev)
+    C.gemm(A, B, acc, True, True, accumulate=True)
+    torch.testing.assert_close(acc, ref - 0.5, rtol=1e-4, atol=2e-3)
+    M2, N2, K2 = 768, 3072, 4096  # cfg 7 with split-K partials: accumulates in the external reduce
+    assert C.gemm_plan(True, True, M2, N2, K2, accumulate=True)[:2][0] == 7
+    A2 = _mk((K2, M2), dev, g)
+    B2 = _mk((K2, N2), dev, g)
+    acc2 = torch.full((M2, N2), 1.5, device=dev)
+    C.gemm(A2, B2, acc2, True, True, accumulate=True)
+    torch.testing.assert_close(acc2, A2.float().t() @ B2.float() + 1.5, rtol=1e-4, atol=4e-3)
