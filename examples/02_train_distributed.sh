@@ -4,8 +4,9 @@
 # smdistributed.dataparallel (cells :92-101 hyperparameters, :115-118 distribution,
 # :156-158 fit, :172-186 load_history + plot_history). Here: one process per GPU via
 # torch.distributed.run, RCCL over xGMI, and the fused LeNet engine in bf16 (BASELINE.json config 3:
-# "default config bf16, DDP world_size=8"): one launch per step whose update blocks exchange the
-# gradient over xGMI (PRECISION=fp32 runs the reference dtype's four-kernel step instead).
+# "default config bf16, DDP world_size=8"): two launches per step, the second of which exchanges
+# the gradient over xGMI inside its update blocks when the bring-up vote picks that transport
+# (PRECISION=fp32 runs the reference dtype's four-kernel step instead).
 #
 #   examples/02_train_distributed.sh [NGPUS] [extra main.py flags...]
 set -euo pipefail

@@ -34,6 +34,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -43,6 +44,21 @@ constexpr int AB = 64;  // query / key block
 // raw v_exp_f32 (2^x): exp2f wraps it in a denormal-range fix-up (compare, select, two
 // ldexp) that the probabilities here never need; exp2(-inf) = 0 doubles as the mask
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Backward softmax-gradient math on score PAIRS (build A/B switch, -DMLT_ATTN_PKF32=1): the
+// scale-and-shift and dS = P * dP' of two adjacent accumulator rows as one v_pk_fma_f32 / one
+// v_pk_mul_f32 instead of two scalar ops each; the exp2 stays scalar. Off by default: see
+// profiles/r5/attn_pkf32_ab.jsonl for the measured A/B.
+#ifndef MLT_ATTN_PKF32
+#define MLT_ATTN_PKF32 0
+#endif
+// p = exp2(s * sl2 - lr) and ds = p * dp for rows (r0, r0 + 1) of one f32x4 accumulator
+__device__ __forceinline__ void pk_prob_ds(const f32x4& s, const f32x4& dp, float sl2, f32x2 nlr, int r0, f32x2& p,
+                                           f32x2& d) {
+  const f32x2 x = __builtin_elementwise_fma(f32x2{s[r0], s[r0 + 1]}, f32x2{sl2, sl2}, nlr);
+  p = f32x2{fast_exp2(x.x), fast_exp2(x.y)};
+  d = p * f32x2{dp[r0], dp[r0 + 1]};
+}
 
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -903,6 +919,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qt * 16 + 4 * g);
         const float lr[4] = {l4.x, l4.y, l4.z, l4.w};
         f32x4 pc[NK], dsc[NK];
+        if constexpr (PATH == 0 && MLT_ATTN_PKF32) {
+          const f32x2 nl01 = {-lr[0], -lr[1]}, nl23 = {-lr[2], -lr[3]};
+#pragma unroll
+          for (int n = 0; n < NK; ++n) {
+            f32x2 pa, pb, da, db;
+            pk_prob_ds(sv[n], dp[n], sl2, nl01, 0, pa, da);
+            pk_prob_ds(sv[n], dp[n], sl2, nl23, 2, pb, db);
+            pc[n] = f32x4{pa.x, pa.y, pb.x, pb.y};
+            dsc[n] = f32x4{da.x, da.y, db.x, db.y};
+          }
+        } else {
 #pragma unroll
         for (int n = 0; n < NK; ++n)
 #pragma unroll
@@ -920,6 +947,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
             pc[n][r] = pv;
             dsc[n][r] = pv * dp[n][r];
           }
+        }
 #pragma unroll
         for (int n = 0; n < NK; ++n) {
           if (qt & 1) {
@@ -1123,6 +1151,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
             dp[n] = mfma(va, of[n][kh], dp[n]);
           }
         }
+        if constexpr (FULL && MLT_ATTN_PKF32) {
+#pragma unroll
+          for (int n = 0; n < NQ; ++n) {
+            const f32x2 nl = {-lq[n], -lq[n]};
+            f32x2 pa, pb, da, db;
+            pk_prob_ds(sv[n], dp[n], sl2, nl, 0, pa, da);
+            pk_prob_ds(sv[n], dp[n], sl2, nl, 2, pb, db);
+            ds[n][kt] = f32x4{da.x, da.y, db.x, db.y};
+          }
+        } else
 #pragma unroll
         for (int n = 0; n < NQ; ++n)
 #pragma unroll

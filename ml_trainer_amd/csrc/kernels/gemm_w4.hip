@@ -26,12 +26,53 @@
 
 namespace mlt {
 
+#include "gelu_table.inc"
+
 enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // LDS: two K-tile stages of 64 KB; after the loop, four per-wave 64 x 132 fp32 epilogue images
 __device__ __forceinline__ uint32_t pack2(uint16_t lo, uint16_t hi) { return (uint32_t)lo | ((uint32_t)hi << 16); }
 constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 * kW4Pitch * 4 : 131072;
+
+// GELU / GELU' of the (b)GELU epilogues from exact tables at the bf16 input points (scripts/
+// gen_gelu_table.py: layout, accuracy, why) instead of the A&S erf of mlt_gemm.h; the table sits in
+// LDS behind the epilogue images (158,736 B of the 160 KB). Build switch -DMLT_W4_GELU_TAB=0: the
+// erf polynomial (A/B: profiles/r5/gemm_gelu_tab_ab.jsonl).
+#ifndef MLT_W4_GELU_TAB
+#define MLT_W4_GELU_TAB 1
+#endif
+constexpr int kGeluTabBytes = MLT_GELU_TAB_ENTRIES * 4;
+template <int EK>
+constexpr bool w4_gelu_tab() {
+  return MLT_W4_GELU_TAB && (EK == W4_GELU || EK == W4_DGELU);
+}
+template <int EK>
+constexpr int w4_smem() {
+  return kW4Smem + (w4_gelu_tab<EK>() ? kGeluTabBytes : 0);
+}
+static_assert(kW4Smem + kGeluTabBytes <= 160 * 1024, "GELU table must fit beside the epilogue images");
+// workgroup copy of the epilogue's table into LDS (read only after the epilogue's first barrier)
+template <int EK>
+__device__ __forceinline__ void w4_load_gelu_tab(uint8_t* smem) {
+  if constexpr (w4_gelu_tab<EK>()) {
+    const uint4* src = reinterpret_cast<const uint4*>(EK == W4_GELU ? kGeluPhiTab : kGeluGradTab);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kW4Smem);
+    for (int i = threadIdx.x; i < kGeluTabBytes / 16; i += 256) dst[i] = src[i];
+  }
+}
+// table multipliers of a bf16 pair (element 0 in the low half): index = min(sat(|bits| - (LO - 1)),
+// NR + 1) + sign (NR + 2), both halves at once in 16-bit packed integer ops, then one LDS read each
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_tab2(uint32_t u2, const uint8_t* tab) {
+  const u16x2 u = __builtin_bit_cast(u16x2, u2);
+  const u16x2 sg = u >> (u16x2)15;
+  u16x2 i = __builtin_elementwise_sub_sat(u & (u16x2)0x7fff, (u16x2)(MLT_GELU_TAB_LO - 1));
+  i = __builtin_elementwise_min(i, (u16x2)(MLT_GELU_TAB_NR + 1));
+  i = i * (u16x2)4 + sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2));
+  const uint32_t w = __builtin_bit_cast(uint32_t, i);
+  return f32x2{*reinterpret_cast<const float*>(tab + (w & 0xffffu)), *reinterpret_cast<const float*>(tab + (w >> 16))};
+}
 
 // ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct
 // stores would be 64 x 8 bytes per lane in 32-byte row pieces (store-issue bound). Each wave
@@ -105,13 +146,26 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         }
         *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) =
             make_uint4(a[0], a[1], a[2], a[3]);
-        gelu2<4>(x2);
+        if constexpr (w4_gelu_tab<EK>()) {
+#pragma unroll
+          for (int q2 = 0; q2 < 4; ++q2) x2[q2] = x2[q2] * gelu_tab2(a[q2], smem + kW4Smem);
+        } else {
+          gelu2<4>(x2);
+        }
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) v[2 * q2] = x2[q2].x, v[2 * q2 + 1] = x2[q2].y;
       } else if constexpr (EK == W4_DGELU) {
         const uint4 sv = sd[0][it];
-        f32x2 x2[4] = {unpack_bf16x2(sv.x), unpack_bf16x2(sv.y), unpack_bf16x2(sv.z), unpack_bf16x2(sv.w)};
-        gelu_grad2<4>(x2);
+        f32x2 x2[4];
+        if constexpr (w4_gelu_tab<EK>()) {
+          const uint32_t sw4[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+          for (int q2 = 0; q2 < 4; ++q2) x2[q2] = gelu_tab2(sw4[q2], smem + kW4Smem);
+        } else {
+          x2[0] = unpack_bf16x2(sv.x), x2[1] = unpack_bf16x2(sv.y), x2[2] = unpack_bf16x2(sv.z);
+          x2[3] = unpack_bf16x2(sv.w);
+          gelu_grad2<4>(x2);
+        }
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) {
           const f32x2 gv = f32x2{v[2 * q2], v[2 * q2 + 1]} * x2[q2];
@@ -298,6 +352,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4f8_kernel(const uint8_t* __rest
   const int gm_ = group_m > 0 ? group_m : tiles_m;
   const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);  // split z (see gemm_w4_kernel)
   const int T = tiles_m * tiles_n, G = gridDim.x;
+  w4_load_gelu_tab<EK>(smem);
   if (G >= T) {
     gemm_w4f8_tile<OutT, EK, FA, FB>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 128, lda, ldb, ldc, epi,
                                      xcd_remap(blockIdx.x, G), gm_, tiles_m, tiles_n, smem);
@@ -330,6 +385,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint8_t* __restri
   // split z = blockIdx.y: K-tiles [z * ksteps, min(nk, (z + 1) * ksteps)), output slab z (cstride)
   const int z = blockIdx.y, kt0 = z * ksteps, nkt = min(ksteps, nk - kt0);
   const int T = tiles_m * tiles_n, G = gridDim.x;
+  w4_load_gelu_tab<EK>(smem);
   if (G >= T) {
     gemm_w4_tile<OutT, EK, AN, BN>(A, B, C + (int64_t)z * cstride, nkt, (int64_t)kt0 * 64, lda, ldb, ldc, epi,
                                    xcd_remap(blockIdx.x, G), gm_, tiles_m, tiles_n, smem);
@@ -349,7 +405,7 @@ template <typename OutT, int EK, bool AN, bool BN>
 static void launch_w4_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                          int64_t ldc, const GemmEpi& e, int group_m, int splits, int ksteps, int64_t cstride,
                          hipStream_t st) {
-  constexpr int SMEM = kW4Smem;
+  constexpr int SMEM = w4_smem<EK>();
   auto kern = gemm_w4_kernel<OutT, EK, AN, BN>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -442,7 +498,7 @@ template <typename OutT, int EK, int FA, int FB>
 static void launch_w4f8_ek(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                            int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st, int splits = 1, int ksteps = 0,
                            int64_t cstride = 0) {
-  constexpr int SMEM = kW4Smem;
+  constexpr int SMEM = w4_smem<EK>();
   auto kern = gemm_w4f8_kernel<OutT, EK, FA, FB>;
   static bool attr_set = false;
   if (!attr_set) {

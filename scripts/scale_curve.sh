@@ -31,8 +31,8 @@ for prec in bf16 fp32; do
   done
 done
 if [ "$ngpu" -ge 8 ]; then
-  # N = 8 transport A/B of the bf16 step under both batch semantics: the one-launch xGMI-fused
-  # step (default), the four-launch step with the one-/two-shot vote (MLT_LENET_FUSED_DP=0),
+  # N = 8 transport A/B of the bf16 step under both batch semantics: whatever the bring-up vote
+  # picks (the xGMI-fused two-launch step when it wins), the four-launch step with the one-/two-shot vote (MLT_LENET_FUSED_DP=0),
   # and RCCL forced (MLT_XGMI_AR=0)
   for scaling in weak reference; do
     for variant in fused fourlaunch rccl; do
