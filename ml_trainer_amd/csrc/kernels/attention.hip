@@ -47,8 +47,11 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 
 // Backward softmax-gradient math on score PAIRS (build A/B switch, -DMLT_ATTN_PKF32=1): the
 // scale-and-shift and dS = P * dP' of two adjacent accumulator rows as one v_pk_fma_f32 / one
-// v_pk_mul_f32 instead of two scalar ops each; the exp2 stays scalar. Off by default: see
-// profiles/r5/attn_pkf32_ab.jsonl for the measured A/B.
+// v_pk_mul_f32 instead of two scalar ops each; the exp2 stays scalar. Off by default: measured at
+// B512 (profiles/r5/gemm_gelu_tab_attn_pkf32_ab.jsonl, profiles/pmc/attn_bf16_b512_r5*.jsonl) it
+// cuts VALU instructions 5 % (dK/dV) / 9 % (dQ), VALU per MFMA 4.30 -> 4.07 / 4.89 -> 4.44, but the
+// backward pair is not faster (1.946-1.958 vs 1.937-1.945 ms): dQ -2.7 % busy cycles, dK/dV +1.6 %
+// (packed f32 ops between MFMAs cost more issue than the two scalar ops, MI355X_MICROARCH.md).
 #ifndef MLT_ATTN_PKF32
 #define MLT_ATTN_PKF32 0
 #endif

@@ -38,7 +38,9 @@ constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 
 // GELU / GELU' of the (b)GELU epilogues from exact tables at the bf16 input points (scripts/
 // gen_gelu_table.py: layout, accuracy, why) instead of the A&S erf of mlt_gemm.h; the table sits in
 // LDS behind the epilogue images (158,736 B of the 160 KB). Build switch -DMLT_W4_GELU_TAB=0: the
-// erf polynomial (A/B: profiles/r5/gemm_gelu_tab_ab.jsonl).
+// erf polynomial. Same-box A/B at 256 K tokens (profiles/r5/gemm_gelu_tab_attn_pkf32_ab.jsonl): bias +
+// GELU 832 -> 862-870 TF, dGELU 839-842 -> 914-917, dGELU + column sums 809-812 -> 880-887 (plain
+// epilogue 1,097-1,107); BERT-base 3,038-3,040 -> 3,070-3,074 samples/s.
 #ifndef MLT_W4_GELU_TAB
 #define MLT_W4_GELU_TAB 1
 #endif
