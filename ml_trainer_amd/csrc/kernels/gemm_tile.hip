@@ -33,6 +33,16 @@
 
 namespace mlt {
 
+// exact GELU / GELU' at the bf16 input points for the quantising epilogue (scripts/gen_gelu_table.py;
+// the 4-wave kernel's epilogues use the same tables, gemm_w4.hip). Build switch -DMLT_Q8_GELU_TAB=0:
+// the A&S erf polynomial of mlt_gemm.h. Same-box A/B at the large config's FFN (262 K tokens,
+// profiles/r5/fp8_q8_gelu_tab_ab.jsonl): q8 GELU forward 2.37 -> 2.28 ms, q8 dGELU 2.49-2.50 ->
+// 2.37-2.38 ms; fp8 `large` 1,183-1,184 -> 1,202-1,205 samples/s.
+#include "gelu_table.inc"
+#ifndef MLT_Q8_GELU_TAB
+#define MLT_Q8_GELU_TAB 1
+#endif
+
 template <int V>
 using PIC = std::integral_constant<int, V>;
 
@@ -370,7 +380,7 @@ using IC = std::integral_constant<int, V>;
 // column partial sum of the quadrant (bias gradient), both halves combined by one shuffle.
 template <int FMT>
 __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc, const GemmEpi& epi, float* cs,
-                                            int gm0, int gn0, int N, int lane, float& amx) {
+                                            int gm0, int gn0, int N, int lane, float& amx, const uint8_t* tab) {
   constexpr int EPS = 36;
   const float s = *epi.q_scale;
 #pragma unroll
@@ -400,7 +410,12 @@ __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc
         f32x2 x2[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) x2[q] = unpack_bf16x2(pr[4 * hh + q]);
-        gelu2<4>(x2);
+        if constexpr (MLT_Q8_GELU_TAB) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x2[q] = x2[q] * gelu_tab2(pr[4 * hh + q], tab);
+        } else {
+          gelu2<4>(x2);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[8 * hh + 2 * q] = x2[q].x, v[8 * hh + 2 * q + 1] = x2[q].y;
       }
@@ -411,9 +426,14 @@ __device__ __forceinline__ void q8_quadrant(uint8_t* __restrict__ C, int64_t ldc
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         f32x2 x2[4];
+        if constexpr (MLT_Q8_GELU_TAB) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x2[q] = unpack_bf16x2(w[4 * hh + q]);
-        gelu_grad2<4>(x2);
+          for (int q = 0; q < 4; ++q) x2[q] = gelu_tab2(w[4 * hh + q], tab);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x2[q] = unpack_bf16x2(w[4 * hh + q]);
+          gelu_grad2<4>(x2);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[8 * hh + 2 * q] *= x2[q].x, v[8 * hh + 2 * q + 1] *= x2[q].y;
       }
@@ -495,6 +515,9 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = K / (F8 ? 128 : T_BK);
   const int kt0 = ksplit * ksteps, kt1 = min(nk, kt0 + ksteps);
+  if constexpr (sizeof(OutT) == 1 && MLT_Q8_GELU_TAB) {  // quantising GELU / dGELU epilogue: its table
+    if (epi.mode == 1 || epi.mode == 2) gelu_tab_load(smem + 2 * BUF, epi.mode == 2, T_NT);
+  }
 
   // glds sources of the four half-tiles (0 A0, 1 A1, 2 B0, 3 B1), two 16-B chunks per thread
   // each: 32-bit offsets from the uniform operand bases (the host guarantees < 4 GiB spans)
@@ -724,9 +747,11 @@ __global__ __launch_bounds__(T_NT, 1) void gemm_pp_kernel(const uint8_t* __restr
     if constexpr (sizeof(OutT) == 1) {  // quantising epilogue (interior tiles, no split: host-checked)
       stage_q(qd);
       if (epi.q_fmt == 0)
-        q8_quadrant<0>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx);
+        q8_quadrant<0>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx,
+                       smem + 2 * BUF);
       else
-        q8_quadrant<1>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx);
+        q8_quadrant<1>(reinterpret_cast<uint8_t*>(C), ldc, epi, cs, q_gm0(qd), q_gn0(qd), N, lane, q_amx,
+                       smem + 2 * BUF);
       return;
     } else {
     auto stg = [&]() __attribute__((always_inline)) { stage_q(qd); };
@@ -1003,7 +1028,8 @@ void launch_tile(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C,
 template <bool AM, bool BNL, typename OutT, int F8A, int F8B>
 void launch_pp(const GemmPlan& p, const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda,
                int64_t ldb, int64_t ldc, const GemmEpi& e, float* ws, unsigned* cnt, hipStream_t st) {
-  constexpr int SMEM = 2 * 4 * 16384;  // two K-tiles; the epilogue image (8 x 64 x 36 fp32) fits inside
+  // two K-tiles; the epilogue image (8 x 64 x 36 fp32) fits inside; + the GELU table (quantising epilogue)
+  constexpr int SMEM = 2 * 4 * 16384 + (sizeof(OutT) == 1 && MLT_Q8_GELU_TAB ? kGeluTabBytes : 0);
   auto kern = gemm_pp_kernel<AM, BNL, OutT, F8A, F8B>;
   static bool attr_set = false;
   if (!attr_set) {

@@ -44,7 +44,6 @@ constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 
 #ifndef MLT_W4_GELU_TAB
 #define MLT_W4_GELU_TAB 1
 #endif
-constexpr int kGeluTabBytes = MLT_GELU_TAB_ENTRIES * 4;
 template <int EK>
 constexpr bool w4_gelu_tab() {
   return MLT_W4_GELU_TAB && (EK == W4_GELU || EK == W4_DGELU);
@@ -57,23 +56,7 @@ static_assert(kW4Smem + kGeluTabBytes <= 160 * 1024, "GELU table must fit beside
 // workgroup copy of the epilogue's table into LDS (read only after the epilogue's first barrier)
 template <int EK>
 __device__ __forceinline__ void w4_load_gelu_tab(uint8_t* smem) {
-  if constexpr (w4_gelu_tab<EK>()) {
-    const uint4* src = reinterpret_cast<const uint4*>(EK == W4_GELU ? kGeluPhiTab : kGeluGradTab);
-    uint4* dst = reinterpret_cast<uint4*>(smem + kW4Smem);
-    for (int i = threadIdx.x; i < kGeluTabBytes / 16; i += 256) dst[i] = src[i];
-  }
-}
-// table multipliers of a bf16 pair (element 0 in the low half): index = min(sat(|bits| - (LO - 1)),
-// NR + 1) + sign (NR + 2), both halves at once in 16-bit packed integer ops, then one LDS read each
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 gelu_tab2(uint32_t u2, const uint8_t* tab) {
-  const u16x2 u = __builtin_bit_cast(u16x2, u2);
-  const u16x2 sg = u >> (u16x2)15;
-  u16x2 i = __builtin_elementwise_sub_sat(u & (u16x2)0x7fff, (u16x2)(MLT_GELU_TAB_LO - 1));
-  i = __builtin_elementwise_min(i, (u16x2)(MLT_GELU_TAB_NR + 1));
-  i = i * (u16x2)4 + sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2));
-  const uint32_t w = __builtin_bit_cast(uint32_t, i);
-  return f32x2{*reinterpret_cast<const float*>(tab + (w & 0xffffu)), *reinterpret_cast<const float*>(tab + (w >> 16))};
+  if constexpr (w4_gelu_tab<EK>()) gelu_tab_load(smem + kW4Smem, EK == W4_DGELU, 256);
 }
 
 // ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct

@@ -76,8 +76,9 @@ def test_table_gelu_matches_erf_at_every_bf16_point():
 
 
 def test_kernel_uses_the_generated_layout():
-    src = open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", "gemm_w4.hip")).read()
-    assert '#include "gelu_table.inc"' in src
+    for f in ("gemm_w4.hip", "gemm_tile.hip"):
+        assert '#include "gelu_table.inc"' in open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", f)).read()
+    src = open(INC).read()
     assert "__builtin_elementwise_sub_sat(u & (u16x2)0x7fff, (u16x2)(MLT_GELU_TAB_LO - 1))" in src
     assert "__builtin_elementwise_min(i, (u16x2)(MLT_GELU_TAB_NR + 1))" in src
     assert "sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2))" in src
