@@ -54,7 +54,8 @@ def _torch_paths():
 
 def _headers():
     # (+ generated kernel fragments included by the .hip files, e.g. gemm_w4_loop.inc)
-    return glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.inc"))
+    return (glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.inc")) +
+            glob.glob(os.path.join(CSRC, "kernels", "*.inc")))
 
 
 def _newer(src: str, obj: str, deps, cmd=None) -> bool:

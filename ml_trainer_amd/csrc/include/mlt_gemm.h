@@ -31,36 +31,16 @@ struct GemmEpi {
   int q_fmt = 0;                   // 0 e4m3, 1 e5m2
 };
 
-// GELU and its derivative (erf by Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, far below the
-// bf16 output's ulp: one v_rcp and one v_exp instead of the library erff). These scalar forms are
-// the two-wide forms below operation for operation (v_pk_fma_f32 / v_pk_mul_f32 round each lane
-// exactly as v_fma_f32 / v_mul_f32), so every epilogue -- packed or not, in-kernel or split-K
-// reduce -- produces the same bits. q = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2).
-__device__ __forceinline__ float phi_tail(float x, float& ax, float& e) {
-  ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(ax, 0.3275911f * 0.70710678118654752f, 1.f));
-  float h = fmaf(t, 0.5f * 1.061405429f, 0.5f * -1.453152027f);
-  h = fmaf(t, h, 0.5f * 1.421413741f);
-  h = fmaf(t, h, 0.5f * -0.284496736f);
-  h = fmaf(t, h, 0.5f * 0.254829592f);
-  e = __builtin_amdgcn_exp2f((x * (-0.5f * 1.4426950408889634f)) * x);
-  return (t * h) * e;
-}
-__device__ __forceinline__ float gelu_f(float x) {
-  float ax, e;
-  const float q = phi_tail(x, ax, e);
-  return fmaf(-ax, q, (x + ax) * 0.5f);
-}
-__device__ __forceinline__ float gelu_grad(float x) {
-  float ax, e;
-  const float q = phi_tail(x, ax, e);
-  return fmaf(x * 0.3989422804014327f, e, 0.5f + copysignf(0.5f - q, x));
-}
-
-// Two-wide forms for the VALU-bound GEMM epilogues (gemm_w4.hip): the same A&S 7.1.26 erf,
-// written on float2 so every non-transcendental step is one v_pk_fma_f32 / v_pk_mul_f32 for two
-// elements (the scalar forms above compile to ~19 single-element VALU ops + 2 transcendentals
-// per element; these to ~11 + 2). q = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2) = 0.5 poly(t) e^{-x^2/2}
+// GELU and its derivative. Every epilogue evaluates them at bf16 points (the GELU input is the
+// bf16-rounded pre-activation it also saves; the dGELU epilogue reads that bf16 tensor back), so
+// they come from exact tables indexed by the bf16 bits (mlt_gelu_table.inc, scripts/gen_gelu_table.py):
+// gelu_f / gelu_grad / gelu_pair_g from global memory, gelu_tab2 from an LDS copy (4-wave and
+// quantising epilogues) -- one multiply by the same entry, so every path produces the same bits.
+//
+// The two-wide A&S 7.1.26 erf below is the build-switch alternative of the 4-wave and quantising
+// epilogues (-DMLT_W4_GELU_TAB=0 / -DMLT_Q8_GELU_TAB=0, kept for their A/Bs): every
+// non-transcendental step one v_pk_fma_f32 / v_pk_mul_f32 for two elements (~11 + 2
+// transcendentals per element). q = Phi(-|x|) = 0.5 erfc(|x| / sqrt 2) = 0.5 poly(t) e^{-x^2/2}
 // (the 0.5 and 1/sqrt 2 folded into the constants), then
 //   gelu(x)  = x Phi(x) = relu(x) - |x| q
 //   gelu'(x) = Phi(x) + x phi(x),  Phi(x) = 0.5 + copysign(0.5 - q, x),  phi(x) = e^{-x^2/2} / sqrt(2 pi)
@@ -74,6 +54,7 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(f32x2 v) {
 __device__ __forceinline__ f32x2 unpack_bf16x2(uint32_t u) {
   return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
+#include "mlt_gelu_table.inc"
 // q = Phi(-|x|) of N pairs, step by step across the pairs (N independent chains in source order:
 // a dependent packed op right behind its producer costs an s_nop on gfx950); also |x| and
 // e^{-x^2/2}
@@ -350,8 +331,7 @@ __device__ __forceinline__ void epi_store8_loop(uint16_t* __restrict__ C, int64_
     if constexpr (MODE == 1) {
       const uint4 pre = pack_bf16x8(v);
       *reinterpret_cast<uint4*>(const_cast<uint16_t*>(epi.aux) + (int64_t)gm * epi.ldaux + gn) = pre;
-      f32x2 x2[4] = {unpack_bf16x2(pre.x), unpack_bf16x2(pre.y), unpack_bf16x2(pre.z), unpack_bf16x2(pre.w)};
-      gelu2<4>(x2);
+      const f32x2 x2[4] = {gelu_pair_g(pre.x), gelu_pair_g(pre.y), gelu_pair_g(pre.z), gelu_pair_g(pre.w)};
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[2 * q] = x2[q].x, v[2 * q + 1] = x2[q].y;
     } else if constexpr (MODE == 3) {

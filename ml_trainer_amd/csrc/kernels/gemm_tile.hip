@@ -38,7 +38,6 @@ namespace mlt {
 // the A&S erf polynomial of mlt_gemm.h. Same-box A/B at the large config's FFN (262 K tokens,
 // profiles/r5/fp8_q8_gelu_tab_ab.jsonl): q8 GELU forward 2.37 -> 2.28 ms, q8 dGELU 2.49-2.50 ->
 // 2.37-2.38 ms; fp8 `large` 1,183-1,184 -> 1,202-1,205 samples/s.
-#include "gelu_table.inc"
 #ifndef MLT_Q8_GELU_TAB
 #define MLT_Q8_GELU_TAB 1
 #endif

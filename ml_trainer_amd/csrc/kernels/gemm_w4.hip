@@ -26,7 +26,6 @@
 
 namespace mlt {
 
-#include "gelu_table.inc"
 
 enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
 

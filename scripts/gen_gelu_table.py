@@ -1,5 +1,7 @@
 """Generate the exact GELU / GELU' lookup tables of the 4-wave GEMM's epilogues
-(csrc/kernels/gelu_table.inc).
+(csrc/include/mlt_gelu_table.inc, included by mlt_gemm.h: EVERY GELU / GELU' GEMM epilogue -- the
+4-wave kernel's and the quantising epilogue's from an LDS copy, the scalar / split-K / general paths
+from global memory -- multiplies by the same table entry, so they all produce the same bits).
 
 Why a table: the GELU epilogue's input is the bf16-ROUNDED pre-activation (the value it also saves
 for the backward), and the dGELU epilogue reads that same bf16 tensor, so the function is only ever
@@ -18,15 +20,14 @@ Layout (one table per function, 5,892 f32 = 23,568 B, copied to LDS once per wor
 The device index is min(sat_sub(bits & 0x7fff, LO - 1), NR + 1) + s (NR + 2), on both halves of a
 bf16 pair at once (v_pk_sub_u16 clamp / v_pk_min_u16 / v_pk_mad_u16).
 
-Usage: python scripts/gen_gelu_table.py  (rewrites the .inc: tables + the device lookup; gemm_w4.hip
-and gemm_tile.hip include it inside namespace mlt)
+Usage: python scripts/gen_gelu_table.py  (rewrites the .inc: tables + the device lookups)
 """
 import math
 import os
 import struct
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-OUT = os.path.join(HERE, "..", "ml_trainer_amd", "csrc", "kernels", "gelu_table.inc")
+OUT = os.path.join(HERE, "..", "ml_trainer_amd", "csrc", "include", "mlt_gelu_table.inc")
 
 E_LO, E_HI = 107, 130            # bf16 biased exponents covered: [2^-20, 2^3)
 LO = E_LO << 7                   # first covered magnitude bit pattern
@@ -81,6 +82,26 @@ __device__ __forceinline__ f32x2 gelu_tab2(uint32_t u2, const uint8_t* tab) {
   i = i * (u16x2)4 + sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2));
   const uint32_t w = __builtin_bit_cast(uint32_t, i);
   return f32x2{*reinterpret_cast<const float*>(tab + (w & 0xffffu)), *reinterpret_cast<const float*>(tab + (w >> 16))};
+}
+// the same index for one bf16 (bits b), and the scalar / two-wide lookups from global memory (the
+// general, persistent and split-K-reduce epilogues: L1/L2-resident table, no LDS copy)
+__device__ __forceinline__ uint32_t gelu_tab_index(uint32_t b) {
+  const uint32_t m = b & 0x7fffu;
+  const uint32_t i = m > MLT_GELU_TAB_LO - 1 ? min(m - (MLT_GELU_TAB_LO - 1), (uint32_t)MLT_GELU_TAB_NR + 1) : 0u;
+  return i + (b >> 15) * (MLT_GELU_TAB_NR + 2);
+}
+// GELU(x) and GELU'(x) of a bf16 value x (the low 16 bits of its f32 pattern are zero)
+__device__ __forceinline__ float gelu_f(float x) {
+  return x * __uint_as_float(kGeluPhiTab[gelu_tab_index(__float_as_uint(x) >> 16)]);
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  return __uint_as_float(kGeluGradTab[gelu_tab_index(__float_as_uint(x) >> 16)]);
+}
+// GELU of a packed bf16 pair (element 0 in the low half), from global memory
+__device__ __forceinline__ f32x2 gelu_pair_g(uint32_t u2) {
+  const f32x2 x = unpack_bf16x2(u2);
+  return x * f32x2{__uint_as_float(kGeluPhiTab[gelu_tab_index(u2 & 0xffffu)]),
+                   __uint_as_float(kGeluPhiTab[gelu_tab_index(u2 >> 16)])};
 }"""
 
 

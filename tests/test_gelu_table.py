@@ -1,7 +1,8 @@
-"""CPU checks of the 4-wave GEMM's table GELU epilogues (csrc/kernels/gelu_table.inc, gemm_w4.hip
-gelu_tab2): the committed include is exactly the generator's output, and the device index sequence
-(16-bit packed saturating subtract / min / sign offset), replayed in numpy over EVERY bf16 bit
-pattern, gives GELU and GELU' within 1e-6 absolute of the float64 erf forms."""
+"""CPU checks of the GEMM epilogues' table GELU (csrc/include/mlt_gelu_table.inc: gelu_tab2 from LDS in
+the 4-wave / quantising epilogues, gelu_f / gelu_grad / gelu_pair_g from global memory elsewhere):
+the committed include is exactly the generator's output, and the device index sequence (16-bit
+packed saturating subtract / min / sign offset), replayed in numpy over EVERY bf16 bit pattern,
+gives GELU and GELU' within 1e-6 absolute of the float64 erf forms."""
 import importlib.util
 import math
 import os
@@ -11,7 +12,7 @@ import numpy as np
 from scipy.special import erfc
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-INC = os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", "gelu_table.inc")
+INC = os.path.join(ROOT, "ml_trainer_amd", "csrc", "include", "mlt_gelu_table.inc")
 
 
 def _gen():
@@ -75,10 +76,17 @@ def test_table_gelu_matches_erf_at_every_bf16_point():
     assert gelu[x == 12.0][0] == 12.0 and gelu[x == -12.0][0] == 0.0
 
 
-def test_kernel_uses_the_generated_layout():
-    for f in ("gemm_w4.hip", "gemm_tile.hip"):
-        assert '#include "gelu_table.inc"' in open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", f)).read()
-    src = open(INC).read()
-    assert "__builtin_elementwise_sub_sat(u & (u16x2)0x7fff, (u16x2)(MLT_GELU_TAB_LO - 1))" in src
-    assert "__builtin_elementwise_min(i, (u16x2)(MLT_GELU_TAB_NR + 1))" in src
-    assert "sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2))" in src
+def test_kernels_use_the_generated_layout():
+    inc = open(INC).read()
+    # the packed (LDS) index and the scalar (global) index are the same function of the bits
+    assert "__builtin_elementwise_sub_sat(u & (u16x2)0x7fff, (u16x2)(MLT_GELU_TAB_LO - 1))" in inc
+    assert "__builtin_elementwise_min(i, (u16x2)(MLT_GELU_TAB_NR + 1))" in inc
+    assert "sg * (u16x2)(4 * (MLT_GELU_TAB_NR + 2))" in inc
+    assert "m > MLT_GELU_TAB_LO - 1 ? min(m - (MLT_GELU_TAB_LO - 1), (uint32_t)MLT_GELU_TAB_NR + 1) : 0u" in inc
+    assert "i + (b >> 15) * (MLT_GELU_TAB_NR + 2)" in inc
+    hdr = open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "include", "mlt_gemm.h")).read()
+    assert '#include "mlt_gelu_table.inc"' in hdr
+    w4 = open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", "gemm_w4.hip")).read()
+    pp = open(os.path.join(ROOT, "ml_trainer_amd", "csrc", "kernels", "gemm_tile.hip")).read()
+    assert "gelu_tab2(a[q2], smem + kW4Smem)" in w4 and "gelu_tab2(sw4[q2], smem + kW4Smem)" in w4
+    assert "gelu_tab2(pr[4 * hh + q], tab)" in pp and "gelu_tab2(w[4 * hh + q], tab)" in pp

@@ -1,4 +1,6 @@
 """bf16 MFMA GEMM (csrc/kernels/gemm.hip) vs a plain torch fp32 reference of the same op."""
+import math
+
 import pytest
 import torch
 
@@ -404,3 +406,44 @@ def test_w4_wgrad_accumulate_plan(dev):
     acc2 = torch.full((M2, N2), 1.5, device=dev)
     C.gemm(A2, B2, acc2, True, True, accumulate=True)
     torch.testing.assert_close(acc2, A2.float().t() @ B2.float() + 1.5, rtol=1e-4, atol=4e-3)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gelu_epilogues_same_bits_on_every_kernel(dev, mode):
+    """Every GEMM kernel's GELU (mode 1) / dGELU (mode 2) epilogue multiplies by the same exact table
+    entry (csrc/include/mlt_gelu_table.inc; LDS copy in the 4-wave kernel, global memory elsewhere):
+    with operands whose products and sums are exact in fp32 (so every kernel reaches the same
+    pre-activation whatever its accumulation order), the 4-wave, ping-pong, tile, persistent and
+    general kernels and the split-K reduce all write identical bits, which also match torch's erf
+    GELU within bf16 rounding."""
+    C = require_native()
+    M, N, K = 4096, 2304, 256
+    g = torch.Generator().manual_seed(5 + mode)
+    # entries in {-1, 0, 1} / 4: every partial sum is a multiple of 1/16 below 16 -> exact in fp32
+    A = (torch.randint(-1, 2, (M, K), generator=g).float() / 4).to(torch.bfloat16).to(dev)
+    B = (torch.randint(-1, 2, (N, K), generator=g).float() / 4).to(torch.bfloat16).to(dev)
+    bias = (torch.randn(N, generator=g) * 2).to(dev)
+    pre = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16).to(dev)
+    outs = {}
+    for cfg, splits in ((7, 0), (5, 0), (1, 0), (6, 0), (0, 0), (1, 2)):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        if mode == 1:
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            C.gemm(A, B, out, False, False, bias=bias, aux=aux, mode=1, cfg=cfg, splits=splits)
+            outs[(cfg, splits)] = (out, aux)
+        else:
+            C.gemm(A, B, out, False, False, aux=pre, mode=2, cfg=cfg, splits=splits)
+            outs[(cfg, splits)] = (out, pre)
+    ref_out, ref_aux = outs[(7, 0)]
+    for key, (out, aux) in outs.items():
+        assert torch.equal(aux, ref_aux), key
+        assert torch.equal(out, ref_out), key
+    x = ref_aux.float()
+    acc = A.float() @ B.float().t()
+    if mode == 1:
+        torch.testing.assert_close(x, acc + bias, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(ref_out.float(), torch.nn.functional.gelu(x.double()).float(), rtol=8e-3, atol=1e-6)
+    else:
+        xd = x.double()
+        dg = 0.5 * torch.erfc(-xd / math.sqrt(2.0)) + xd * torch.exp(-0.5 * xd * xd) / math.sqrt(2.0 * math.pi)
+        torch.testing.assert_close(ref_out.float(), (acc.double() * dg).float(), rtol=8e-3, atol=1e-6)
