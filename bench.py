@@ -31,10 +31,7 @@ Usage:  python bench.py --gpus N --steps K --warmup W
 Timing: every hipGraph the K timed steps replay is captured and uploaded before the timed
 region (a capture counter is checked after it); wall time between barrier+synchronize pairs is
 reported. The LeNet timed region holds no hipEvent (two timing-event records cost ~30 us of wall
-time per region here); per-kernel device time comes from rocprofv3 (profiles/). The bf16 LeNet
-timed region replays graphs of the largest d <= 64 dividing K steps, and the W warmup steps replay
-those same graphs (the last one through a device step limit that lets exactly the remaining
-warmup steps run: LeNetStepEngine.replay_limited), so the timed replays are warm and few.
+time per region here); per-kernel device time comes from rocprofv3 (profiles/).
 
 BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgrad GEMMs with
 delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
@@ -359,71 +356,50 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     targets = torch.randint(0, 10, (N,), dtype=torch.int64, device=dev, generator=g)
     engine.set_dataset(data, targets, batch_size=per_gpu, augment=True)
     # graphs of up to 64 steps: one replay covers a short timed run, long runs amortise launches
-    # (each graph boundary leaves the device idle ~5-9 us: profiles/r5/lenet_graph_boundary.jsonl).
-    # bf16 two-launch step: the timed graph holds the largest d <= 64 dividing K steps, and the warmup
-    # replays that SAME graph -- its last replay through a device step limit that lets only the
-    # remaining warmup steps run (engine.replay_limited: the other launches exit at entry) -- so the
-    # timed region never pays a graph's cold first replay (~2 us/step of device time) and replays
-    # as few graphs as possible. Otherwise (fp32, one-launch, --steps-per-graph): the largest d <= 64
-    # dividing both K and W, so that the warmup replays the very graph the timed steps replay
+    # steps per graph: the largest d <= 64 dividing both K and W, so that the warmup replays the very
+    # graph the timed steps replay (a freshly uploaded graph's first replay costs ~40 us more, measured
+    # by scripts/debug/replay_cold.py); min(64, K) when they share no useful divisor
     spg = args.steps_per_graph
-    use_graph = not args.no_graph
-    primed = (use_graph and not spg and precision == "bf16" and not engine.eng.onelaunch
-              and (engine.fused or engine.in_graph_collective))
     if not spg:
-        if primed:
-            spg = max(d for d in range(1, 65) if args.steps % d == 0)
-        else:
-            common = [d for d in range(1, 65) if args.steps % d == 0 and args.warmup > 0 and args.warmup % d == 0]
-            spg = max(common) if common and max(common) >= 4 else max(1, min(64, args.steps))
+        common = [d for d in range(1, 65) if args.steps % d == 0 and args.warmup > 0 and args.warmup % d == 0]
+        spg = max(common) if common and max(common) >= 4 else max(1, min(64, args.steps))
+    use_graph = not args.no_graph
 
     state = {"epoch": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}
 
-    def execute(events, warm: bool = False) -> int:
-        """Run planned engine calls; return samples processed on this rank. warm: full-batch step
-        runs replay the timed graph (the remainder through replay_limited)."""
+    def run(nsteps: int) -> int:
+        """Run nsteps training steps; return samples processed on this rank."""
         samples = 0
-        for ev in events:
+        for ev in lenet_plan(nsteps, state, N, world, rank, per_gpu, spg, shard_indices):
             if ev[0] == "epoch":
                 engine.start_epoch(torch.as_tensor(ev[1], dtype=torch.int32))
-                continue
-            _, b, k, per_graph = ev
-            if warm and primed and b == per_gpu:
-                full, rem = divmod(k, spg)
-                if full:
-                    engine.train_steps(b, full * spg, use_graph=True, steps_per_graph=spg, flush=False)
-                if rem:
-                    engine.replay_limited(b, spg, rem)
             else:
+                _, b, k, per_graph = ev
                 # flush=False: a one-launch step's update runs at the head of the next step's launch
                 # (steady-state pipelining: K launches carry K steps and K updates); the last one
                 # is flushed after the timed region
                 engine.train_steps(b, k, use_graph=use_graph, steps_per_graph=per_graph, flush=False)
-            samples += b * k
+                samples += b * k
         return samples
 
     # capture + upload every hipGraph the warmup AND the timed steps replay before any step runs
     # (no step runs here), so the timed region holds exactly K steps of replays and nothing else,
     # and the warmup replays end right before t0 (no capture gap lets the GPU idle down in between)
-    plan_w = list(lenet_plan(args.warmup, state, N, world, rank, per_gpu, spg, shard_indices))
-    plan_t = list(lenet_plan(args.steps, dict(state), N, world, rank, per_gpu, spg, shard_indices))
-    precapture(engine, plan_t, use_graph)
-    if not primed:
-        precapture(engine, plan_w, use_graph)
-    else:  # the warmup's partial-batch (epoch end) calls, if any, replay graphs of their own
-        precapture(engine, [ev for ev in plan_w if ev[0] == "steps" and ev[1] != per_gpu], use_graph)
+    st_w = dict(state)
+    plan_w = list(lenet_plan(args.warmup, st_w, N, world, rank, per_gpu, spg, shard_indices))
+    precapture(engine, plan_w, use_graph)
+    precapture(engine, lenet_plan(args.steps, dict(st_w), N, world, rank, per_gpu, spg, shard_indices), use_graph)
     # no hipEvent inside the timed region: two timing-event records cost ~30 us of wall time per
     # region on this stack (21.1-21.9 vs 19.6-19.7 us/step at K=20,
     # profiles/r4/lenet_timed_region_events_ab.jsonl); per-kernel device times come from rocprofv3
-    execute(plan_w, warm=True)
-    plan_t = list(lenet_plan(args.steps, state, N, world, rank, per_gpu, spg, shard_indices))  # (same calls)
+    run(args.warmup)
     captures_before = engine.captures
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    samples = execute(plan_t)
+    samples = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -481,8 +457,6 @@ def bench_lenet(args, world, rank, dev, backend, precision):
                    "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
                    "hipgraph_steps": 0 if args.no_graph else spg,
-                   "warmup_replays": ("the timed graph (its last replay limited on the device to the remaining "
-                                      "warmup steps)" if primed else "graphs of the largest common divisor of K and W"),
                    "kernels_per_step": round(nodes / spg, 2) if nodes else None,
                    "update": ("pipelined: step k's batch reductions / exchange / optimizer update run in "
                               "step k+1's launch beside its sample blocks' input phase"

@@ -999,8 +999,7 @@ class LeNetEngine {
       P_.stage2 = get("stage2", at::kByte, B * 3072).data_ptr<uint8_t>();
       P_.meta2 = get("meta2", at::kLong, B * 4).data_ptr<int64_t>();
       P_.metaN = get("metaN", at::kLong, B * 4).data_ptr<int64_t>();
-      // [step, step in epoch, lr bits, pending one-launch batch, step-limit skip marker, pad x3]
-      P_.stepinfo = get("stepinfo", at::kLong, 8).data_ptr<int64_t>();
+      P_.stepinfo = get("stepinfo", at::kLong, 4).data_ptr<int64_t>();
       Tensor sh = bufs["shadow"].cast<Tensor>();
       check_dev(sh, "shadow", at::kShort, 1);
       keep_.push_back(sh);
@@ -1028,7 +1027,6 @@ class LeNetEngine {
     flush();
     A_ = make_aug(data, perm, ctrl, seed, pad, flip, batch_stride, mean, stdv);
     TORCH_CHECK(A_.ctrl != nullptr, "ctrl required");
-    TORCH_CHECK(ctrl.numel() >= 4, "ctrl: [step, step in epoch, step limit, pad] (4 x int64)");
     check_dev(dtargets, "dtargets", at::kLong, A_.n);
     P_.dtargets = dtargets.data_ptr<int64_t>();
     aug_keep_ = {data, perm, ctrl, dtargets};
@@ -1044,9 +1042,7 @@ class LeNetEngine {
 
   void set_ctrl(Tensor ctrl) {
     flush();
-    // [global step, step in epoch, step limit (the bf16 per-sample kernel runs only steps below it;
-    // INT64_MAX = none), pad]
-    check_dev(ctrl, "ctrl", at::kLong, 4, 8);
+    check_dev(ctrl, "ctrl", at::kLong, 2, 8);
     A_.ctrl = ctrl.data_ptr<int64_t>();
     ctrl_keep_ = ctrl;
     graphs_.clear();

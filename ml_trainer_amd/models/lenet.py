@@ -113,12 +113,11 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         "cestat": torch.zeros(B * 2, dtype=torch.float64, device=device),
         # bf16 MFMA engine (lenet_mfma.hip): raw next-step images staged by the per-sample kernel,
         # tagged (global step, perm position, dataset row, target); metaN = the perm lookup one step
-        # further; stepinfo = (step, step in epoch, lr bits, pending one-launch batch, step-limit skip
-        # marker) handed to the wgrad kernel
+        # further; stepinfo = (step, step in epoch, lr bits) handed to the wgrad kernel
         "stage2": torch.zeros(B * 3072, dtype=torch.uint8, device=device),
         "meta2": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
         "metaN": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
-        "stepinfo": torch.zeros(8, dtype=torch.int64, device=device),
+        "stepinfo": torch.zeros(4, dtype=torch.int64, device=device),
         # bf16 engine: the next step's augmented inputs, prepared by the batch-reduction kernel's
         # prep blocks (bf16 pixels, 8 KB per sample) and their (step, position, target) tags
         "prep": torch.zeros(B * 8192, dtype=torch.uint8, device=device),

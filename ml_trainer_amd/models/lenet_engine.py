@@ -61,8 +61,6 @@ def fused_dp_forced() -> bool:
     return os.environ.get("MLT_LENET_FUSED_DP", "1") == "2"
 
 
-_NO_LIMIT = (1 << 63) - 1  # ctrl[2]: no device step limit
-
 class TransportError(RuntimeError):
     """The data-parallel gradient collective failed (peer timeout / RCCL async error)."""
 
@@ -100,8 +98,7 @@ class LeNetStepEngine:
         bufs["wimg"] = torch.zeros(C.lenet_mfma_wimg_elems(), dtype=torch.int16, device=self.device)
         self.bufs = bufs
         self.stats = bufs["stats"]
-        # [global step, step in epoch, step limit (replay_limited), pad]
-        self.ctrl = torch.tensor([0, 0, _NO_LIMIT, 0], dtype=torch.int64, device=self.device)
+        self.ctrl = torch.zeros(2, dtype=torch.int64, device=self.device)
         self.eng = C.LeNetEngine(model.cfg_id, self.max_batch, bufs)
         self.eng.set_ctrl(self.ctrl)
         self.precision = precision
@@ -458,27 +455,6 @@ class LeNetStepEngine:
         if sig != getattr(self, "_host_sig", None):
             self.eng.invalidate_shadow()
             self._host_sig = sig
-
-    def replay_limited(self, B: int, k: int, n: int) -> None:
-        """Run the first ``n`` steps of the captured ``k``-step training graph (n <= k), through
-        that very graph: a device step limit (ctrl[2] = step + n, set on the stream) makes the
-        launches of its last k - n steps exit at entry, then the limit is lifted. A warmup of
-        fewer steps than a timed region's graph holds thereby replays -- and warms -- the graph the
-        timed region replays (a graph's first replay runs ~2 us/step slower on the device,
-        scripts/debug/replay_cold.py), without running more than n training steps. bf16 engine,
-        two-launch step only."""
-        if not (0 < n <= k):
-            raise ValueError(f"replay_limited: need 0 < n <= k, got n={n}, k={k}")
-        if self.precision != "bf16" or not (self.fused or self.in_graph_collective) or self.eng.onelaunch:
-            raise RuntimeError("replay_limited: bf16 engine, graph-replayed step without the one-launch form")
-        mode = self._train_mode()
-        self._note_host_writes()
-        self._ensure_graph(mode, B, k)
-        torch.add(self.ctrl[0:1], n, out=self.ctrl[2:3])
-        self.eng.replay(mode, B, k)
-        self._poll_transport()
-        self.ctrl[2:3].fill_(_NO_LIMIT)
-        self.bufs["stepinfo"][4:5].zero_()
 
     def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8,
                     flush: bool = True) -> None:

@@ -1,3 +1,4 @@
+# (the device step limit / limited-replay build this A/B measured was reverted: see profiles/README.md)
 # Device step limit (ctrl[2]) + warmup through the timed graph (bench: limited replay): LeNet GPU
 # tests on the new build (bitwise limited-replay test included), then a same-box A/B:
 #   new/old .so with --steps-per-graph 5 (the previous flow: kernel-side cost of the limit checks)

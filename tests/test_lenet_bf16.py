@@ -146,7 +146,7 @@ def test_bf16_graph_equals_eager_bitwise(dev):
         runs.append((flat.data.clone(), eng.stats.clone(), eng.ctrl.clone()))
     assert torch.equal(runs[0][0], runs[1][0])
     assert torch.equal(runs[0][1], runs[1][1])
-    assert runs[1][2][:2].tolist() == [8, 8]
+    assert runs[1][2].tolist() == [8, 8]
 
 
 @pytest.mark.gpu
@@ -448,45 +448,3 @@ def test_bf16_onelaunch_dp_loopback_matches_two_launch(dev, B):
     _, two = _train_run(False, "adamw", B, 0, 3, N=128, dp=True)
     for a, b in zip(one, two):
         assert torch.equal(a, b)
-
-
-def _limited_run(opt, B, seq, seed=13, N=600, dp=False):
-    """Train on the toy set through `seq`: ("n", k, spg) = train_steps(B, k, spg), ("lim", k, n) =
-    replay_limited(B, k, n). Returns the state (params, grads, stats, ctrl[:2], prep tags)."""
-    from ml_trainer_amd.parallel.comm import create_xgmi_loopback
-    dev = torch.device("cuda", 0)
-    data, targets = _toy_data(N, 5)
-    m = _mk("default", seed).to(dev)
-    eng, flat = _engine(m, opt, max_batch=max(B, 8), lr=1e-3)
-    if dp:
-        eng.use_transport(xgmi=create_xgmi_loopback(flat.numel, dev))
-    eng.set_dataset(data, targets, batch_size=B)
-    eng.start_epoch(torch.randperm(N, generator=torch.Generator().manual_seed(0)))
-    for kind, a, b in seq:
-        if kind == "n":
-            eng.train_steps(B, a, use_graph=True, steps_per_graph=b)
-        else:
-            eng.replay_limited(B, a, b)
-    torch.cuda.synchronize()
-    return eng, (flat.data.clone(), flat.grad.clone(), eng.stats.clone(), eng.ctrl[:2].clone())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt", ["sgd", "adamw"])
-@pytest.mark.parametrize("dp", [False, True])
-def test_bf16_replay_limited_runs_exactly_n_steps(dev, opt, dp):
-    """replay_limited(B, k, n) runs the first n steps of the k-step graph and nothing else (the
-    launches past the device step limit exit at entry, the batch-reduction kernel skips its
-    update, stats, counter advance and next-step prep): 5 limited + 20 full steps through ONE
-    20-step graph are bitwise the 25 steps of 5-step graphs, and the limit is lifted afterwards."""
-    B = 32
-    eng_a, ref = _limited_run(opt, B, [("n", 25, 5)], dp=dp)
-    eng_b, got = _limited_run(opt, B, [("lim", 20, 5), ("n", 20, 20)], dp=dp)
-    for r, g in zip(ref, got):
-        assert torch.equal(r, g)
-    assert int(eng_b.ctrl[2].item()) == (1 << 63) - 1 and int(eng_b.bufs["stepinfo"][4].item()) == 0
-    # a limited replay with n = k is a plain replay; n = 1 after it continues the same sequence
-    _, ref2 = _limited_run(opt, B, [("n", 21, 1)], dp=dp)
-    _, got2 = _limited_run(opt, B, [("lim", 20, 20), ("lim", 20, 1)], dp=dp)
-    for r, g in zip(ref2, got2):
-        assert torch.equal(r, g)
