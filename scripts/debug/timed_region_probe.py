@@ -40,18 +40,25 @@ class Stub:
         return getattr(self.inner, k)
 
 
-rows = []
-for rep in range(12):
-    torch.cuda.synchronize()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.train_steps(32, K, use_graph=True, steps_per_graph=K, flush=False)
-    t1 = time.perf_counter()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    rows.append(((t1 - t0) * 1e6, (t2 - t1) * 1e6, (t3 - t2) * 1e6, (t3 - t0) * 1e6))
+eng.prepare(32, K, use_graph=True, steps_per_graph=5)
+eng.train_steps(32, K, use_graph=True, steps_per_graph=5, flush=False)
+for spg in (5, 20):
+    rows = []
+    for rep in range(12):
+        torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.train_steps(32, K, use_graph=True, steps_per_graph=spg, flush=False)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        rows.append(((t1 - t0) * 1e6, (t2 - t1) * 1e6, (t3 - t2) * 1e6, (t3 - t0) * 1e6))
+    rows.sort(key=lambda r: r[3])
+    med = rows[len(rows) // 2]
+    print(f"K={K} spg={spg}: launch calls {med[0]:.1f} us, first sync {med[1]:.1f} us, second sync {med[2]:.1f} us, "
+          f"region {med[3]:.1f} us = {med[3] / K:.2f} us/step")
 real = eng.eng
 eng.eng = Stub(real)
 py = []
@@ -66,10 +73,6 @@ for rep in range(50):
     t0 = time.perf_counter()
     torch.cuda.synchronize()
     idle.append((time.perf_counter() - t0) * 1e6)
-rows.sort(key=lambda r: r[3])
-med = rows[len(rows) // 2]
-print(f"K={K}: launch call {med[0]:.1f} us, first sync {med[1]:.1f} us, second sync {med[2]:.1f} us, region {med[3]:.1f} us "
-      f"= {med[3] / K:.2f} us/step")
 py.sort()
 idle.sort()
 print(f"python path with replay stubbed: median {py[len(py) // 2]:.2f} us; idle synchronize median {idle[len(idle) // 2]:.2f} us")
