@@ -438,6 +438,7 @@ def bench_lenet(args, world, rank, dev, backend, precision):
         comm = {"buckets": 1, "bucket_mb": [round(flat.numel * 4 / 2 ** 20, 3)], "comm_dtype": "float32",
                 "in_graph": engine.in_graph_collective, "overlap_pct": 0.0,
                 "fused_into_reduction_kernel": engine.dp_transport == "xgmi-fused",
+                "fused_two_phase": bool(getattr(engine, "fused_two", False)),
                 "allreduce_ms": round(tt[key], 4) if (tt and key in tt) else None}
     out = {
         "metric": "samples/sec/node",

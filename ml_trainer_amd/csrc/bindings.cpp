@@ -883,6 +883,8 @@ class PyXgmi {
   int algo() const { return x_.algo(); }
   void set_fault(int f) { x_.set_fault(f); }
   int fault() const { return x_.fault(); }
+  void set_fused_two(bool t) { x_.set_fused_two(t); }
+  bool fused_two() const { return x_.fused_two(); }
   XgmiAllReduce& raw() { return x_; }
 
  private:
@@ -1446,7 +1448,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("world", [](PyXgmi& x) { return x.raw().world(); })
       .def_property("timeout_ms", &PyXgmi::timeout_ms, &PyXgmi::set_timeout_ms)
       .def_property("algo", &PyXgmi::algo, &PyXgmi::set_algo)
-      .def_property("fault", &PyXgmi::fault, &PyXgmi::set_fault);
+      .def_property("fault", &PyXgmi::fault, &PyXgmi::set_fault)
+      .def_property("fused_two", &PyXgmi::fused_two, &PyXgmi::set_fused_two);
   py::class_<PyPrefetcher>(m, "PinnedPrefetcher")
       .def(py::init<int64_t, int, int>(), py::arg("slot_bytes"), py::arg("depth"), py::arg("device"))
       .def("slot", &PyPrefetcher::slot)

@@ -13,11 +13,12 @@ static void hcheck(hipError_t e, const char* what) {
 }
 
 // region: data [2][cap] | flags [2][G][W] | t1 [2][W][slot] | t2 [2][W][slot] | f1 [2][G][W] | f2 [2][G][W]
-//         | fg [2][max(cap, kFusedGranules)] (the fused step's granules) | fe (its device error word)
+//         | fg [2][max(cap, kFusedGranules)] (the fused step's granules) | fr [same] (its two-phase
+//         variant's reduced granules) | fe (its device error word)
 // (the t* / f* parts belong to the two-shot algorithm, ff to the fused LeNet step's exchange, which
 // shares `data`), every part 256-byte aligned
 struct RegionLayout {
-  size_t flags, t1, t2, f1, f2, fg, fe, bytes;
+  size_t flags, t1, t2, f1, f2, fg, fr, fe, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static int64_t fused_cap(int64_t cap) { return cap > XgmiAllReduce::kFusedGranules ? cap : XgmiAllReduce::kFusedGranules; }
@@ -30,7 +31,8 @@ static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t sl
   L.f1 = align256(L.t2 + tb);
   L.f2 = align256(L.f1 + fl);
   L.fg = align256(L.f2 + fl);                                           // fused step: [2][fcap] granules
-  L.fe = align256(L.fg + (size_t)2 * fused_cap(cap) * sizeof(uint64_t));  // fused step: device error word
+  L.fr = align256(L.fg + (size_t)2 * fused_cap(cap) * sizeof(uint64_t));  // two-phase: reduced granules
+  L.fe = align256(L.fr + (size_t)2 * fused_cap(cap) * sizeof(uint64_t));  // fused step: device error word
   L.bytes = L.fe + 256;
   return L;
 }
@@ -99,6 +101,7 @@ void XgmiAllReduce::open(const std::vector<std::string>& handles) {
     P->f1[q] = reinterpret_cast<uint64_t*>(c + L.f1);
     P->f2[q] = reinterpret_cast<uint64_t*>(c + L.f2);
     fg_[q] = reinterpret_cast<uint64_t*>(c + L.fg);
+    fr_[q] = reinterpret_cast<uint64_t*>(c + L.fr);
     if (q == rank_) derr_ = reinterpret_cast<unsigned*>(c + L.fe);
   }
   opened_ = true;
@@ -122,7 +125,11 @@ XgmiFused XgmiAllReduce::fused_view() const {
   XgmiFused X;
   std::memset(&X, 0, sizeof(X));
   (void)P;
-  for (int q = 0; q < world_; ++q) X.gran[q] = fg_[q];
+  for (int q = 0; q < world_; ++q) {
+    X.gran[q] = fg_[q];
+    X.red[q] = fr_[q];
+  }
+  X.two = two_ && world_ > 1 ? 1 : 0;
   X.seqs = fseqs_;
   X.err = err_;
   X.derr = derr_;

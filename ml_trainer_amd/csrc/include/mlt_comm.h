@@ -73,6 +73,10 @@ class XgmiAllReduce {
   // fault injection for tests: 1 = withhold half of this rank's slice flags (see allreduce.hip)
   void set_fault(int f) { fault_ = f; }
   int fault() const { return fault_; }
+  // fused LeNet step: two-phase exchange (each 64-granule chunk reduced by its owner rank, which
+  // publishes the sum for the others: 2 (W-1)/W of the granules per rank instead of W - 1)
+  void set_fused_two(bool t) { two_ = t; }
+  bool fused_two() const { return two_; }
   // 0 one-shot (pull everything), 1 two-shot (push reduce-scatter + push all-gather); every rank
   // must use the same algorithm for a given call. Graphs keep the algorithm they were captured with.
   void set_algo(int a);
@@ -103,6 +107,8 @@ class XgmiAllReduce {
   unsigned* derr_ = nullptr;  // device copy of the error word (in the region)
   bool opened_ = false;
   int fault_ = 0;
+  bool two_ = false;
+  uint64_t* fr_[8] = {nullptr};
   void* peers_host_ = nullptr;  // XgmiPeers
 };
 

@@ -253,12 +253,15 @@ void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank,
 // update in the same launch -- no flags, no barriers, one round trip. W = 1 is the loopback.
 struct XgmiFused {
   uint64_t* gran[kXgmiMaxRanks];   // per-rank [2][cap] granules (indexed by flat parameter offset)
+  uint64_t* red[kXgmiMaxRanks];    // two-phase exchange: per-rank [2][cap] granules of the REDUCED values
+                                   // of the 64-granule chunks that rank owns (chunk c: rank c % W)
   uint64_t* seqs;                  // [G] per-block launch counters (this rank)
   unsigned* err;                   // sticky error word (host-mapped: the host polls it)
   unsigned* derr;                  // its device copy (what the kernel reads)
   int64_t cap;
   long long timeout;               // ticks of the 100 MHz constant clock
   int rank, W, G, fault;
+  int two;                         // 1: two-phase exchange (reduce-scatter into owners, owners publish)
 };
 // two-shot variant: slot = floats per [rank] slot of t1 / t2 (>= ceil(n / W) rounded up to 4)
 void launch_xgmi_allreduce_2shot(float* grad, int64_t n, const XgmiPeers& P, int rank, int W, int64_t slot,

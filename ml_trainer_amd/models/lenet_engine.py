@@ -61,6 +61,16 @@ def fused_dp_forced() -> bool:
     return os.environ.get("MLT_LENET_FUSED_DP", "1") == "2"
 
 
+def fused_two_mode() -> str:
+    """The fused exchange's two-phase form (each 64-granule chunk reduced by one owner rank, which
+    publishes the sum: 2 (W-1)/W of the granules read per rank instead of W - 1): MLT_XGMI_FUSED_TWO
+    = "auto" (default: a vote candidate at W >= 4), "1" (forced whenever the fused step runs, any
+    W > 1), "0" (never)."""
+    import os
+    v = os.environ.get("MLT_XGMI_FUSED_TWO", "auto")
+    return v if v in ("0", "1") else "auto"
+
+
 class TransportError(RuntimeError):
     """The data-parallel gradient collective failed (peer timeout / RCCL async error)."""
 
@@ -109,6 +119,7 @@ class LeNetStepEngine:
         self.xgmi = None
         self.captures = 0  # hipGraphs captured so far (bench asserts none inside its timed region)
         self.dp_transport = "none" if self.world_size == 1 else "torch.distributed"
+        self.fused_two = False  # the fused exchange runs in its two-phase form
         # the transport is chosen once the optimizer is known (its self-test / timing trial runs the
         # engine's batch-reduction kernels, which need the flat-buffer layout of set_optimizer)
         self._transport_pending = self.world_size > 1
@@ -158,6 +169,14 @@ class LeNetStepEngine:
             if not fused_ok:
                 warnings.warn("fused xGMI exchange failed its self-test on some rank; using the "
                               "four-launch data-parallel step")
+        W = dist.get_world_size(process_group)
+        tmode = fused_two_mode()
+        two_ok = False
+        if fused_ok and W > 1 and (tmode == "1" or (tmode == "auto" and W >= 4)):
+            # the two-phase form proves itself the same way before it may be timed or chosen
+            two_ok = self._fused_selftest(x, process_group, two=True)
+            if not two_ok:
+                warnings.warn("two-phase fused xGMI exchange failed its self-test on some rank")
         self.eng.fused_dp = False
         t = self.flat.grad.clone()
         cands = []
@@ -179,7 +198,13 @@ class LeNetStepEngine:
             # four-launch step's collective behind the same batch reductions
             B = self.max_batch
             self.eng.set_xgmi(x)
-            cands.append(("xgmi-fused", lambda: self.eng.reduce_only(B, True)))
+
+            def fused(two):
+                x.fused_two = two
+                self.eng.reduce_only(B, True)
+            cands.append(("xgmi-fused", lambda: fused(False)))
+            if two_ok:
+                cands.append(("xgmi-fused2", lambda: fused(True)))
             cands.append(("reduce", lambda: self.eng.reduce_only(B, False)))
         times = {}
         for name, fn in cands:
@@ -194,7 +219,7 @@ class LeNetStepEngine:
             times[name] = s.elapsed_time(e) / 50
         # every rank votes with its own timings and health: the slowest rank decides (MAX), and
         # an xGMI error word raised on ANY rank during the trial rules the xGMI kernels out
-        names = ("xgmi", "xgmi2", "rccl", "xgmi-fused", "reduce")
+        names = ("xgmi", "xgmi2", "rccl", "xgmi-fused", "xgmi-fused2", "reduce")
         bad = 1.0 if (x is not None and x.error()) else 0.0
         coll_dev = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
         vote = torch.tensor([bad] + [times.get(k, float("inf")) for k in names], device=coll_dev)
@@ -203,12 +228,18 @@ class LeNetStepEngine:
         bad, agreed = v[0], dict(zip(names, v[1:]))
         if x is not None and bad != 0.0:
             warnings.warn("xGMI all-reduce failed its timing trial on some rank; using RCCL")
-            agreed["xgmi"] = agreed["xgmi2"] = agreed["xgmi-fused"] = float("inf")
+            agreed["xgmi"] = agreed["xgmi2"] = agreed["xgmi-fused"] = agreed["xgmi-fused2"] = float("inf")
         self.transport_times_ms = {k: agreed[k] for k in names if k in times}
         self.flat.grad.zero_()
         self.stats.zero_()  # (the trial reductions accumulated their stats)
         four = min(("xgmi", "xgmi2", "rccl"), key=lambda k: agreed[k])
-        if fused_ok and (fused_dp_forced() or agreed["xgmi-fused"] <= agreed["reduce"] + agreed[four]):
+        if x is not None:
+            x.fused_two = False
+        # the fused step's form: two-phase when forced, else when it measured faster on every rank
+        fk = "xgmi-fused2" if two_ok and (tmode == "1" or agreed["xgmi-fused2"] < agreed["xgmi-fused"]) else "xgmi-fused"
+        if fused_ok and (fused_dp_forced() or agreed[fk] <= agreed["reduce"] + agreed[four]):
+            x.fused_two = fk == "xgmi-fused2"
+            self.fused_two = x.fused_two
             self.eng.set_comm(None)
             self.eng.set_xgmi(x)
             self.eng.fused_dp = True
@@ -226,15 +257,17 @@ class LeNetStepEngine:
             self.eng.set_xgmi(x)
             self.dp_transport = "xgmi-oneshot" if best == "xgmi" else "xgmi-twoshot"
 
-    def _fused_selftest(self, x, process_group, rounds: int = 12) -> bool:
+    def _fused_selftest(self, x, process_group, rounds: int = 12, two: bool = False) -> bool:
         """Bring-up test of the fused step's exchange protocol on the real fabric (collective):
         ``rounds`` back-to-back rounds, each with fresh random per-rank activations / slabs, of the
         batch reductions alone (this rank's gradient) and of the batch reductions + granule exchange
         (the lenet_mwx kernel the fused step's update blocks share), under GEMM load from a side
         stream; every exchanged gradient word is compared with the host's RANK-ORDERED sum of every
-        rank's local gradient (what each rank's kernel computes), bitwise. MIN vote over ranks."""
+        rank's local gradient (what each rank's kernel computes), bitwise. MIN vote over ranks.
+        two: the two-phase form of the exchange (XgmiAllReduce.fused_two)."""
         import torch.distributed as dist
         dev = self.device
+        x.fused_two = two
         W = dist.get_world_size(process_group)
         rank = dist.get_rank(process_group)
         B = self.max_batch
@@ -273,8 +306,13 @@ class LeNetStepEngine:
         self.flat.grad.zero_()
         self.stats.zero_()
         self.eng.set_xgmi(None)
-        self.fused_selftest_ok = int(flag.item()) == 1
-        return self.fused_selftest_ok
+        x.fused_two = False
+        ok = int(flag.item()) == 1
+        if two:
+            self.fused2_selftest_ok = ok
+        else:
+            self.fused_selftest_ok = ok
+        return ok
 
     def _poll_transport(self) -> None:
         """Non-blocking health check of the in-graph collective, run after every graph replay:

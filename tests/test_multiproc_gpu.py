@@ -211,7 +211,7 @@ def _fused_dp_worker(rank, world, port, out_dir):
     N = 64 * world
     data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
     targets = torch.randint(0, 10, (N,), generator=gd)
-    for variant, fused, one in (("1", True, False), ("0", False, False), ("one", True, True)):
+    for variant, fused, one in (("1", True, False), ("0", False, False), ("one", True, True), ("two", True, False)):
         torch.manual_seed(0)
         m = MLModel().to(dev)
         flat = FlatParams(m.parameters())
@@ -221,6 +221,7 @@ def _fused_dp_worker(rank, world, port, out_dir):
         xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
         assert xe is not None
         xe.algo = 0
+        xe.fused_two = variant == "two"  # the exchange's two-phase form (chunk owners publish the sums)
         eng.use_transport(xgmi=xe, fused=fused)
         assert eng.dp_transport == ("xgmi-fused" if fused else "xgmi-oneshot")
         eng.set_dataset(data, targets, batch_size=8)
@@ -240,20 +241,22 @@ def _fused_dp_worker(rank, world, port, out_dir):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_lenet_bf16_fused_dp_matches_four_launch(world):
-    """Two launches per data-parallel step (and one with the opt-in one-launch step), bitwise equal to
-    the four-launch step and identical on every rank (W = 8: the node's size, as 8 processes on the
-    box's one GPU)."""
+    """Two launches per data-parallel step (and one with the opt-in one-launch step; and the exchange's
+    two-phase form), bitwise equal to the four-launch step and identical on every rank (W = 8: the
+    node's size, as 8 processes on the box's one GPU)."""
     r = _run(_fused_dp_worker, world)
     assert len(r) == world
     for d in r:
-        assert d["err1"] == 0 and d["err0"] == 0 and d["errone"] == 0
+        assert d["err1"] == 0 and d["err0"] == 0 and d["errone"] == 0 and d["errtwo"] == 0
         assert torch.equal(d["p1"], d["p0"]) and torch.equal(d["g1"], d["g0"])
+        assert torch.equal(d["ptwo"], d["p0"]) and torch.equal(d["gtwo"], d["g0"])
+        assert d["nodestwo"] == 6
         assert torch.equal(d["pone"], d["p0"]) and torch.equal(d["gone"], d["g0"])
         assert (d["nodesone"], d["nodes1"], d["nodes0"]) == (3, 6, 12)  # 1 / 2 / 4 kernels per step
         assert torch.equal(d["p1"], r[0]["p1"])
 
 
-def _selftest_worker(rank, world, port, out_dir, inject):
+def _selftest_worker(rank, world, port, out_dir, inject, two=False):
     """Transport bring-up of the bf16 engine at W = 2 (both ranks on the box's GPU): the fused
     exchange's own self-test runs before it may carry a step; MLT_XGMI_INJECT_FAULT="0:2" makes
     rank 0 publish corrupted values, which rank 1's check catches -- then EVERY rank rejects the
@@ -263,6 +266,8 @@ def _selftest_worker(rank, world, port, out_dir, inject):
     os.environ["MLT_XGMI_TIMEOUT_MS"] = "20000"
     if inject:
         os.environ["MLT_XGMI_INJECT_FAULT"] = "0:2"
+    if two:
+        os.environ["MLT_XGMI_FUSED_TWO"] = "1"
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -285,20 +290,25 @@ def _selftest_worker(rank, world, port, out_dir, inject):
     eng.train_steps(8, 4, use_graph=True, steps_per_graph=2)
     eng.check_transport()
     torch.cuda.synchronize()
-    out = {"ok": getattr(eng, "fused_selftest_ok", None), "transport": eng.dp_transport,
-           "times": eng.transport_times_ms, "p": flat.data.cpu()}
+    out = {"ok": getattr(eng, "fused_selftest_ok", None), "ok2": getattr(eng, "fused2_selftest_ok", None),
+           "two": eng.fused_two, "transport": eng.dp_transport, "times": eng.transport_times_ms, "p": flat.data.cpu()}
     torch.save(out, os.path.join(out_dir, f"s{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("inject", [False, True])
-def test_fused_exchange_selftest_and_fallback(inject):
+@pytest.mark.parametrize("inject,two", [(False, False), (True, False), (False, True)])
+def test_fused_exchange_selftest_and_fallback(inject, two):
+    """two: MLT_XGMI_FUSED_TWO=1 -- the two-phase form runs its own self-test and, when the fused
+    step is taken, carries it."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_selftest_worker, args=(2, free_port(), d, inject), nprocs=2, join=True)
+        mp.spawn(_selftest_worker, args=(2, free_port(), d, inject, two), nprocs=2, join=True)
         r = [torch.load(os.path.join(d, f"s{i}.pt"), weights_only=True) for i in range(2)]
     for x in r:
         assert x["ok"] is (not inject), x
+        if two:
+            assert x["ok2"] is True and "xgmi-fused2" in x["times"], x
+            assert x["two"] is (x["transport"] == "xgmi-fused"), x
         if inject:
             assert x["transport"] in ("xgmi-oneshot", "xgmi-twoshot"), x["transport"]
         else:
