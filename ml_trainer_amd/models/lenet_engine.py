@@ -440,6 +440,7 @@ class LeNetStepEngine:
             self.eng.set_comm(None)
             self.eng.set_xgmi(xgmi)
             self.eng.fused_dp = fused
+            self.fused_two = fused and bool(getattr(xgmi, "fused_two", False))
             if fused:
                 self.dp_transport = "xgmi-fused"
             else:
