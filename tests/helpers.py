@@ -4,7 +4,28 @@ import socket
 import torch
 
 
+_PORTS_USED = set()
+
+
 def free_port() -> int:
+    """A rendezvous port for spawned ranks: drawn below the kernel's ephemeral range (32768+), so an
+    outgoing connection cannot take it between this check and the rank's bind (which the OS-picked
+    port 0 allowed: EADDRINUSE flakes), never handed out twice in one test process."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        if p in _PORTS_USED:
+            continue
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        _PORTS_USED.add(p)
+        return p
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
