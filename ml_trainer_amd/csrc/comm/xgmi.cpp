@@ -127,7 +127,7 @@ XgmiFused XgmiAllReduce::fused_view() const {
   (void)P;
   for (int q = 0; q < world_; ++q) {
     X.gran[q] = fg_[q];
-    X.red[q] = fr_[q];
+    if (fr_[q] != fg_[q] + 2 * fused_cap(cap_)) throw std::runtime_error("xgmi: fused region layout");
   }
   X.two = two_ && world_ > 1 ? 1 : 0;
   X.seqs = fseqs_;

@@ -252,9 +252,10 @@ void launch_xgmi_allreduce(float* grad, int64_t n, const XgmiPeers& P, int rank,
 // W - 1 peers' granules of ITS elements until their tags match, sums in rank order and applies the
 // update in the same launch -- no flags, no barriers, one round trip. W = 1 is the loopback.
 struct XgmiFused {
-  uint64_t* gran[kXgmiMaxRanks];   // per-rank [2][cap] granules (indexed by flat parameter offset)
-  uint64_t* red[kXgmiMaxRanks];    // two-phase exchange: per-rank [2][cap] granules of the REDUCED values
-                                   // of the 64-granule chunks that rank owns (chunk c: rank c % W)
+  uint64_t* gran[kXgmiMaxRanks];   // per-rank [2][cap] granules (indexed by flat parameter offset),
+                                   // followed (gran + 2 cap) by the two-phase exchange's [2][cap] granules
+                                   // of the REDUCED values of the 64-granule chunks the rank owns
+                                   // (chunk c: rank c % W)
   uint64_t* seqs;                  // [G] per-block launch counters (this rank)
   unsigned* err;                   // sticky error word (host-mapped: the host polls it)
   unsigned* derr;                  // its device copy (what the kernel reads)

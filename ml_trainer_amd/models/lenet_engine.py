@@ -161,7 +161,9 @@ class LeNetStepEngine:
         if self.comm is None and self.xgmi is None:
             return
         fused_ok = False
-        if x is not None and self.precision == "bf16" and fused_dp_enabled():
+        W = dist.get_world_size(process_group)
+        # (the fused exchange kernels, and their self-test / flush path, exist for 2, 4 and 8 ranks)
+        if x is not None and self.precision == "bf16" and fused_dp_enabled() and W in (2, 4, 8):
             # bf16 over xGMI: the exchange can run inside the step (one launch per step), but only
             # once its own protocol -- not just the one-/two-shot kernels -- proved bit-exact on
             # this fabric, on every rank
@@ -169,7 +171,6 @@ class LeNetStepEngine:
             if not fused_ok:
                 warnings.warn("fused xGMI exchange failed its self-test on some rank; using the "
                               "four-launch data-parallel step")
-        W = dist.get_world_size(process_group)
         tmode = fused_two_mode()
         two_ok = False
         if fused_ok and W > 1 and (tmode == "1" or (tmode == "auto" and W >= 4)):
