@@ -37,7 +37,7 @@ BASELINE.json config 5 ("large" fp8: 24L/1024H BERT encoder, OCP fp8 forward/dgr
 delayed scaling): ``--model large [--grad-accum N]`` (``--model bert-large`` = same model in bf16).
 
 BASELINE.json config 4 (BERT-base classifier, seq 512, bf16, DDP): ``--model bert-base``
-(per-GPU batch --batch, default 1024; native MFMA GEMM / flash-attention / LayerNorm kernels,
+(per-GPU batch --batch, default 1536; native MFMA GEMM / flash-attention / LayerNorm kernels,
 fused AdamW on flat fp32 masters with bf16 shadows, bucketed RCCL all-reduce overlapped with
 backward for N > 1).
 """
@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch (weak) / global batch (reference); default 32 (LeNet), "
-                         "1024 (bert-base: 152 GiB), 256 (bert-large), 512 (large fp8: 245 GiB of HBM)")
+                         "1536 (bert-base: 228 GiB), 256 (bert-large), 512 (large fp8: 245 GiB of HBM)")
     ap.add_argument("--scaling", choices=["weak", "reference"], default="weak")
     ap.add_argument("--model", default="default",
                     choices=["default", "tiny", "bert-base", "bert-tiny", "bert-large", "large"])
@@ -493,8 +493,10 @@ def main():
         # BERT-base 2,552 / 2,665 / 2,710 samples/s at 128 / 256 / 512 using 21 / 40 / 77 GiB; the fp8
         # `large` config, BASELINE config 5 "sized to fill HBM": 1,013 / 1,030 samples/s at 256 / 512
         # using 126 / 245 GiB; profiles/batch_sweep_r2.jsonl; round 4, same box: BERT-base 2,921 / 2,929
-        # at 512 vs 2,965 / 2,964 at 1024 (152 GiB), profiles/r4/bert_base_batch_groupm_ab.jsonl)
-        args.batch = {"bert-base": 1024, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
+        # at 512 vs 2,965 / 2,964 at 1024 (152 GiB), profiles/r4/bert_base_batch_groupm_ab.jsonl; round 5,
+        # same box: 3,084 / 3,088 at 1024 vs 3,112 / 3,110 at 1536 (228 GiB),
+        # profiles/r5/bert_base_batch_1024_1536.jsonl)
+        args.batch = {"bert-base": 1536, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
 
     if args.device == "cpu" or not torch.cuda.is_available():
         if world > 1:
