@@ -401,9 +401,9 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     t0 = time.perf_counter()
     samples = run(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if world > 1:  # (one rank: no barrier, and nothing left for a second synchronize to wait for)
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if engine.captures != captures_before:
         raise RuntimeError("a hipGraph was captured inside the timed region")
