@@ -1396,6 +1396,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return py::make_tuple(p.cfg, p.splits, p.ksteps, p.ws_floats, p.ext);
   }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cfg") = -1, py::arg("splits") = 0);
   m.def("set_gemm_split_mode", &set_gemm_split_mode, py::arg("mode"));
+  m.def("set_gemm_w4q8", &set_gemm_w4q8, py::arg("on"));
   m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
   m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
   m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));

@@ -126,5 +126,7 @@ void launch_gemm_w4_f8_splitk(const uint8_t* A, const uint8_t* B, float* ws, int
 template <typename OutT, int FA, int FB>
 void launch_gemm_w4_f8(const uint8_t* A, const uint8_t* B, OutT* C, int M, int N, int K, int64_t lda, int64_t ldb,
                        int64_t ldc, const GemmEpi& e, int group_m, hipStream_t st);
+bool launch_gemm_w4_f8_q(int fmt_a, const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K,
+                         int64_t lda, int64_t ldb, int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st);
 
 }  // namespace mlt

@@ -185,6 +185,7 @@ struct GemmPlan {
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits,
                         int accumulate = 0);
 void set_gemm_split_mode(int mode);  // -1 planner, 0 in-kernel last-arriver, 1 external reduce
+void set_gemm_w4q8(int on);          // gemm_f8_q GELU: 1 4-wave kernel, 0 ping-pong, -1 env
 void launch_gemm_bf16(const GemmPlan& plan, int a_mn, int b_mn, bool out_f32, const uint16_t* A, const uint16_t* B,
                       void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
                       const uint16_t* aux, int64_t ldaux, const uint16_t* res, int64_t ldres, float alpha, int mode,

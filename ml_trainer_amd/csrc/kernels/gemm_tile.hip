@@ -1141,6 +1141,10 @@ void launch_split_reduce(const GemmPlan& p, const float* ws, OutT* C, int M, int
 
 void set_gemm_split_mode(int mode) { g_split_mode = mode; }
 
+// which kernel runs gemm_f8_q's GELU epilogue: 1 the 4-wave one, 0 the ping-pong one, -1 MLT_GEMM_W4Q8
+static int g_w4q8 = -1;
+void set_gemm_w4q8(int on) { g_w4q8 = on; }
+
 GemmPlan plan_gemm_bf16(int a_mn, int b_mn, int M, int N, int K, int force_cfg, int force_splits, int accumulate) {
   (void)b_mn;
   // (the 4-wave kernel's in-kernel epilogue cannot accumulate into C: an accumulating GEMM takes it
@@ -1272,9 +1276,17 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
   e.q_amax = out_amax;
   e.q_colpart = colpart;
   e.q_fmt = out_fmt;
-  // (the ping-pong kernel: a 4-wave form of this epilogue measured slower -- 2.73 vs 2.43 ms per
-  // FFN1 call in the fp8 `large` step, its GELU / fp8-pack VALU serialised behind the main loop --
-  // and needed more than 256 VGPRs; profiles/README.md, round 4)
+  // the 4-wave kernel's quantising GELU epilogue when it fits (MLT_GEMM_W4Q8=0 / set_gemm_w4q8(0):
+  // the ping-pong kernel's): 1.93 vs 2.27 ms per FFN1 call of the fp8 `large` step (262144 x 4096 x
+  // 1024; profiles/r5/fp8_q8_w4_ab.jsonl). Its first form, Y^T stored as 64 rows x 16 bytes per
+  // instruction, took 2.63 ms: the 4-wave epilogue is not hidden behind another wave group's main
+  // loop, so the Y^T pass is stored as 16 columns x 64 contiguous bytes per instruction instead.
+  // (Round 4's 4-wave q8 form, on the erf GELU, had lost too: 2.73 vs 2.43 ms.)
+  if (g_w4q8 < 0) {
+    const char* v = getenv("MLT_GEMM_W4Q8");
+    g_w4q8 = (v && atoi(v) == 0) ? 0 : 1;
+  }
+  if (g_w4q8 && launch_gemm_w4_f8_q(fmt_a, A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st)) return;
   GemmPlan p{5, 1, K / 128, 0, 0};
   if (fmt_a == 0 && fmt_b == 0)
     launch_pp<false, false, uint8_t, 0, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);

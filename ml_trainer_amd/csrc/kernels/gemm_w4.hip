@@ -20,6 +20,7 @@
 // Requirements (host-checked, else the caller falls back): M, N multiples of 256, K a multiple of
 // 128 and >= 256, 16-byte aligned rows, no split-K / accumulate / fp8 scales.
 #include "mlt_common.h"
+#include "mlt_fp8.h"
 #include "mlt_gemm.h"
 #include "mlt_gemm_tile.h"
 #include "gemm_w4_loop.inc"
@@ -27,7 +28,15 @@
 namespace mlt {
 
 
-enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3 };
+// W4_Q8GELU / W4_Q8DGELU: the quantising ("q8") epilogues of the fp8 FFN (OutT = fp8 bytes): GELU /
+// dGELU as W4_GELU / W4_DGELU, then amax, scale, fp8 Y (e4m3 / e5m2) and fp8 Y^T from the same LDS image
+enum W4Epi { W4_PLAIN = 0, W4_GELU = 1, W4_RES = 2, W4_DGELU = 3, W4_Q8GELU = 4, W4_Q8DGELU = 5 };
+template <int EK>
+constexpr bool w4_gel() { return EK == W4_GELU || EK == W4_Q8GELU; }
+template <int EK>
+constexpr bool w4_dgel() { return EK == W4_DGELU || EK == W4_Q8DGELU; }
+template <int EK>
+constexpr bool w4_q8() { return EK == W4_Q8GELU || EK == W4_Q8DGELU; }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // LDS: two K-tile stages of 64 KB; after the loop, four per-wave 64 x 132 fp32 epilogue images
@@ -45,7 +54,7 @@ constexpr int kW4Pitch = 132, kW4Smem = 4 * 64 * kW4Pitch * 4 > 131072 ? 4 * 64 
 #endif
 template <int EK>
 constexpr bool w4_gelu_tab() {
-  return MLT_W4_GELU_TAB && (EK == W4_GELU || EK == W4_DGELU);
+  return MLT_W4_GELU_TAB && (w4_gel<EK>() || w4_dgel<EK>());
 }
 template <int EK>
 constexpr int w4_smem() {
@@ -55,7 +64,7 @@ static_assert(kW4Smem + kGeluTabBytes <= 160 * 1024, "GELU table must fit beside
 // workgroup copy of the epilogue's table into LDS (read only after the epilogue's first barrier)
 template <int EK>
 __device__ __forceinline__ void w4_load_gelu_tab(uint8_t* smem) {
-  if constexpr (w4_gelu_tab<EK>()) gelu_tab_load(smem + kW4Smem, EK == W4_DGELU, 256);
+  if constexpr (w4_gelu_tab<EK>()) gelu_tab_load(smem + kW4Smem, w4_dgel<EK>(), 256);
 }
 
 // ---- epilogue through LDS: a lane's accumulator fragment holds 4 columns of one row, so direct
@@ -71,6 +80,9 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
   constexpr int P = kW4Pitch;
   float* img = reinterpret_cast<float*>(smem) + w * 64 * P;
   const int rsub = lane >> 4, cc = lane & 15;  // read side: row 4 * it + rsub, columns 8 cc .. + 7
+  constexpr int QF = EK == W4_Q8DGELU ? 1 : 0;  // q8 output format: e4m3 (GELU: FFN2's input) / e5m2 (dGELU: a dY)
+  float q_amx = 0.f, q_s = 1.f;
+  if constexpr (w4_q8<EK>()) q_s = *epi.q_scale;
   const int gn = n0 + wc * 128 + 8 * cc;
   float bs[8];
 #pragma unroll
@@ -107,7 +119,7 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
       asm volatile(MLT_W4_IMG_H0 ::[va] "v"(va) : "memory");
     else
       asm volatile(MLT_W4_IMG_H1 ::[va] "v"(va) : "memory");
-    if constexpr (EK == W4_DGELU) side_loads(h, sd[0]);
+    if constexpr (w4_dgel<EK>()) side_loads(h, sd[0]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own image: no barrier needed
     float csum[8];  // dGELU + q_colpart: the half's column sums (bias gradient of the dGELU output)
 #pragma unroll
@@ -120,7 +132,7 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bs[e];
-      if constexpr (EK == W4_GELU) {  // keep the (bf16-rounded) pre-activation for the backward
+      if constexpr (w4_gel<EK>()) {  // keep the (bf16-rounded) pre-activation for the backward
         uint32_t a[4];                // (two-wide GELU: this epilogue is VALU-bound, mlt_gemm.h)
         f32x2 x2[4];
 #pragma unroll
@@ -138,7 +150,7 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         }
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) v[2 * q2] = x2[q2].x, v[2 * q2 + 1] = x2[q2].y;
-      } else if constexpr (EK == W4_DGELU) {
+      } else if constexpr (w4_dgel<EK>()) {
         const uint4 sv = sd[0][it];
         f32x2 x2[4];
         if constexpr (w4_gelu_tab<EK>()) {
@@ -163,6 +175,20 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += bf16_to_f32((uint16_t)(sw4[e >> 1] >> (16 * (e & 1))));
       }
+      if constexpr (w4_q8<EK>()) {
+        // amax of the unscaled output, then the SCALED values: fp8 row store, and back into the
+        // image for the transposed pass below
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          q_amx = fmaxf(q_amx, fabsf(v[e]));
+          v[e] *= q_s;
+        }
+        *reinterpret_cast<float4*>(img + row * P + 8 * cc) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(img + row * P + 8 * cc + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(C) + (int64_t)gm * ldc + gn) =
+            make_uint2(pack4_fp8<QF>(v[0], v[1], v[2], v[3]), pack4_fp8<QF>(v[4], v[5], v[6], v[7]));
+        continue;
+      }
       OutT* cp = C + (int64_t)gm * ldc + gn;
       if constexpr (sizeof(OutT) == 4) {
         *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
@@ -173,7 +199,32 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
                        cvt_pk_bf16(f32x2{v[4], v[5]}), cvt_pk_bf16(f32x2{v[6], v[7]}));
       }
     }
-    if constexpr (EK == W4_DGELU) {
+    if constexpr (w4_q8<EK>()) {
+      // Y^T: per pass p, lane (kq = lane / 16, cq = lane % 16) takes columns 32 p + 2 cq, + 1 and
+      // rows 16 kq .. + 15 of the half's image: one 16-byte store per column, the 4 kq lanes of a
+      // column covering its 64 contiguous bytes of the consumer's k-contiguous operand
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row pass's image writes (this wave's own)
+      const int kq = lane >> 4, cq = lane & 15;
+      const int qoff = 2 * cq * (int)epi.ldqt + 16 * kq;  // the lane's part: a 32-bit offset off a wave-uniform base
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float* cimg = img + (16 * kq) * P + 32 * p + 2 * cq;
+        uint8_t* const qt0 = epi.qt + (int64_t)(n0 + wc * 128 + 32 * p) * epi.ldqt + (m0 + wr * 128 + 64 * h) + qoff;
+        uint32_t w0[4], w1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float2 x0 = *reinterpret_cast<const float2*>(cimg + (4 * k + 0) * P);
+          const float2 x1 = *reinterpret_cast<const float2*>(cimg + (4 * k + 1) * P);
+          const float2 x2 = *reinterpret_cast<const float2*>(cimg + (4 * k + 2) * P);
+          const float2 x3 = *reinterpret_cast<const float2*>(cimg + (4 * k + 3) * P);
+          w0[k] = pack4_fp8<QF>(x0.x, x1.x, x2.x, x3.x);
+          w1[k] = pack4_fp8<QF>(x0.y, x1.y, x2.y, x3.y);
+        }
+        *reinterpret_cast<uint4*>(qt0) = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+        *reinterpret_cast<uint4*>(qt0 + epi.ldqt) = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+      }
+    }
+    if constexpr (w4_dgel<EK>()) {
       if (epi.q_colpart) {  // the 4 lanes of a column group (rsub) hold 16 rows each: one 64-row block
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -188,6 +239,10 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
       }
     }
     if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
+  }
+  if constexpr (w4_q8<EK>()) {  // this wave's amax into the output's slots
+    q_amx = wave_max(q_amx);
+    if (lane == 0) atomic_max_pos(epi.q_amax, q_amx);
   }
 }
 
@@ -555,6 +610,26 @@ bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t
   if (e.mode != 0 && e.res) return false;
   return true;
 }
+// the quantising fp8 FFN1 epilogue on the 4-wave kernel (gemm_f8_q, GELU: e4m3 A, e4m3 out);
+// false when the shape / layout / formats do not fit
+bool launch_gemm_w4_f8_q(int fmt_a, const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K,
+                         int64_t lda, int64_t ldb, int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st) {
+  if (M % 256 || N % 256 || K % 256 || K < 512) return false;
+  if (lda % 16 || ldb % 16 || ldy % 16 || e.ldqt % 16 || e.ldqt * 32 >= (int64_t)1 << 31) return false;
+  if (lda * 256 > (int64_t)1 << 31 || ldb * 256 > (int64_t)1 << 31) return false;
+  if (!e.aux || !e.qt || !e.q_scale || !e.q_amax || e.res || e.accumulate) return false;
+  if ((e.ldaux * 2) % 16 || ((uintptr_t)e.aux) % 16 || ((uintptr_t)e.qt) % 16 || ((uintptr_t)Y) % 16) return false;
+  if (e.bias && ((uintptr_t)e.bias) % 16) return false;
+  if (e.mode == 1 && fmt_a == 0 && e.q_fmt == 0 && !e.q_colpart) {
+    launch_w4f8_ek<uint8_t, W4_Q8GELU, 0, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, group_m, st);
+    return true;
+  }
+  // (the dGELU form -- W4_Q8DGELU, column partials on top of the quantising epilogue -- needs more
+  // VGPRs than the asm-owned-accumulator layout leaves: the compiler spills 122 values into the
+  // accumulator AGPRs, which the build guard refuses; FFN2-dgrad stays on the ping-pong kernel)
+  return false;
+}
+
 #define MLT_W4F8_INST(OT, FA, FB)                                                                                   \
   template void launch_gemm_w4_f8<OT, FA, FB>(const uint8_t*, const uint8_t*, OT*, int, int, int, int64_t, int64_t, \
                                               int64_t, const GemmEpi&, int, hipStream_t);

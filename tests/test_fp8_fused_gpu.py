@@ -74,6 +74,34 @@ def test_gemm_f8_q_matches_fp32(dev, mode, shape):
         torch.testing.assert_close(cs, 7.0 + ref.sum(0), rtol=1e-3, atol=1e-3 * ref.abs().sum(0).max().item())
 
 
+@pytest.mark.parametrize("shape", [(1024, 512, 1024), (8192, 2048, 512), (4096, 4096, 1024)])
+def test_gemm_f8_q_gelu_4wave_matches_pingpong(dev, shape):
+    """FFN1's quantising GELU epilogue on the 4-wave kernel (gemm_w4.hip W4_Q8GELU) writes the same
+    bytes -- fp8 Y, Y^T, bf16 pre-activation, amax -- as the ping-pong kernel's (q8_quadrant)."""
+    C = require_native()
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _rand_f8((M, K), 0, g, dev, 2.0)
+    B = _rand_f8((N, K), 0, g, dev, 2.0)
+    bias = torch.randn(N, generator=g).to(dev)
+    isa, isb = torch.tensor([0.5], device=dev), torch.tensor([0.125], device=dev)
+    scale = torch.tensor([3.0], device=dev)
+    outs = []
+    try:
+        for on in (1, 0):
+            C.set_gemm_w4q8(on)
+            Y = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=dev)
+            Yt = torch.empty(N, M, dtype=torch.float8_e4m3fn, device=dev)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
+            C.gemm_f8_q(A, B, Y, Yt, 0, 0, isa, isb, 0, scale, amax, bias=bias, aux=aux, mode=1)
+            outs.append((Y.view(torch.uint8), Yt.view(torch.uint8), aux, amax.max()))
+    finally:
+        C.set_gemm_w4q8(-1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_gemm_f8_q_rejects_edge_shapes(dev):
     C = require_native()
     A = torch.zeros(320, 128, dtype=torch.float8_e4m3fn, device=dev)
