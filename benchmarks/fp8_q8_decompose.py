@@ -1,7 +1,8 @@
 """Where the fp8 quantising FFN1 GEMM's time goes (large config shape: M tokens x 4096, K = 1024):
 the plain GEMM on the 4-wave kernel (cfg 7) and on the ping-pong kernel (cfg 5), each with the
-bf16 bias + GELU epilogue (pre-activation saved), and the quantising (q8) epilogue of the ping-pong
-kernel (fp8 Y + Y^T + amax). One JSON line. FFN_TOKENS (default 262144)."""
+bf16 bias + GELU epilogue (pre-activation saved), and the quantising (q8) epilogues of gemm_f8_q
+(fp8 Y + Y^T + amax): FFN1's GELU and FFN2-dgrad's dGELU (+ column sums). MLT_GEMM_W4Q8=0 puts the
+q8 forms on the ping-pong kernel instead of the 4-wave one. One JSON line. FFN_TOKENS (default 262144)."""
 import json
 import os
 import sys
@@ -45,6 +46,14 @@ for cfg in (7, 5):
                                                           cfg=cfg)), 4)
 r["q8_gelu_ms"] = round(timeit(lambda: C.gemm_f8_q(x8, w1, a8, a8t, 0, 0, one, one, 0, one, amax, bias=b1, aux=pre,
                                                    mode=1)), 4)
+# FFN2-dgrad's quantising dGELU form: e5m2 dY (T x H) x W2 (stored [F][H]) -> e5m2 dA + its transpose,
+# times gelu'(pre-activation), column sums (the FFN1 bias gradient)
+dy8 = torch.randn(T, H, device=dev).to(torch.float8_e5m2)
+g8 = torch.empty(T, F, dtype=torch.float8_e5m2, device=dev)
+g8t = torch.empty(F, T, dtype=torch.float8_e5m2, device=dev)
+cs = torch.zeros(F, device=dev)
+r["q8_dgelu_ms"] = round(timeit(lambda: C.gemm_f8_q(dy8, w1, g8, g8t, 1, 0, one, one, 1, one, amax, aux=pre, mode=2,
+                                                    colsum_out=cs, colsum_accumulate=True)), 4)
 fl = 2.0 * T * F * H
 for k in list(r):
     if k.endswith("_ms"):

@@ -1276,9 +1276,10 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
   e.q_amax = out_amax;
   e.q_colpart = colpart;
   e.q_fmt = out_fmt;
-  // the 4-wave kernel's quantising GELU epilogue when it fits (MLT_GEMM_W4Q8=0 / set_gemm_w4q8(0):
-  // the ping-pong kernel's): 1.93 vs 2.27 ms per FFN1 call of the fp8 `large` step (262144 x 4096 x
-  // 1024; profiles/r5/fp8_q8_w4_ab.jsonl). Its first form, Y^T stored as 64 rows x 16 bytes per
+  // the 4-wave kernel's quantising epilogues when they fit (MLT_GEMM_W4Q8=0 / set_gemm_w4q8(0): the
+  // ping-pong kernel's): 1.93 vs 2.27 ms per FFN1 (GELU) call and 1.97 vs 2.37 ms per FFN2-dgrad
+  // (dGELU) call of the fp8 `large` step (262144 x 4096 x 1024), 1,262 vs 1,204 samples/s for the
+  // step (profiles/r5/fp8_q8_w4_ab.jsonl). Its first form, Y^T stored as 64 rows x 16 bytes per
   // instruction, took 2.63 ms: the 4-wave epilogue is not hidden behind another wave group's main
   // loop, so the Y^T pass is stored as 16 columns x 64 contiguous bytes per instruction instead.
   // (Round 4's 4-wave q8 form, on the erf GELU, had lost too: 2.73 vs 2.43 ms.)

@@ -98,13 +98,17 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
   // which hold the not-yet-read accumulators (scripts/check_w4_agpr.py guards every build)
   constexpr int SH = EK == W4_RES ? 2 : 1;
   uint4 sd[SH][16];
-  auto side_loads = [&](int h, uint4 (&dst)[16]) __attribute__((always_inline)) {
+  // (the quantising dGELU form loads them in two 8-row batches, its row loop unrolled by 8 to match:
+  // fully unrolled, the compiler spilled 108-207 values into the accumulator AGPRs)
+  constexpr int SB = EK == W4_Q8DGELU ? 8 : 16;
+  auto side_loads = [&](int h, uint4 (&dst)[16], int it0 = 0) __attribute__((always_inline)) {
     const uint16_t* sx = EK == W4_RES ? epi.res : epi.aux;
     const int64_t ldx = EK == W4_RES ? epi.ldres : epi.ldaux;
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int i = 0; i < SB; ++i) {
+      const int it = it0 + i;
       const int gm = m0 + wr * 128 + 64 * h + 4 * it + rsub;
-      dst[it] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
+      dst[i] = *reinterpret_cast<const uint4*>(sx + (int64_t)gm * ldx + gn);
     }
   };
   if constexpr (EK == W4_RES) {
@@ -124,9 +128,12 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
     float csum[8];  // dGELU + q_colpart: the half's column sums (bias gradient of the dGELU output)
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-#pragma unroll
+#pragma unroll SB
     for (int it = 0; it < 16; ++it) {
       const int row = 4 * it + rsub, gm = m0 + wr * 128 + 64 * h + row;
+      if constexpr (SB < 16) {
+        if (it > 0 && it % SB == 0) side_loads(h, sd[0], it);
+      }
       const float4 lo = *reinterpret_cast<const float4*>(img + row * P + 8 * cc);
       const float4 hi = *reinterpret_cast<const float4*>(img + row * P + 8 * cc + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -151,7 +158,7 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) v[2 * q2] = x2[q2].x, v[2 * q2 + 1] = x2[q2].y;
       } else if constexpr (w4_dgel<EK>()) {
-        const uint4 sv = sd[0][it];
+        const uint4 sv = sd[0][it % SB];
         f32x2 x2[4];
         if constexpr (w4_gelu_tab<EK>()) {
           const uint32_t sw4[4] = {sv.x, sv.y, sv.z, sv.w};
@@ -199,6 +206,20 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
                        cvt_pk_bf16(f32x2{v[4], v[5]}), cvt_pk_bf16(f32x2{v[6], v[7]}));
       }
     }
+    if constexpr (w4_dgel<EK>()) {
+      if (epi.q_colpart) {  // the 4 lanes of a column group (rsub) hold 16 rows each: one 64-row block
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          csum[e] += __shfl_xor(csum[e], 16);
+          csum[e] += __shfl_xor(csum[e], 32);
+        }
+        if (rsub == 0) {
+          float* cp = epi.q_colpart + (int64_t)((m0 + wr * 128 + 64 * h) >> 6) * N + gn;
+          *reinterpret_cast<float4*>(cp) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+        }
+      }
+    }
     if constexpr (w4_q8<EK>()) {
       // Y^T: per pass p, lane (kq = lane / 16, cq = lane % 16) takes columns 32 p + 2 cq, + 1 and
       // rows 16 kq .. + 15 of the half's image: one 16-byte store per column, the 4 kq lanes of a
@@ -222,20 +243,6 @@ __device__ __forceinline__ void w4_epilogue(OutT* __restrict__ C, int64_t ldc, c
         }
         *reinterpret_cast<uint4*>(qt0) = make_uint4(w0[0], w0[1], w0[2], w0[3]);
         *reinterpret_cast<uint4*>(qt0 + epi.ldqt) = make_uint4(w1[0], w1[1], w1[2], w1[3]);
-      }
-    }
-    if constexpr (w4_dgel<EK>()) {
-      if (epi.q_colpart) {  // the 4 lanes of a column group (rsub) hold 16 rows each: one 64-row block
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          csum[e] += __shfl_xor(csum[e], 16);
-          csum[e] += __shfl_xor(csum[e], 32);
-        }
-        if (rsub == 0) {
-          float* cp = epi.q_colpart + (int64_t)((m0 + wr * 128 + 64 * h) >> 6) * N + gn;
-          *reinterpret_cast<float4*>(cp) = make_float4(csum[0], csum[1], csum[2], csum[3]);
-          *reinterpret_cast<float4*>(cp + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
-        }
       }
     }
     if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is rewritten
@@ -610,8 +617,9 @@ bool gemm_w4_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t
   if (e.mode != 0 && e.res) return false;
   return true;
 }
-// the quantising fp8 FFN1 epilogue on the 4-wave kernel (gemm_f8_q, GELU: e4m3 A, e4m3 out);
-// false when the shape / layout / formats do not fit
+// the quantising fp8 FFN epilogues on the 4-wave kernel (gemm_f8_q): FFN1's GELU (e4m3 A, e4m3 out)
+// and FFN2-dgrad's dGELU (e5m2 A, e5m2 out, column partials); false when the shape / layout /
+// formats do not fit
 bool launch_gemm_w4_f8_q(int fmt_a, const uint8_t* A, const uint8_t* B, uint8_t* Y, int M, int N, int K,
                          int64_t lda, int64_t ldb, int64_t ldy, const GemmEpi& e, int group_m, hipStream_t st) {
   if (M % 256 || N % 256 || K % 256 || K < 512) return false;
@@ -624,9 +632,10 @@ bool launch_gemm_w4_f8_q(int fmt_a, const uint8_t* A, const uint8_t* B, uint8_t*
     launch_w4f8_ek<uint8_t, W4_Q8GELU, 0, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, group_m, st);
     return true;
   }
-  // (the dGELU form -- W4_Q8DGELU, column partials on top of the quantising epilogue -- needs more
-  // VGPRs than the asm-owned-accumulator layout leaves: the compiler spills 122 values into the
-  // accumulator AGPRs, which the build guard refuses; FFN2-dgrad stays on the ping-pong kernel)
+  if (e.mode == 2 && fmt_a == 1 && e.q_fmt == 1) {
+    launch_w4f8_ek<uint8_t, W4_Q8DGELU, 1, 0>(A, B, Y, M, N, K, lda, ldb, ldy, e, group_m, st);
+    return true;
+  }
   return false;
 }
 

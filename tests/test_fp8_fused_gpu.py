@@ -74,32 +74,41 @@ def test_gemm_f8_q_matches_fp32(dev, mode, shape):
         torch.testing.assert_close(cs, 7.0 + ref.sum(0), rtol=1e-3, atol=1e-3 * ref.abs().sum(0).max().item())
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("shape", [(1024, 512, 1024), (8192, 2048, 512), (4096, 4096, 1024)])
-def test_gemm_f8_q_gelu_4wave_matches_pingpong(dev, shape):
-    """FFN1's quantising GELU epilogue on the 4-wave kernel (gemm_w4.hip W4_Q8GELU) writes the same
-    bytes -- fp8 Y, Y^T, bf16 pre-activation, amax -- as the ping-pong kernel's (q8_quadrant)."""
+def test_gemm_f8_q_4wave_matches_pingpong(dev, mode, shape):
+    """The quantising epilogues on the 4-wave kernel (gemm_w4.hip W4_Q8GELU: FFN1, e4m3; W4_Q8DGELU:
+    FFN2-dgrad, e5m2) write the same bytes -- fp8 Y, Y^T, the bf16 pre-activation, amax -- as the
+    ping-pong kernel's (q8_quadrant); the dGELU column sums (bias gradient) agree to fp32 rounding
+    (their 64-row partials are summed in a different order)."""
     C = require_native()
     M, N, K = shape
-    g = torch.Generator().manual_seed(M + N + K)
-    A = _rand_f8((M, K), 0, g, dev, 2.0)
+    g = torch.Generator().manual_seed(M + N + K + mode)
+    fa = fo = 1 if mode == 2 else 0
+    A = _rand_f8((M, K), fa, g, dev, 2.0)
     B = _rand_f8((N, K), 0, g, dev, 2.0)
-    bias = torch.randn(N, generator=g).to(dev)
+    bias = torch.randn(N, generator=g).to(dev) if mode == 1 else None
+    pre = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16).to(dev)
     isa, isb = torch.tensor([0.5], device=dev), torch.tensor([0.125], device=dev)
     scale = torch.tensor([3.0], device=dev)
     outs = []
     try:
         for on in (1, 0):
             C.set_gemm_w4q8(on)
-            Y = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=dev)
-            Yt = torch.empty(N, M, dtype=torch.float8_e4m3fn, device=dev)
-            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            Y = torch.empty(M, N, dtype=F8[fo], device=dev)
+            Yt = torch.empty(N, M, dtype=F8[fo], device=dev)
+            aux = pre.clone() if mode == 2 else torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             amax = torch.zeros(C.FP8_AMAX_SLOTS, device=dev)
-            C.gemm_f8_q(A, B, Y, Yt, 0, 0, isa, isb, 0, scale, amax, bias=bias, aux=aux, mode=1)
-            outs.append((Y.view(torch.uint8), Yt.view(torch.uint8), aux, amax.max()))
+            cs = torch.full((N,), 7.0, device=dev) if mode == 2 else None
+            C.gemm_f8_q(A, B, Y, Yt, fa, 0, isa, isb, fo, scale, amax, bias=bias, aux=aux, mode=mode,
+                        colsum_out=cs, colsum_accumulate=True)
+            outs.append(((Y.view(torch.uint8), Yt.view(torch.uint8), aux, amax.max()), cs))
     finally:
         C.set_gemm_w4q8(-1)
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0][0], outs[1][0]):
         assert torch.equal(a, b)
+    if mode == 2:
+        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
 
 
 def test_gemm_f8_q_rejects_edge_shapes(dev):
