@@ -41,6 +41,7 @@ DDP checkpoints.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -55,8 +56,10 @@ DEFAULT_FIRST_BUCKET_MB = 4.0
 # alpha-beta model of one bucket's ring all-reduce on an 8 x MI355X node (RCCL over xGMI):
 #   t(M) = ALPHA + 2 (W - 1) / W * M / BUS
 # ALPHA: per-collective launch + protocol latency; BUS: the all-reduce's bus bandwidth with RCCL's
-# rings spread over the 7 point-to-point links (~153 GB/s each). Both overridable from a measured
-# bucket sweep (scripts/bucket_sweep.sh): MLT_DDP_ALPHA_US, MLT_DDP_BUS_GBPS.
+# rings spread over the 7 point-to-point links (~153 GB/s each). These are the model's priors: the
+# one-time re-plan fits both on the live process group (DistributedDataParallel._measure_alpha_beta:
+# timed all-reduces of two sizes, MAX over ranks); MLT_DDP_ALPHA_US / MLT_DDP_BUS_GBPS override the
+# fit (e.g. from scripts/bucket_sweep.sh), MLT_DDP_MEASURE_AB=0 keeps the priors.
 XGMI_ALPHA_US = 25.0
 XGMI_BUS_GBPS = 300.0
 MIN_BUCKET_MB, MAX_BUCKET_MB = 4.0, 128.0
@@ -319,6 +322,51 @@ class DistributedDataParallel(nn.Module):
         import time
         return time.perf_counter()
 
+    def _measure_alpha_beta(self) -> Optional[tuple]:
+        """Fit the alpha-beta model on this group's real wire: all-reduces of 64 KB (latency-bound) and
+        min(max(M, 4 MB), 64 MB) (bandwidth-bound) through the same path the buckets take (native
+        RCCL communicator or torch.distributed), each timed host-side around device syncs after
+        a warmup; the MAX over ranks is agreed so every rank plans alike. Returns (alpha_us,
+        bus_gbps), or None when the two points do not give a positive slope (then the priors stay)."""
+        import time
+        dev = self.flat.device
+        cuda = dev.type == "cuda"
+        dt = self.comm_dtype or self.flat.grad.dtype
+        esz = torch.empty((), dtype=dt).element_size()
+        small, large = 64 * 1024, int(min(max(self._grad_bytes, 4 * 2 ** 20), 64 * 2 ** 20))
+        buf = torch.zeros(large // esz, dtype=dt, device=dev)
+
+        def timed(nbytes: int, reps: int) -> float:
+            v = buf[:max(1, nbytes // esz)]
+
+            def once():
+                if self._ncomm is not None:
+                    self._ncomm.all_reduce(v, "avg")
+                else:
+                    dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.process_group)
+            once()
+            if cuda:
+                torch.cuda.synchronize(dev)
+            dist.barrier(group=self.process_group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                once()
+            if cuda:
+                torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) * 1e6 / reps
+
+        ts, tl = timed(small, 8), timed(large, 3)
+        del buf
+        t = torch.tensor([ts, tl], dtype=torch.float64, device=dev if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        ts, tl = (float(x) for x in t.tolist())
+        slope = (tl - ts) / (large - small)  # us per byte
+        if not slope > 0:
+            return None
+        bus = 2.0 * (self.world_size - 1) / self.world_size / (slope * 1e3)
+        alpha = max(ts - slope * small, 0.5 * ts)
+        return alpha, bus
+
     def _maybe_replan(self) -> None:
         """At the forward after the timed backward: agree the backward time (MAX over ranks, so
         every rank computes the same plan), then rebuild the buckets once from the alpha-beta model."""
@@ -335,9 +383,21 @@ class DistributedDataParallel(nn.Module):
         t = torch.tensor([ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
         ms = float(t.item())
-        cap, first = plan_buckets(self._grad_bytes, self.world_size, ms)
+        alpha = bus = None
+        ab = "model"
+        if "MLT_DDP_ALPHA_US" in os.environ or "MLT_DDP_BUS_GBPS" in os.environ:
+            ab = "env"
+        elif os.environ.get("MLT_DDP_MEASURE_AB", "1") != "0":
+            fit = self._measure_alpha_beta()
+            if fit is not None:
+                alpha, bus = fit
+                ab = "measured"
+        cap, first = plan_buckets(self._grad_bytes, self.world_size, ms, alpha_us=alpha, bus_gbps=bus)
         self.bucket_plan = {"cap_mb": cap, "first_mb": first, "source": "alpha-beta", "bwd_ms": round(ms, 4),
-                            "replans": 1}
+                            "replans": 1, "ab": ab,
+                            "alpha_us": round(alpha if alpha is not None else allreduce_us(0, self.world_size), 3),
+                            "bus_gbps": round(bus if bus is not None else float(
+                                os.environ.get("MLT_DDP_BUS_GBPS", XGMI_BUS_GBPS)), 3)}
         old = list(self._buckets)
         self._bucket_cap = int(cap * 2 ** 20)
         self._first_cap = int(first * 2 ** 20)

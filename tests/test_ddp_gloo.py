@@ -304,3 +304,40 @@ def test_ddp_autoplan_rebuckets_once_bitwise():
         assert f[0]["layouts"][0] == lay[2]
         for r in range(world):
             assert torch.equal(a[r]["params"], f[r]["params"])
+
+
+def _ab_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    for k in ("MLT_DDP_ALPHA_US", "MLT_DDP_BUS_GBPS", "MLT_DDP_MEASURE_AB"):
+        os.environ.pop(k, None)
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(5)
+    model = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(4)])
+    ddp = DistributedDataParallel(model)
+    g = torch.Generator().manual_seed(3 + rank)
+    for _ in range(3):
+        ddp(torch.randn(8, 64, generator=g)).pow(2).mean().backward()
+    torch.save({"plan": ddp.bucket_plan, "grad_bytes": ddp._grad_bytes}, os.path.join(out_dir, f"ab{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_replan_fits_alpha_beta_on_the_live_group():
+    """With no MLT_DDP_ALPHA_US / MLT_DDP_BUS_GBPS, the one-time re-plan fits the alpha-beta model on
+    the group's own wire (timed all-reduces of two sizes, MAX over ranks): every rank records the same
+    measured alpha / bus bandwidth, and the caps are the planner's for exactly those values."""
+    from ml_trainer_amd.parallel.ddp import plan_buckets
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ab_worker, args=(world, free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"ab{k}.pt"), weights_only=True) for k in range(world)]
+    plan = r[0]["plan"]
+    assert r[1]["plan"] == plan
+    assert plan["source"] == "alpha-beta" and plan["replans"] == 1
+    if plan["ab"] == "measured":  # (a noisy host can give a non-positive slope: then the priors stay)
+        assert plan["alpha_us"] > 0 and plan["bus_gbps"] > 0
+        cap, first = plan_buckets(r[0]["grad_bytes"], world, plan["bwd_ms"], alpha_us=plan["alpha_us"],
+                                  bus_gbps=plan["bus_gbps"])
+        assert abs(cap - plan["cap_mb"]) <= 1e-6 * max(1.0, cap) + 1e-3 and first <= cap
+    else:
+        assert plan["ab"] == "model"
