@@ -70,6 +70,33 @@ def _bert_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _bert_autoplan_worker(rank, world, port, out_dir):
+    dist_env(rank, world, port)
+    for k in ("MLT_DDP_ALPHA_US", "MLT_DDP_BUS_GBPS", "MLT_DDP_MEASURE_AB", "MLT_DDP_AUTOPLAN"):
+        os.environ.pop(k, None)
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(rank)
+    m = BertClassifier(bert_config("bert-tiny")).to(dev)
+    ddp = DistributedDataParallel(m)  # no caps: timed backward + alpha-beta fit on the live group
+    opt = FusedAdamW(m.parameters(), lr=1e-3, flat=ddp.flat)
+    g = torch.Generator().manual_seed(11 + rank)
+    ids = torch.randint(5, 1000, (2, 128), generator=g).to(dev)
+    y = torch.randint(0, 2, (2,), generator=g).to(dev)
+    for _ in range(4):
+        opt.zero_grad(set_to_none=False)
+        F.cross_entropy(ddp(ids), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    torch.save({"p": ddp.flat.data.cpu(), "plan": ddp.bucket_plan}, os.path.join(out_dir, f"b{rank}.pt"))
+    dist.destroy_process_group()
+
+
 def _run(fn, world=2, *extra):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(fn, args=(world, free_port(), d, *extra), nprocs=world, join=True)
@@ -80,6 +107,16 @@ def test_lenet_engine_two_ranks_stay_in_sync():
     r = _run(_lenet_worker)
     assert torch.equal(r[0]["p"], r[1]["p"])
     assert r[0]["ctrl"].tolist() == [6, 6]
+
+
+def test_bert_ddp_autoplan_fits_alpha_beta_on_gpu():
+    """DDP on device gradients with no caps: the one-time re-plan times the backward, fits alpha /
+    bus bandwidth with all-reduces of device buffers through the bucket path, and every rank ends
+    with the same plan and identical weights."""
+    r = _run(_bert_autoplan_worker)
+    assert r[0]["plan"] == r[1]["plan"]
+    assert r[0]["plan"]["source"] == "alpha-beta" and r[0]["plan"]["ab"] in ("measured", "model")
+    assert torch.equal(r[0]["p"], r[1]["p"])
 
 
 def test_bert_ddp_direct_grads_two_ranks():
