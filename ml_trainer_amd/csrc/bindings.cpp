@@ -660,6 +660,7 @@ void ln_fwd(Tensor X, Tensor gamma, Tensor beta, Tensor Y, Tensor mean, Tensor r
 }
 
 int64_t ln_partial_blocks(int64_t rows) { return ln_bwd_partial_blocks(rows); }
+int64_t ln_q8_partial_blocks(int64_t rows) { return ln_bwd_q8_partial_blocks(rows); }
 
 // dxsum (optional): column sums of DX (bias gradient of the producing linear layer), accumulated
 // into when dxsum_acc.
@@ -690,6 +691,38 @@ void ln_bwd(Tensor DY, Tensor X, Tensor gamma, Tensor mean, Tensor rstd, Tensor 
   launch_ln_bwd(bf16_ptr(DY), bf16_ptr(X), gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                 (uint16_t*)DX.data_ptr(), part.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
                 rows, (int)D, accumulate ? 1 : 0, dr, dxs, dxsum_acc ? 1 : 0, cur_stream());
+}
+
+// ln_bwd + the e5m2 quantisation of DX for the fp8 GEMMs that take it as dY (Y8, YT8, amax with
+// the consumer's scale); dxsum is required. Returns false (nothing launched) when the shape is
+// not covered (rows % 32, D not 768 / 1024): the caller then runs ln_bwd + fp8_cast_transpose.
+bool ln_bwd_q8(Tensor DY, Tensor X, Tensor gamma, Tensor mean, Tensor rstd, Tensor DX, Tensor part, Tensor dgamma,
+               Tensor dbeta, bool accumulate, Tensor dxsum, bool dxsum_acc, Tensor Y8, Tensor YT8, Tensor scale,
+               Tensor amax) {
+  const int64_t D = gamma.numel(), rows = X.numel() / std::max<int64_t>(D, 1);
+  if (rows % 32 || (D != 768 && D != 1024)) return false;
+  check_bf16_2d(X, "X", rows, D);
+  check_bf16_2d(DY, "DY", rows, D);
+  check_bf16_2d(DX, "DX", rows, D);
+  check_dev(gamma, "gamma", at::kFloat, D);
+  check_dev(mean, "mean", at::kFloat, rows, 4);
+  check_dev(rstd, "rstd", at::kFloat, rows, 4);
+  check_dev(part, "part", at::kFloat, (int64_t)ln_bwd_q8_partial_blocks(rows) * 3 * D);
+  check_dev(dgamma, "dgamma", at::kFloat, D);
+  check_dev(dbeta, "dbeta", at::kFloat, D);
+  check_dev(dxsum, "dxsum", at::kFloat, D);
+  TORCH_CHECK(Y8.is_cuda() && Y8.is_contiguous() && is_fp8_storage(Y8) && Y8.numel() == rows * D &&
+                  reinterpret_cast<uintptr_t>(Y8.data_ptr()) % 16 == 0, "Y8: contiguous fp8 [rows, D]");
+  TORCH_CHECK(YT8.is_cuda() && YT8.is_contiguous() && is_fp8_storage(YT8) && YT8.numel() == rows * D &&
+                  reinterpret_cast<uintptr_t>(YT8.data_ptr()) % 16 == 0, "YT8: contiguous fp8 [D, rows]");
+  check_dev(scale, "scale", at::kFloat, 1, 4);
+  check_dev(amax, "amax", at::kFloat, kAmaxSlots * kAmaxStride, 4);
+  return launch_ln_bwd_q8(bf16_ptr(DY), bf16_ptr(X), gamma.data_ptr<float>(), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), (uint16_t*)DX.data_ptr(), part.data_ptr<float>(),
+                          dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, (int)D, accumulate ? 1 : 0,
+                          dxsum.data_ptr<float>(), dxsum_acc ? 1 : 0, reinterpret_cast<uint8_t*>(Y8.data_ptr()),
+                          reinterpret_cast<uint8_t*>(YT8.data_ptr()), scale.data_ptr<float>(),
+                          amax.data_ptr<float>(), cur_stream());
 }
 
 void embed_fwd(Tensor ids, c10::optional<Tensor> tt, Tensor Ww, Tensor Wp, Tensor Wt, Tensor out, int64_t S) {
@@ -1416,6 +1449,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cfg") = -1, py::arg("splits") = 0, py::arg("accumulate") = false);
   m.def("colsum", &colsum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);
   m.def("ln_fwd", &ln_fwd);
+  m.def("ln_q8_partial_blocks", &ln_q8_partial_blocks, py::arg("rows"));
+  m.def("ln_bwd_q8", &ln_bwd_q8, py::arg("DY"), py::arg("X"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("DX"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accumulate"), py::arg("dxsum"),
+        py::arg("dxsum_acc"), py::arg("Y8"), py::arg("YT8"), py::arg("scale"), py::arg("amax"));
   m.def("ln_bwd", &ln_bwd, py::arg("DY"), py::arg("X"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("DX"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accumulate") = false,
         py::arg("dres") = py::none(), py::arg("dxsum") = py::none(), py::arg("dxsum_acc") = false);

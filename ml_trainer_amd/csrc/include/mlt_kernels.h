@@ -289,6 +289,13 @@ int ln_bwd_partial_blocks(int64_t rows);
 void launch_ln_bwd(const uint16_t* DY, const uint16_t* X, const float* gamma, const float* mean, const float* rstd,
                    uint16_t* DX, float* part, float* dgamma, float* dbeta, int64_t rows, int D, int accumulate,
                    const uint16_t* DRES, float* dxsum, int dxsum_acc, hipStream_t st);
+// LayerNorm backward that also quantises dx (the next fp8 GEMM's dY): e5m2 Y8 [rows, D] + YT8
+// [D, rows] with scale *qscale, amax into qamax's slots; dxsum required. false: shape not covered
+int ln_bwd_q8_partial_blocks(int64_t rows);
+bool launch_ln_bwd_q8(const uint16_t* DY, const uint16_t* X, const float* gamma, const float* mean, const float* rstd,
+                      uint16_t* DX, float* part, float* dgamma, float* dbeta, int64_t rows, int D, int accumulate,
+                      float* dxsum, int dxsum_acc, uint8_t* Y8, uint8_t* YT8, const float* qscale, float* qamax,
+                      hipStream_t st);
 void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const uint16_t* Ww, const uint16_t* Wp,
                       const uint16_t* Wt, uint16_t* out, int64_t rows, int S, int D, int64_t vocab, int ntype,
                       hipStream_t st);

@@ -7,8 +7,11 @@
 // dbeta accumulated per lane across a grid-stride set of rows, reduced across the
 // block's waves in LDS, written as per-block partials and summed over blocks by a
 // second kernel in a fixed order (deterministic, no atomics).
+#include <algorithm>
+
 #include "mlt_common.h"
 #include "mlt_kernels.h"
+#include "mlt_fp8.h"
 
 namespace mlt {
 
@@ -176,6 +179,135 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     part[(int64_t)blockIdx.x * NS * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
+// fp8 variant (DXS, no DRES): the same dx, plus dx quantised for the fp8 GEMMs that consume it as
+// their dY -- e5m2 Y [rows, D] and Y^T [D, rows] with the consumer's delayed scale, and its amax.
+// Each quantised value is the bf16-rounded dx times the scale, the value the separate cast-transpose
+// would read back, so Y / Y^T / amax equal ln_bwd + fp8_cast_transpose bit for bit (the dgamma /
+// dbeta / column-sum partials cover other row sets, so those agree to fp32 rounding). A block
+// walks 32-row chunks (wave w: rows 8 w .. 8 w + 7); the chunk's fp8 rows are staged in LDS and
+// leave as 32-byte Y^T row pieces, 4 columns per thread.
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_q8_kernel(const uint16_t* __restrict__ DY, const uint16_t* __restrict__ X,
+                                                        const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, uint16_t* __restrict__ DX,
+                                                        float* __restrict__ part, int64_t rows, uint8_t* __restrict__ Y8,
+                                                        uint8_t* __restrict__ YT8, const float* __restrict__ qscale,
+                                                        float* __restrict__ qamax) {
+  constexpr int D = VPL * 256, E = VPL * 4, NS = 3, CR = 32;
+  constexpr int RED_BYTES = 4 * NS * D * 4, TILE_BYTES = CR * D;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[RED_BYTES > TILE_BYTES ? RED_BYTES : TILE_BYTES];
+  uint8_t* tile = smem;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float qs = *qscale;
+  float dg[E], db[E], g[E], dxs[E], mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < E; ++i) dg[i] = db[i] = dxs[i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const float4 gv = *reinterpret_cast<const float4*>(gamma + 4 * (lane + 64 * v));
+    g[4 * v] = gv.x, g[4 * v + 1] = gv.y, g[4 * v + 2] = gv.z, g[4 * v + 3] = gv.w;
+  }
+  const int64_t nchunks = rows / CR;
+  ushort4 nx[VPL], ndy[VPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    const int64_t rr = r < rows ? r : rows - 1;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      nx[v] = reinterpret_cast<const ushort4*>(X + rr * D)[lane + 64 * v];
+      ndy[v] = reinterpret_cast<const ushort4*>(DY + rr * D)[lane + 64 * v];
+    }
+    nmu = mean[rr];
+    nrs = rstd[rr];
+  };
+  int64_t ch = blockIdx.x;
+  if (ch < nchunks) fetch(ch * CR + wid * 8);
+  for (; ch < nchunks; ch += gridDim.x) {
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+      const int rl = wid * 8 + k;
+      const int64_t row = ch * CR + rl;
+      float x[E], dy[E];
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        x[4 * v + 0] = bf16_to_f32(nx[v].x), x[4 * v + 1] = bf16_to_f32(nx[v].y);
+        x[4 * v + 2] = bf16_to_f32(nx[v].z), x[4 * v + 3] = bf16_to_f32(nx[v].w);
+        dy[4 * v + 0] = bf16_to_f32(ndy[v].x), dy[4 * v + 1] = bf16_to_f32(ndy[v].y);
+        dy[4 * v + 2] = bf16_to_f32(ndy[v].z), dy[4 * v + 3] = bf16_to_f32(ndy[v].w);
+      }
+      const float mu = nmu, rs = nrs;
+      fetch(k < 7 ? row + 1 : (ch + gridDim.x) * CR + wid * 8);  // past the end: re-reads the last row
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        const float xh = (x[i] - mu) * rs;
+        x[i] = xh;
+        const float t = dy[i] * g[i];
+        s1 += t;
+        s2 += t * xh;
+        dg[i] += dy[i] * xh;
+        db[i] += dy[i];
+      }
+      s1 = wave_sum(s1) * (1.f / D);
+      s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = 4 * v + q;
+          o[q] = bf16_to_f32(f32_to_bf16(rs * (dy[i] * g[i] - s1 - x[i] * s2)));  // dx as stored
+          dxs[i] += o[q];
+          mx = fmaxf(mx, fabsf(o[q]));
+        }
+        ushort4 u;
+        u.x = f32_to_bf16(o[0]), u.y = f32_to_bf16(o[1]), u.z = f32_to_bf16(o[2]), u.w = f32_to_bf16(o[3]);
+        reinterpret_cast<ushort4*>(DX + row * D)[lane + 64 * v] = u;
+        const uint32_t q8 = pack4_fp8<1>(o[0] * qs, o[1] * qs, o[2] * qs, o[3] * qs);
+        *reinterpret_cast<uint32_t*>(Y8 + row * D + 4 * (lane + 64 * v)) = q8;
+        *reinterpret_cast<uint32_t*>(tile + rl * D + 4 * (lane + 64 * v)) = q8;
+      }
+    }
+    __syncthreads();
+    // Y^T: thread t takes columns 4 t .. 4 t + 3, the chunk's 32 rows -> 32 bytes per column
+    if (threadIdx.x * 4 < D) {
+      const int c4 = threadIdx.x * 4;
+      uint32_t d[CR];
+#pragma unroll
+      for (int r = 0; r < CR; ++r) d[r] = *reinterpret_cast<const uint32_t*>(tile + r * D + c4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int sh = 8 * j;
+        uint32_t w[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          w[q] = ((d[4 * q] >> sh) & 0xffu) | (((d[4 * q + 1] >> sh) & 0xffu) << 8) |
+                 (((d[4 * q + 2] >> sh) & 0xffu) << 16) | (((d[4 * q + 3] >> sh) & 0xffu) << 24);
+        uint4* tp = reinterpret_cast<uint4*>(YT8 + (int64_t)(c4 + j) * rows + ch * CR);
+        tp[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        tp[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      }
+    }
+    __syncthreads();  // the tile is rewritten by the next chunk
+  }
+  float* red = reinterpret_cast<float*>(smem);  // [4][NS * D], after the last chunk's barrier
+#pragma unroll
+  for (int v = 0; v < VPL; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * (lane + 64 * v) + q;
+      red[wid * NS * D + c] = dg[4 * v + q];
+      red[wid * NS * D + D + c] = db[4 * v + q];
+      red[wid * NS * D + 2 * D + c] = dxs[4 * v + q];
+    }
+  mx = wave_max(mx);
+  if (lane == 0) atomic_max_pos(qamax, mx);
+  __syncthreads();
+  for (int c = threadIdx.x; c < NS * D; c += 256)
+    part[(int64_t)blockIdx.x * NS * D + c] =
+        (red[c] + red[NS * D + c]) + (red[2 * NS * D + c] + red[3 * NS * D + c]);
+}
+
 // out_k[c] (+)= sum_r part[r][k*seg + c]: wave = 4 columns, lanes stride the rows, xor tree (fixed order)
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int64_t ld, int W,
                                                           int seg, SegOut o, int accmask) {
@@ -232,6 +364,10 @@ void launch_ln_fwd(const uint16_t* X, const float* gamma, const float* beta, uin
   }
 }
 
+// the fp8 variant's grid: 32-row chunks, up to 3 blocks per CU (48 KB of LDS each) -- its chunk
+// barriers leave 2 blocks per CU short of latency hiding
+int ln_bwd_q8_partial_blocks(int64_t rows) { return (int)std::min<int64_t>(std::max<int64_t>(rows / 32, 1), 768); }
+
 int ln_bwd_partial_blocks(int64_t rows) {
   int64_t nb = (rows + 3) / 4;
   return (int)(nb < 512 ? nb : 512);
@@ -258,6 +394,24 @@ void launch_ln_bwd(const uint16_t* DY, const uint16_t* X, const float* gamma, co
 #undef MLT_LN_BWD
   SegOut o{{dgamma, dbeta, dxsum}};
   launch_reduce_rows(part, nb, (dxsum ? 3 : 2) * D, (dxsum ? 3 : 2) * D, D, o, (accumulate ? 3 : 0) | (dxsum_acc ? 4 : 0), st);
+}
+
+bool launch_ln_bwd_q8(const uint16_t* DY, const uint16_t* X, const float* gamma, const float* mean, const float* rstd,
+                      uint16_t* DX, float* part, float* dgamma, float* dbeta, int64_t rows, int D, int accumulate,
+                      float* dxsum, int dxsum_acc, uint8_t* Y8, uint8_t* YT8, const float* qscale, float* qamax,
+                      hipStream_t st) {
+  if (rows <= 0 || rows % 32 || (D != 768 && D != 1024)) return false;
+  const int nb = ln_bwd_q8_partial_blocks(rows);
+  const dim3 grid(nb), block(256);
+  if (D == 1024)
+    hipLaunchKernelGGL(ln_bwd_q8_kernel<4>, grid, block, 0, st, DY, X, gamma, mean, rstd, DX, part, rows, Y8, YT8, qscale,
+                       qamax);
+  else
+    hipLaunchKernelGGL(ln_bwd_q8_kernel<3>, grid, block, 0, st, DY, X, gamma, mean, rstd, DX, part, rows, Y8, YT8, qscale,
+                       qamax);
+  SegOut o{{dgamma, dbeta, dxsum}};
+  launch_reduce_rows(part, nb, 3 * D, 3 * D, D, o, (accumulate ? 3 : 0) | (dxsum_acc ? 4 : 0), st);
+  return true;
 }
 
 // ---------------------------------------------------------------------------

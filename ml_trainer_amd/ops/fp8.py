@@ -205,6 +205,12 @@ class Fp8Linear:
             if st.dyt is None or st.dy8 is None or st.dy8[0] != dy.data_ptr():
                 raise RuntimeError("fp8 wgrad: pre-quantised dY without its transpose")
             dy8t, st.dyt = st.dyt, None
+        elif st.dyt is not None and st.dy8 is not None and st.dy8[0] == dy.data_ptr():
+            # bf16 dY whose e5m2 copy and transpose the producing LayerNorm backward already wrote
+            # (ln_bwd_q8, which also reduced the bias gradient)
+            if db_out is not None:
+                raise RuntimeError("fp8 wgrad: LayerNorm-quantised dY carries its bias gradient already")
+            dy8t, st.dyt = st.dyt, None
         else:
             dy8, dy8t = ctx.cast_t(dy, st.mdy, E5M2, colsum_out=db_out, colsum_accumulate=db_acc)
             st.dy8 = (dy.data_ptr(), dy8)
@@ -231,6 +237,30 @@ class Fp8Linear:
                   mode=2 if aux is not None else 0, res=res)
         return out
 
+
+    # ---- LayerNorm backward quantises the out-proj / FFN2 dY ------------------------------------
+    # In the post-LN blocks the LayerNorm backward's dx is the dY of the out-projection (attention
+    # block) and of FFN2: C.ln_bwd_q8 writes its e5m2 copy and transpose with that weight's dY scale
+    # (plus amax, plus the bias gradient it already reduced), so the separate cast-transpose pass
+    # over dx disappears. Opt-in (MLT_FP8_LN_Q=1): measured slower -- 508 us per call against 308 us
+    # of ln_bwd + 184 us of cast-transpose at 262144 x 1024, fp8 `large` 1,250 vs 1,254 samples/s
+    # (profiles/r5/fp8_ln_bwd_q8_ab.jsonl). Its 32-row chunk barriers and the transposed pass leave
+    # the loads idle; the two streaming kernels it replaces each run near 5.2-5.8 TB/s.
+    fuse_ln = os.environ.get("MLT_FP8_LN_Q", "0") == "1"
+
+    @staticmethod
+    def ln_bwd_q_state(w, x):
+        """(state, context) when a LayerNorm backward may quantise ``w``'s dY: its e5m2 scale exists
+        and the forward left X^T (of ``x``) for w's fp8 weight gradient; else None."""
+        if not Fp8Linear.fuse_ln:
+            return None
+        st = getattr(w, "_mlt_f8", None)
+        if st is None or st.xt is None or st.xt[0] != x.data_ptr() or not _fp8_wgrad_ok(x, w):
+            return None
+        ctx = context(x.device)
+        if not ctx._ready[st.mdy]:
+            return None
+        return st, ctx
 
     # ---- FFN fusion: the GEMM epilogues quantise for the next GEMM ------------------------------
     # FFN1's forward epilogue writes GELU(.) as FFN2's e4m3 input and its transpose (FFN2's wgrad

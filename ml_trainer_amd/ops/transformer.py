@@ -277,8 +277,10 @@ def _ln_fwd(x, gamma, beta, eps):
     return y, (x, gamma, mean, rstd)
 
 
-def _ln_bwd(saved, beta, dy, G, dxsum_param=None):
+def _ln_bwd(saved, beta, dy, G, dxsum_param=None, q8=None):
     """LayerNorm backward; with ``dxsum_param`` also the column sums of dx (= that bias's grad).
+    ``q8`` = (impl, w, x): dx is the dY of linear ``w`` (input ``x``); an fp8 ``impl`` that can take
+    it pre-quantised gets dx's e5m2 copy and transpose from this same kernel (C.ln_bwd_q8).
     Returns (dx, dgamma|None, dbeta|None, dbias|None)."""
     C = require_native()
     x, gamma, mean, rstd = saved
@@ -307,6 +309,21 @@ def _ln_bwd(saved, beta, dy, G, dxsum_param=None):
             dxs_t, dxs_acc = so, True
         else:
             dxs = dxs_t = torch.empty(D, dtype=torch.float32, device=dev)
+    if want and q8 is not None and hasattr(q8[0], "ln_bwd_q_state"):
+        r = q8[0].ln_bwd_q_state(q8[1], q8[2])
+        if r is not None:
+            st, fctx = r
+            rows = x.shape[0]
+            nq = C.ln_q8_partial_blocks(rows) * 3 * D
+            if part.numel() < nq:
+                part = torch.empty(nq, dtype=torch.float32, device=dev)
+            y8 = torch.empty(rows, D, dtype=torch.float8_e5m2, device=dev)
+            yt8 = torch.empty(D, rows, dtype=torch.float8_e5m2, device=dev)
+            if C.ln_bwd_q8(dy, x, gamma, mean, rstd, dx, part, dg_t, db_t, acc, dxs_t, dxs_acc, y8, yt8,
+                           fctx.scale[st.mdy:st.mdy + 1], fctx.amax[st.mdy]):
+                st.dy8 = (dx.data_ptr(), y8)
+                st.dyt = yt8
+                return dx, dg, db, dxs
     C.ln_bwd(dy, x, gamma, mean, rstd, dx, part, dg_t, db_t, acc, None, dxsum=dxs_t, dxsum_acc=dxs_acc)
     return dx, dg, db, dxs
 
@@ -382,7 +399,8 @@ class _AttentionLNBlock(torch.autograd.Function):
     def backward(ctx, dy):
         t = ctx.saved_tensors
         G = _Grads()
-        da, dg, db, dbo = _ln_bwd(t[4:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3])
+        da, dg, db, dbo = _ln_bwd(t[4:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3],
+                                  q8=(ctx.impl, ctx.params[2], t[2]))  # da = out-proj dY (input attn)
         dx, dwqkv, dbqkv, dwo, dbo = _attn_bwd(t[:4], ctx.params, ctx.lens, *ctx.dims, da, G, dbo=dbo,
                                                impl=ctx.impl)
         G.done()
@@ -404,7 +422,8 @@ class _FFNLNBlock(torch.autograd.Function):
     def backward(ctx, dy):
         t = ctx.saved_tensors
         G = _Grads()
-        df, dg, db, db2 = _ln_bwd(t[3:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3])
+        df, dg, db, db2 = _ln_bwd(t[3:], ctx.beta, dy.contiguous().to(torch.bfloat16), G, dxsum_param=ctx.params[3],
+                                  q8=(ctx.impl, ctx.params[2], t[2]))  # df = FFN2 dY (input a)
         dx, dw1, db1, dw2, db2 = _ffn_bwd(t[:3], ctx.params, df, G, db2=db2, impl=ctx.impl)
         G.done()
         return dx, dw1, db1, dw2, db2, dg, db, None, None

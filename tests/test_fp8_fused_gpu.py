@@ -180,3 +180,93 @@ def test_fused_ffn_matches_unfused(dev):
     for name, a, b in zip(("x", "w1", "b1", "w2", "b2"), gf, gu):
         r = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert r < 6e-2, (name, r)
+
+
+@pytest.mark.parametrize("D", [768, 1024])
+@pytest.mark.parametrize("rows", [480, 4096, 20480])  # 20480: > 512 blocks x 32 rows, chunks grid-stride
+def test_ln_bwd_q8_matches_ln_bwd_plus_cast(dev, D, rows):
+    """C.ln_bwd_q8 (LayerNorm backward + e5m2 quantisation of dx): Y8, Y8^T and amax are bit for bit
+    the separate cast-transpose of the dx it wrote; that dx matches C.ln_bwd to one bf16 rounding
+    (the two kernels' fp32 expressions may contract differently), dgamma / dbeta / column sums of dx
+    to fp32 rounding (partials over other row sets)."""
+    C = require_native()
+    g = torch.Generator().manual_seed(rows + D)
+    x = (torch.randn(rows, D, generator=g) * 2 + 0.3).to(torch.bfloat16).to(dev)
+    dy = (torch.randn(rows, D, generator=g) * 0.01).to(torch.bfloat16).to(dev)
+    gamma = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(D, generator=g)).to(dev)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    C.ln_fwd(x, gamma, beta, torch.empty_like(x), mean, rstd, 1e-12)
+    scale = torch.tensor([512.0], device=dev)
+    nb = max(C.ln_partial_blocks(rows), C.ln_q8_partial_blocks(rows))
+
+    def bufs():
+        return (torch.empty_like(x), torch.empty(nb * 3 * D, device=dev), *(torch.empty(D, device=dev) for _ in range(3)),
+                torch.empty(rows, D, dtype=torch.float8_e5m2, device=dev),
+                torch.empty(D, rows, dtype=torch.float8_e5m2, device=dev), torch.zeros(C.FP8_AMAX_SLOTS, device=dev))
+    dx, part, dg, db, dxs, y8, yt8, amax = bufs()
+    assert C.ln_bwd_q8(dy, x, gamma, mean, rstd, dx, part, dg, db, False, dxs, False, y8, yt8, scale, amax)
+    rx, rpart, rdg, rdb, rdxs, ry8, ryt8, ramax = bufs()
+    C.ln_bwd(dy, x, gamma, mean, rstd, rx, rpart, rdg, rdb, False, None, dxsum=rdxs, dxsum_acc=False)
+    C.fp8_cast_transpose(dx, ry8, ryt8, scale, ramax, 1)  # the cast of the fused kernel's own dx
+    assert torch.equal(y8.view(torch.uint8), ry8.view(torch.uint8))
+    assert torch.equal(yt8.view(torch.uint8), ryt8.view(torch.uint8))
+    assert float(amax.max()) == float(ramax.max())
+    torch.testing.assert_close(dx.float(), rx.float(), rtol=8e-3, atol=1e-6)
+    assert (dx != rx).float().mean().item() < 0.01
+    for a, b in ((dg, rdg), (db, rdb), (dxs, rdxs)):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * b.abs().max().item())
+
+
+def test_ln_bwd_q8_declines_uncovered_shapes(dev):
+    C = require_native()
+    D, rows = 1024, 100  # rows % 32 != 0: the caller keeps ln_bwd + the separate cast
+    t = lambda *s, dt=torch.bfloat16: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+    f8 = torch.float8_e5m2
+    assert not C.ln_bwd_q8(t(rows, D), t(rows, D), t(D, dt=torch.float32), t(rows, dt=torch.float32),
+                           t(rows, dt=torch.float32), t(rows, D), t(C.ln_q8_partial_blocks(rows) * 3 * D, dt=torch.float32),
+                           t(D, dt=torch.float32), t(D, dt=torch.float32), False, t(D, dt=torch.float32), False,
+                           t(rows, D, dt=f8), t(D, rows, dt=f8), t(1, dt=torch.float32) + 1,
+                           t(C.FP8_AMAX_SLOTS, dt=torch.float32))
+
+
+def test_fp8_bert_ln_quantised_dy_matches_separate_cast(dev, monkeypatch):
+    """A 768-wide fp8 encoder layer trained a few steps with the LayerNorm backward quantising the
+    out-proj / FFN2 dY (Fp8Linear.fuse_ln, opt-in) vs the separate cast-transpose: the fused kernel runs
+    (2 calls per layer per step once the scales exist) and the losses agree to fp32 rounding of the
+    LayerNorm partial sums."""
+    import torch.nn.functional as F
+    from ml_trainer_amd.models.bert import BertClassifier, bert_config
+    from ml_trainer_amd.ops import fp8 as fp8mod
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    C = require_native()
+    calls = []
+    real = C.ln_bwd_q8
+
+    def counting(*a):
+        r = real(*a)
+        calls.append(r)
+        return r
+    monkeypatch.setattr(C, "ln_bwd_q8", counting)
+    cfg = bert_config("bert-tiny", fp8=True, hidden=768, heads=12, intermediate=3072, layers=1)
+    ids = torch.randint(5, 1000, (4, 128), device=dev)
+    y = torch.randint(0, 2, (4,), device=dev)
+    losses = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(fp8mod.Fp8Linear, "fuse_ln", fuse)
+        fp8mod._CTX.clear()  # fresh delayed-scaling state for each run
+        torch.manual_seed(0)
+        m = BertClassifier(cfg).to(dev)
+        opt = FusedAdamW(m.parameters(), lr=1e-4)
+        ls = []
+        for _ in range(4):
+            opt.zero_grad()
+            loss = F.cross_entropy(m(ids), y)
+            loss.backward()
+            opt.step()
+            ls.append(float(loss))
+        losses[fuse] = ls
+    assert calls and all(calls), calls
+    for a, b in zip(losses[True], losses[False]):
+        assert abs(a - b) <= 2e-3 * abs(b) + 1e-4, losses
