@@ -1,7 +1,7 @@
 # ln_bwd_q8 with 768 blocks: fp8-fused tests, fp8 `large` A/B (MLT_FP8_LN_Q=1/0), kernel time
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r5ak
+O=gpurun_out/${R5_OUT:-r5ak}
 mkdir -p $O
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fp8_fused_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
