@@ -1287,7 +1287,15 @@ void launch_gemm_f8_q(int fmt_a, int fmt_b, const uint8_t* A, const uint8_t* B, 
     const char* v = getenv("MLT_GEMM_W4Q8");
     g_w4q8 = (v && atoi(v) == 0) ? 0 : 1;
   }
-  if (g_w4q8 && launch_gemm_w4_f8_q(fmt_a, A, B, Y, M, N, K, lda, ldb, ldy, e, kGroupM, st)) return;
+  // raster group width 4 (MLT_GEMM_W4Q8_GROUP_M overrides): in isolation 2 M-tiles ran the GELU
+  // form faster (1.91 vs 1.96 ms) and the dGELU form slower (2.08 vs 1.97), 8 / 16 lost on both;
+  // in the fp8 `large` step GELU at 2 lost (1,254 vs 1,263 samples/s) -- profiles/r5/fp8_q8_w4_group_m.jsonl
+  static const int q_group_m = [] {
+    const char* v = getenv("MLT_GEMM_W4Q8_GROUP_M");
+    return v ? atoi(v) : 0;
+  }();
+  const int gm_q = q_group_m > 0 ? q_group_m : kGroupM;
+  if (g_w4q8 && launch_gemm_w4_f8_q(fmt_a, A, B, Y, M, N, K, lda, ldb, ldy, e, gm_q, st)) return;
   GemmPlan p{5, 1, K / 128, 0, 0};
   if (fmt_a == 0 && fmt_b == 0)
     launch_pp<false, false, uint8_t, 0, 0>(p, A, B, Y, M, N, K, lda, ldb, ldy, e, nullptr, nullptr, st);
