@@ -52,10 +52,24 @@ def _torch_paths():
     return inc, lib, abi
 
 
-def _headers():
-    # (+ generated kernel fragments included by the .hip files, e.g. gemm_w4_loop.inc)
-    return (glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.inc")) +
-            glob.glob(os.path.join(CSRC, "kernels", "*.inc")))
+def _deps(src: str, seen=None):
+    """The in-tree files ``src`` includes, transitively (``#include "..."`` resolved against its own
+    directory and csrc/include): a kernel file rebuilds only when something it includes changed."""
+    import re
+    seen = set() if seen is None else seen
+    try:
+        text = open(src).read()
+    except OSError:
+        return seen
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        for d in (os.path.dirname(src), os.path.join(CSRC, "include")):
+            f = os.path.join(d, name)
+            if os.path.exists(f):
+                if f not in seen:
+                    seen.add(f)
+                    _deps(f, seen)
+                break
+    return seen
 
 
 def _newer(src: str, obj: str, deps, cmd=None) -> bool:
@@ -99,9 +113,8 @@ def _run(cmd):
 FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"],
               "lenet_mfma.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
                                  "-mllvm", "-amdgpu-kernarg-preload-count=12"]}
-# translation units split off a kernel file for parallel compilation share its flags
-# (lenet_mfma_1l_w*.hip: the one-launch step's per-world-size instantiations of lenet_mfma.inc)
-FILE_ALIASES = {"lenet_mfma_1l_": "lenet_mfma.hip"}
+# translation units split off a kernel file for parallel compilation share its flags ({prefix: file})
+FILE_ALIASES = {"lenet_mfma_dp": "lenet_mfma.hip"}  # (lenet_mfma_dp.hip, lenet_mfma_dpw<W>.hip)
 
 
 def _flag_key(name: str) -> str:
@@ -129,7 +142,6 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
     opt = ["-O0", "-g"] if debug else ["-O3"]
     if debug:
         common.append("-DMLT_DEBUG=1")
-    hdrs = _headers()
 
     kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     host_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")) +
@@ -144,7 +156,7 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
         cmd = [HIPCC, "-c", s, "-o", o, f"--offload-arch={ARCH}", *opt, *common, "-munsafe-fp-atomics",
                "-Wno-unused-result", *FILE_FLAGS.get(_flag_key(os.path.basename(s)), []),
                *(extra_flags or {}).get(_flag_key(os.path.basename(s)), [])]
-        if force or _newer(s, o, hdrs, cmd):
+        if force or _newer(s, o, _deps(s), cmd):
             jobs_list.append(cmd)
             if os.path.basename(s) in AGPR_GUARDED:  # + its device asm for the AGPR-spill guard
                 asm_checks.append(os.path.join(BUILD_DIR, os.path.basename(s) + ".s"))
@@ -157,7 +169,7 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
         cmd = [HIPCC, "-c", s, "-o", o, *opt, *common, "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                f"-I{pyinc}", f"-I{pybind11.get_include()}", *[f"-isystem{i}" for i in tinc], "-I/opt/rocm/include",
                "-Wno-deprecated-declarations", "-Wno-unused-result"]
-        if force or _newer(s, o, hdrs, cmd):
+        if force or _newer(s, o, _deps(s), cmd):
             jobs_list.append(cmd)
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -1050,16 +1050,12 @@ class LeNetEngine {
       P_.prep = get("prep", at::kByte, B * 8192).data_ptr<uint8_t>();
       P_.pmeta = get("pmeta", at::kLong, B * 4).data_ptr<int64_t>();
     }
-    if (bufs.contains("sync"))
-      sync_ = reinterpret_cast<unsigned long long*>(get("sync", at::kLong, 64).data_ptr<int64_t>());
-    if (const char* e = std::getenv("MLT_LENET_ONELAUNCH")) onelaunch_ = std::string(e) == "1";
     A_ = LeNetAug{};
     O_ = LeNetOpt{};
   }
 
   void set_aug(Tensor data, Tensor perm, Tensor ctrl, Tensor dtargets, int64_t seed, int pad, int flip,
                int batch_stride, std::vector<double> mean, std::vector<double> stdv) {
-    flush();
     A_ = make_aug(data, perm, ctrl, seed, pad, flip, batch_stride, mean, stdv);
     TORCH_CHECK(A_.ctrl != nullptr, "ctrl required");
     check_dev(dtargets, "dtargets", at::kLong, A_.n);
@@ -1069,14 +1065,12 @@ class LeNetEngine {
   }
 
   void clear_aug() {
-    flush();
     A_.data = nullptr;
     P_.dtargets = nullptr;
     graphs_.clear();
   }
 
   void set_ctrl(Tensor ctrl) {
-    flush();
     check_dev(ctrl, "ctrl", at::kLong, 2, 8);
     A_.ctrl = ctrl.data_ptr<int64_t>();
     ctrl_keep_ = ctrl;
@@ -1090,7 +1084,6 @@ class LeNetEngine {
     const int64_t n = p.numel();
     check_dev(p, "p", at::kFloat, n);
     check_dev(g, "g", at::kFloat, n);
-    flush();  // a pending update belongs to the old optimizer
     O_ = LeNetOpt{};
     master_ = p;
     pack_ver_ = -1;
@@ -1132,7 +1125,6 @@ class LeNetEngine {
   // flat gradient (AVG) over the native communicator and apply the flat optimizer with lr /
   // step read from device memory -- all inside the same stream (and graph).
   void set_xgmi(py::object x) {
-    flush();  // a pending update finishes on the transport it was started with
     if (x.is_none()) {
       xgmi_ = nullptr;
       xgmi_keep_ = py::none();
@@ -1145,7 +1137,6 @@ class LeNetEngine {
   }
 
   void set_comm(py::object comm) {
-    flush();
     if (comm.is_none()) {
       comm_ = nullptr;
       comm_keep_ = py::none();
@@ -1159,7 +1150,6 @@ class LeNetEngine {
   // 0: fp32 kernels (lenet.hip); 1: bf16 MFMA training step (lenet_mfma.hip; evaluation stays fp32)
   void set_precision(int p) {
     TORCH_CHECK(p == 0 || p == 1, "precision: 0 (fp32) or 1 (bf16)");
-    flush();
     if (p == 1) TORCH_CHECK(P_.shadow && P_.wimg && P_.stage2 && P_.meta2 && P_.metaN && P_.stepinfo,
                             "bf16 engine buffers missing");
     prec_ = p;
@@ -1170,7 +1160,6 @@ class LeNetEngine {
   // bf16 + xGMI: the two-launch data-parallel step (default) or the four-launch one (per-sample
   // kernel, batch reductions, xGMI all-reduce, apply) kept for A/B and bitwise cross-checks
   void set_fused_dp(bool f) {
-    flush();
     fused_dp_ = f;
     graphs_.clear();
   }
@@ -1194,72 +1183,27 @@ class LeNetEngine {
   void run(int mode, int B) {
     check_mode(mode, B);
     const bool mf = prec_ == 1 && (mode & LENET_BWD);
-    const bool one = onelaunch(mode, B);
-    if (!one) flush();
     if (mf) launch_lenet_mfma_pack(cfg_, P_, O_, cur_stream());  // shadow / fragment image from the masters
-    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream(), mf, fused_dp_, one ? sync_ : nullptr);
-    if (one) pending_b_ = B;
+    launch_step(cfg_, mode, B, P_, A_, O_, comm_, xgmi_, cur_stream(), mf, fused_dp_);
   }
 
-  // With onelaunch_ the bf16 step runs as ONE launch per step (lenet_mfma_1l_*: this step's samples +
-  // the previous step's update) when the whole grid fits the chip and the step is the fused
-  // single-rank one or the xGMI-fused data-parallel one at W in {1, 2, 4, 8}
-  bool onelaunch(int mode, int B) const {
-    if (!onelaunch_ || !sync_ || prec_ != 1 || !(mode & LENET_BWD) || !A_.ctrl || !P_.stepinfo) return false;
-    const bool local = (mode & LENET_OPT) && !(mode & LENET_REDUCE);
-    const bool dp = (mode & LENET_REDUCE) && xgmi_ && fused_dp_;
-    if (!local && !dp) return false;
-    return lenet_mfma_onelaunch_ok(cfg_, B, dp ? xgmi_->world() : 0);
-  }
-  // Finish the pending update of the last one-launch step (its reductions / exchange / optimizer
-  // update run at the head of the NEXT step's launch): before any host access to the parameters,
-  // gradients or stats, and before anything launches that is not a one-launch step.
-  void flush() {
-    if (pending_b_ <= 0) return;
-    const int B = pending_b_;
-    pending_b_ = 0;
-    if (xgmi_ && fused_dp_) {
-      const XgmiFused X = xgmi_->fused_view();
-      launch_lenet_mfma_flush(cfg_, B, P_, O_, &X, cur_stream());
-    } else {
-      launch_lenet_mfma_flush(cfg_, B, P_, O_, nullptr, cur_stream());
-    }
-  }
-  int pending() const { return pending_b_; }
   // transport bring-up: the batch reductions of the current activation / slab buffers into the
-  // flat gradient (exchange = the fused xGMI exchange too), no update; stats and stepinfo[3] as a
-  // flush leaves them. Nothing may be pending.
+  // flat gradient (exchange = the fused xGMI exchange too), no update, step counters untouched
   void reduce_only(int B, bool exchange) {
-    TORCH_CHECK(pending_b_ == 0, "reduce_only: flush the pending step first");
     TORCH_CHECK(prec_ == 1 && P_.stepinfo && O_.g, "reduce_only: bf16 engine with set_opt");
     TORCH_CHECK(B > 0 && B <= max_b_, "reduce_only: batch");
     if (exchange) {
       TORCH_CHECK(xgmi_ != nullptr, "reduce_only: no xGMI transport");
       const XgmiFused X = xgmi_->fused_view();
-      launch_lenet_mfma_flush(cfg_, B, P_, O_, &X, cur_stream(), false);
+      launch_lenet_mfma_reduce(cfg_, B, P_, O_, &X, cur_stream());
     } else {
-      launch_lenet_mfma_flush(cfg_, B, P_, O_, nullptr, cur_stream(), false);
+      launch_lenet_mfma_reduce(cfg_, B, P_, O_, nullptr, cur_stream());
     }
   }
-  void set_onelaunch(bool on) {
-    flush();
-    onelaunch_ = on;
-    graphs_.clear();
-  }
-  bool onelaunch_enabled() const { return onelaunch_; }
 
   static void launch_step(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                           Communicator* comm, XgmiAllReduce* xgmi, hipStream_t s, bool mfma = false,
-                          bool fused_dp = false, unsigned long long* one_sync = nullptr) {
-    if (one_sync) {  // one launch: this step + the previous step's update (+ exchange)
-      if (mode & LENET_REDUCE) {
-        const XgmiFused X = xgmi->fused_view();
-        launch_lenet_mfma_onelaunch(cfg, mode & ~LENET_REDUCE, B, P, A, O, one_sync, &X, s);
-      } else {
-        launch_lenet_mfma_onelaunch(cfg, mode, B, P, A, O, one_sync, nullptr, s);
-      }
-      return;
-    }
+                          bool fused_dp = false) {
     if (mfma && (mode & LENET_REDUCE) && xgmi && fused_dp) {
       // bf16 data-parallel step in two launches: the per-sample kernel, then batch reductions +
       // xGMI exchange + rank-ordered sum + update (lenet_mwx; world size 1 = loopback)
@@ -1312,12 +1256,10 @@ class LeNetEngine {
     XgmiAllReduce* xgmi = xgmi_;
     const bool mf = prec_ == 1 && (mode & LENET_BWD);
     const bool fused = fused_dp_;
-    unsigned long long* one = onelaunch(mode, B) ? sync_ : nullptr;
     g->capture([&](hipStream_t s) {
       // (no pack here: replay() re-packs when the host changed the masters since the last pack)
-      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf, fused, one);
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg, mode, B, P, A, O, comm, xgmi, s, mf, fused);
     });
-    one_graphs_[key(mode, B, nsteps)] = one != nullptr;
     graphs_[key(mode, B, nsteps)] = std::move(g);
   }
 
@@ -1331,7 +1273,6 @@ class LeNetEngine {
     if (prec_ != 1 || !master_.defined()) return;
     const int64_t v = master_._version();
     if (v == pack_ver_) return;
-    flush();
     launch_lenet_mfma_pack(cfg_, P_, O_, cur_stream());
     pack_ver_ = v;
   }
@@ -1340,11 +1281,8 @@ class LeNetEngine {
   void replay(int mode, int B, int nsteps) {
     auto it = graphs_.find(key(mode, B, nsteps));
     TORCH_CHECK(it != graphs_.end(), "no captured graph for this (mode, B, nsteps)");
-    const bool one = one_graphs_[key(mode, B, nsteps)];
-    if (!one) flush();
     if (mode & LENET_BWD) sync_shadow();
     it->second->launch(cur_stream());
-    if (one) pending_b_ = B;
   }
 
   size_t graph_nodes(int mode, int B, int nsteps) const {
@@ -1370,12 +1308,6 @@ class LeNetEngine {
   XgmiAllReduce* xgmi_ = nullptr;
   py::object xgmi_keep_ = py::none();
   std::map<int64_t, std::unique_ptr<HipGraph>> graphs_;
-  std::map<int64_t, bool> one_graphs_;  // graph key -> holds one-launch steps
-  unsigned long long* sync_ = nullptr;  // one-launch hand-off words ("sync" buffer)
-  // the one-launch step is opt-in (MLT_LENET_ONELAUNCH=1 / .onelaunch): measured slower than the
-  // two-launch step with input prep (profiles/r5/lenet_onelaunch_*.jsonl)
-  bool onelaunch_ = false;
-  int pending_b_ = 0;  // batch of the step whose update is still pending (0: none)
   int prec_ = 0;
   bool fused_dp_ = true;
   int64_t shadow_n_ = 0;
@@ -1514,10 +1446,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("has_graph", &LeNetEngine::has_graph)
       .def("replay", &LeNetEngine::replay)
       .def("invalidate_shadow", &LeNetEngine::invalidate_shadow)
-      .def("flush", &LeNetEngine::flush)
       .def("reduce_only", &LeNetEngine::reduce_only, py::arg("B"), py::arg("exchange"))
-      .def_property_readonly("pending", &LeNetEngine::pending)
-      .def_property("onelaunch", &LeNetEngine::onelaunch_enabled, &LeNetEngine::set_onelaunch)
       .def("graph_nodes", &LeNetEngine::graph_nodes)
       .def("reset_graphs", &LeNetEngine::reset_graphs);
   m.attr("LENET_FWD") = (int)LENET_FWD;

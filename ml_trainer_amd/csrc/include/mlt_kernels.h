@@ -119,18 +119,9 @@ struct XgmiFused;
 void launch_lenet_mfma_dp(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                           const XgmiFused& X, hipStream_t stream);
 int lenet_mfma_wimg_elems();
-// ONE-launch bf16 step (lenet_mfma.hip, lenet_ms<D, UM >= 0>): update blocks finish the PREVIOUS step
-// (batch reductions, X != nullptr: the fused xGMI exchange over X->W ranks, optimizer update) while
-// the sample blocks of this step load / augment their images; an in-launch hand-off (write-through
-// stores, arrival counter in `sync`) precedes the first weight read. This step's own update stays
-// pending (stepinfo[3] = B) until the next one-launch step or launch_lenet_mfma_flush.
-// sync: >= 64 zero-initialised uint64 words owned by the engine (epoch, two arrival counters, error).
-bool lenet_mfma_onelaunch_ok(int cfg, int B, int W);  // W = 0: no exchange
-void launch_lenet_mfma_onelaunch(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
-                                 unsigned long long* sync, const XgmiFused* X, hipStream_t stream);
-// opt = false: batch reductions (+ the exchange when X) into O.g only, no update (self-test / timing)
-void launch_lenet_mfma_flush(int cfg, int B, const LeNetPtrs& P, const LeNetOpt& O, const XgmiFused* X,
-                             hipStream_t stream, bool opt = true);
+// batch reductions (+ the exchange when X) into O.g only, no update (transport self-test / timing)
+void launch_lenet_mfma_reduce(int cfg, int B, const LeNetPtrs& P, const LeNetOpt& O, const XgmiFused* X,
+                              hipStream_t stream);
 int64_t lenet_mfma_xch_granules(int cfg);  // granules per parity the fused exchange needs
 // shadow + wimg from the fp32 masters (O.p)
 void launch_lenet_mfma_pack(int cfg, const LeNetPtrs& P, const LeNetOpt& O, hipStream_t stream);

@@ -122,9 +122,6 @@ def lenet_buffers(cfg_id: int, B: int, device) -> Dict[str, torch.Tensor]:
         # prep blocks (bf16 pixels, 8 KB per sample) and their (step, position, target) tags
         "prep": torch.zeros(B * 8192, dtype=torch.uint8, device=device),
         "pmeta": torch.full((B * 4,), -1, dtype=torch.int64, device=device),
-        # one-launch bf16 step: in-launch hand-off words (launch epoch, two arrival counters on their
-        # own cache lines, error word) -- zeroed once, kept consistent by the kernel itself
-        "sync": torch.zeros(64, dtype=torch.int64, device=device),
     }
     return bufs
 

@@ -4,24 +4,21 @@ One training step of the reference hot loop (``src/trainer.py:180-197``:
 zero_grad -> H2D -> forward -> CE -> loss.item() -> backward (DDP all-reduce)
 -> optimizer.step -> metric) becomes:
 
-* W = 1, bf16 (the bench default, BASELINE configs 2/3): ONE kernel per step
-  (csrc/kernels/lenet_mfma.inc, ``lenet_ms<D, 0>``): one CU per sample (on-GPU
-  RandomCrop/HFlip/Normalize of the HBM-resident uint8 image, conv/fc forward on
-  MFMA, softmax-CE, the whole backward of the sample) plus ~20 update blocks that
-  finish the PREVIOUS step meanwhile (batch reductions in sample order, on-device
-  loss/accuracy sums, the fused optimizer update of the fp32 masters + bf16 shadow)
-  and hand the new weights to the sample blocks inside the launch, while those
-  load and augment their images. So the last step's update is pending until the
-  next step or ``flush()`` (every host access path flushes). Grids too large for
-  one co-resident launch (batch > 220) use the two-launch step (``lenet_ms`` +
-  ``lenet_mw``); fp32 (the reference dtype): four kernels (csrc/kernels/lenet.hip).
-  Either way captured as a multi-step hipGraph, so the host submits one graph per
-  ``steps_per_graph`` steps and never synchronises inside an epoch (B12: no
-  ``loss.item()``, no sklearn round trip);
-* W > 1, bf16 over xGMI: still ONE kernel per step (W in {1, 2, 4, 8}; otherwise
-  ``lenet_ms`` + ``lenet_mwx``): the update blocks publish their batch-reduced
-  gradient slice into an IPC-shared region, pull the peers' slices over xGMI, sum
-  them in rank order and apply the update ("xgmi-fused"; W = 1 loopback for timing);
+* W = 1, bf16 (the bench default, BASELINE configs 2/3): TWO kernels per step
+  (csrc/kernels/lenet_mfma.inc). ``lenet_ms``: one CU per sample (the sample's
+  input -- RandomCrop/HFlip/Normalize of the HBM-resident uint8 image, prepared by
+  the previous step's second kernel -- conv/fc forward on MFMA, softmax-CE, the
+  whole backward of the sample, its weight-gradient slab). ``lenet_mw``: the batch
+  reductions in sample order, the on-device loss/accuracy sums, the fused optimizer
+  update of the fp32 masters + bf16 shadow + fragment images, and (on CUs those
+  leave idle) the NEXT step's augmented inputs. fp32 (the reference dtype): four
+  kernels (csrc/kernels/lenet.hip). Either way captured as a multi-step hipGraph, so
+  the host submits one graph per ``steps_per_graph`` steps and never synchronises
+  inside an epoch (B12: no ``loss.item()``, no sklearn round trip);
+* W > 1, bf16 over xGMI: still two kernels per step (``lenet_ms`` + ``lenet_mwx``):
+  the reduction blocks publish their batch-reduced gradient slice into an IPC-shared
+  region, pull the peers' slices over xGMI, sum them in rank order and apply the
+  update ("xgmi-fused"; W = 1 loopback for timing);
 * W > 1 otherwise: the step's kernels -> all-reduce (AVG) of the flat gradient
   (one 248 KB bucket; latency-bound, so a single collective: the one-/two-shot
   xGMI kernels or RCCL, chosen by a timed vote) -> optimizer launch reading
@@ -29,6 +26,9 @@ zero_grad -> H2D -> forward -> CE -> loss.item() -> backward (DDP all-reduce)
   multi-step hipGraphs contain compute, collective and update of every step;
   without a native transport (MLT_NATIVE_COMM=0) each step is graph(kernels) +
   torch.distributed all-reduce + optimizer launch.
+
+(A one-launch form -- the update folded into the next step's launch -- was measured
+slower in round 5, profiles/r5/lenet_onelaunch_ab.jsonl, and deleted.)
 
 The device step counter ``ctrl`` (``[global_step, step_in_epoch]``) drives
 batch selection from the epoch permutation, the augmentation RNG, the lr table
@@ -162,9 +162,9 @@ class LeNetStepEngine:
             return
         fused_ok = False
         W = dist.get_world_size(process_group)
-        # (the fused exchange kernels, and their self-test / flush path, exist for 2, 4 and 8 ranks)
+        # (the fused exchange is offered for 2, 4 and 8 ranks)
         if x is not None and self.precision == "bf16" and fused_dp_enabled() and W in (2, 4, 8):
-            # bf16 over xGMI: the exchange can run inside the step (one launch per step), but only
+            # bf16 over xGMI: the exchange can run inside the step (two launches per step), but only
             # once its own protocol -- not just the one-/two-shot kernels -- proved bit-exact on
             # this fabric, on every rank
             fused_ok = self._fused_selftest(x, process_group)
@@ -396,21 +396,10 @@ class LeNetStepEngine:
         for k in ("stage_meta", "meta2", "metaN", "pmeta"):
             self.bufs[k].fill_(-1)
 
-    def flush(self) -> None:
-        """Apply the pending update of the last one-launch step (no-op when nothing is pending).
-        Data-parallel (xgmi-fused): a collective -- every rank flushes at the same point."""
-        self.eng.flush()
-
-    def sync_error(self) -> int:
-        """Nonzero when a one-launch step's in-launch wait gave up (a block never became resident)."""
-        return int(self.bufs["sync"][48].item())
-
     def reset_stats(self) -> None:
-        self.flush()  # the pending step's loss / accuracy belong to the previous window
         self.stats.zero_()
 
     def read_stats(self, n_batches: int):
-        self.flush()
         s = self.stats.cpu().tolist()
         return s[0] / max(n_batches, 1), s[1] / max(n_batches, 1)
 
@@ -496,16 +485,8 @@ class LeNetStepEngine:
             self.eng.invalidate_shadow()
             self._host_sig = sig
 
-    def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8,
-                    flush: bool = True) -> None:
-        """Run ``n`` full training steps of batch ``B`` from the device dataset. ``flush=False``
-        leaves the last one-launch step's update pending (it runs at the head of the next step's
-        launch): for loops that read nothing in between (bench, Trainer epochs)."""
-        self._train_steps(B, n, use_graph, steps_per_graph)
-        if flush:
-            self.flush()
-
-    def _train_steps(self, B: int, n: int, use_graph: bool, steps_per_graph: int) -> None:
+    def train_steps(self, B: int, n: int = 1, use_graph: bool = True, steps_per_graph: int = 8) -> None:
+        """Run ``n`` full training steps of batch ``B`` from the device dataset."""
         mode = self._train_mode()
         self._note_host_writes()
         if self.fused or self.in_graph_collective:
@@ -553,7 +534,6 @@ class LeNetStepEngine:
     def eval_steps(self, B: int, n: int = 1) -> None:
         """Forward + CE + accuracy only (validation / test)."""
         C = self.C
-        self.flush()
         for _ in range(n):
             self.eng.run(C.LENET_FWD | C.LENET_CE, B)
             self._advance_eval()
@@ -584,4 +564,3 @@ class LeNetStepEngine:
                     self._dist_step(mode, B, use_graph=False)
         else:
             self.eng.run(C.LENET_FWD | C.LENET_CE, B)
-        self.flush()  # callers read the gradient / parameters right after

@@ -13,8 +13,9 @@ Under that surface (MI355X-first):
 
 * **fused step engine** -- for the reference LeNet on a GPU the whole training
   step (augmentation, fwd, CE, metrics, bwd, optimizer) runs natively: bf16 as
-  ONE kernel per step (the previous step's update folded into the next step's
-  launch), fp32 as four, replayed as multi-step hipGraphs
+  TWO kernels per step (the per-sample chain ``lenet_ms``, then the batch
+  reductions + optimizer update + next-step input prep ``lenet_mw``), fp32 as
+  four, replayed as multi-step hipGraphs
   (``models/lenet_engine.py``): no per-step host syncs (fix B12), no H2D copies
   (HBM-resident dataset);
 * **generic path** -- any ``nn.Module``: native fused optimizer over a flat
@@ -448,15 +449,15 @@ class Trainer:
         done = 0
         while done < full:
             k = min(spg, full - done)
-            eng.train_steps(B, k, use_graph=self.opts.use_graph, steps_per_graph=spg, flush=False)
+            eng.train_steps(B, k, use_graph=self.opts.use_graph, steps_per_graph=spg)
             done += k
             bar.update(k)
             if self._watchdog:
                 self._watchdog.beat()
         if last:
-            eng.train_steps(last, 1, use_graph=self.opts.use_graph, steps_per_graph=1, flush=False)
+            eng.train_steps(last, 1, use_graph=self.opts.use_graph, steps_per_graph=1)
             bar.update(1)
-        loss, acc = eng.read_stats(n)  # the ONE host sync of the epoch (flushes the pending update)
+        loss, acc = eng.read_stats(n)  # the ONE host sync of the epoch
         eng.check_transport()
         bar.set_postfix(loss=loss, metric=acc if self.metric else None)
         bar.close()

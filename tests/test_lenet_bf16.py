@@ -372,79 +372,3 @@ def test_bf16_training_quality_matches_fp32(tmp_path):
     for e, (l32, l16) in enumerate(zip(h["fp32"]["train_loss"], h["bf16"]["train_loss"])):
         assert abs(l32 - l16) <= max(0.05 * l32, 0.05), (e, h["fp32"]["train_loss"], h["bf16"]["train_loss"])
 
-
-def _train_run(onelaunch, opt, B, steps, spg, seed=13, N=300, dp=False, flush_each=True):
-    """Train on the toy set with the one-launch step on or off; returns (params, grads, stats, ctrl)."""
-    from ml_trainer_amd.parallel.comm import create_xgmi_loopback
-    dev = torch.device("cuda", 0)
-    data, targets = _toy_data(N, 5)
-    m = _mk("default", seed).to(dev)
-    eng, flat = _engine(m, opt, max_batch=max(B, 8), lr=1e-3)
-    eng.eng.onelaunch = onelaunch
-    if dp:
-        eng.use_transport(xgmi=create_xgmi_loopback(flat.numel, dev))
-    eng.set_dataset(data, targets, batch_size=B)
-    for ep in range(2):
-        eng.start_epoch(torch.randperm(N, generator=torch.Generator().manual_seed(ep)))
-        full, last = divmod(N, B)
-        done = 0
-        while done < full:
-            k = min(spg, full - done)
-            eng.train_steps(B, k, use_graph=True, steps_per_graph=spg, flush=flush_each)
-            done += k
-        if last:
-            eng.train_steps(last, 1, use_graph=True, steps_per_graph=1, flush=flush_each)
-    eng.flush()
-    torch.cuda.synchronize()
-    assert eng.sync_error() == 0
-    return eng, (flat.data.clone(), flat.grad.clone(), eng.stats.clone(), eng.ctrl.clone())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt", ["sgd", "adamw", "adagrad"])
-@pytest.mark.parametrize("B", [32, 5])
-def test_bf16_onelaunch_matches_two_launch(dev, opt, B):
-    """The one-launch step (this step's sample blocks + the previous step's update blocks, weights
-    handed over inside the launch) == the two-launch step (lenet_ms -> lenet_mw), bit for bit, over
-    two epochs with partial last batches (the pending update changes batch size) and graphs whose
-    steps run with and without a flush between them; one kernel per captured step."""
-    e1, one = _train_run(True, opt, B, 0, 4, flush_each=False)
-    _, two = _train_run(False, opt, B, 0, 4)
-    for a, b in zip(one, two):
-        assert torch.equal(a, b)
-    mode = e1._train_mode()
-    assert e1.eng.graph_nodes(mode, B, 4) == 4
-
-
-@pytest.mark.gpu
-def test_bf16_onelaunch_pending_update(dev):
-    """flush=False leaves exactly the last step's update pending: the masters then equal those one
-    step behind; flush() applies it; reading stats flushes by itself."""
-    data, targets = _toy_data(256, 3)
-    res = {}
-    for n in (3, 4):
-        m = _mk("default", 31).to(dev)
-        eng, flat = _engine(m, "sgd", max_batch=32, lr=1e-2)
-        eng.eng.onelaunch = True
-        eng.set_dataset(data, targets, batch_size=32)
-        eng.start_epoch(torch.arange(256))
-        eng.train_steps(32, n, use_graph=True, steps_per_graph=n, flush=(n == 3))
-        torch.cuda.synchronize()
-        res[n] = (eng, flat, flat.data.clone())
-    eng4, flat4, pend = res[4]
-    assert eng4.eng.pending == 32
-    assert torch.equal(pend, res[3][2])  # step 4's update not applied yet
-    eng4.read_stats(4)                   # flushes
-    assert eng4.eng.pending == 0
-    assert not torch.equal(flat4.data, res[3][2])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("B", [32, 4])
-def test_bf16_onelaunch_dp_loopback_matches_two_launch(dev, B):
-    """The xGMI-fused data-parallel step against the loopback transport: one launch == the two-launch
-    lenet_ms -> lenet_mwx step, bitwise (granule tags on the shared per-block launch counters)."""
-    _, one = _train_run(True, "adamw", B, 0, 3, N=128, dp=True, flush_each=False)
-    _, two = _train_run(False, "adamw", B, 0, 3, N=128, dp=True)
-    for a, b in zip(one, two):
-        assert torch.equal(a, b)

@@ -230,8 +230,8 @@ def test_xgmi_allreduce_three_four_eight_ranks_one_gpu(world, algo):
 
 def _fused_dp_worker(rank, world, port, out_dir):
     """bf16 LeNet data-parallel step over xGMI: the two-launch step (exchange folded into the batch-
-    reduction kernel), the opt-in one-launch step (exchange in update blocks beside the next step's
-    samples) vs the four-launch step (reduction, one-shot all-reduce, apply)."""
+    reduction kernel) and its two-phase form vs the four-launch step (reduction, one-shot all-reduce,
+    apply)."""
     dist_env(rank, world, port)
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
@@ -248,13 +248,12 @@ def _fused_dp_worker(rank, world, port, out_dir):
     N = 64 * world
     data = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, generator=gd)
     targets = torch.randint(0, 10, (N,), generator=gd)
-    for variant, fused, one in (("1", True, False), ("0", False, False), ("one", True, True), ("two", True, False)):
+    for variant, fused in (("1", True), ("0", False), ("two", True)):
         torch.manual_seed(0)
         m = MLModel().to(dev)
         flat = FlatParams(m.parameters())
         opt = build_optimizer("adamw", m.parameters(), lr=1e-3, weight_decay=0.01, flat=flat)
         eng = LeNetStepEngine(m, flat, max_batch=8, optimizer=opt, world_size=world, precision="bf16")
-        eng.eng.onelaunch = one
         xe = create_xgmi_allreduce(None, flat.numel, dev, allow_gloo=True)
         assert xe is not None
         xe.algo = 0
@@ -278,18 +277,16 @@ def _fused_dp_worker(rank, world, port, out_dir):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_lenet_bf16_fused_dp_matches_four_launch(world):
-    """Two launches per data-parallel step (and one with the opt-in one-launch step; and the exchange's
-    two-phase form), bitwise equal to the four-launch step and identical on every rank (W = 8: the
+    """Two launches per data-parallel step (and the exchange's two-phase form), bitwise equal to the four-launch step and identical on every rank (W = 8: the
     node's size, as 8 processes on the box's one GPU)."""
     r = _run(_fused_dp_worker, world)
     assert len(r) == world
     for d in r:
-        assert d["err1"] == 0 and d["err0"] == 0 and d["errone"] == 0 and d["errtwo"] == 0
+        assert d["err1"] == 0 and d["err0"] == 0 and d["errtwo"] == 0
         assert torch.equal(d["p1"], d["p0"]) and torch.equal(d["g1"], d["g0"])
         assert torch.equal(d["ptwo"], d["p0"]) and torch.equal(d["gtwo"], d["g0"])
         assert d["nodestwo"] == 6
-        assert torch.equal(d["pone"], d["p0"]) and torch.equal(d["gone"], d["g0"])
-        assert (d["nodesone"], d["nodes1"], d["nodes0"]) == (3, 6, 12)  # 1 / 2 / 4 kernels per step
+        assert (d["nodes1"], d["nodes0"]) == (6, 12)  # 2 / 4 kernels per step
         assert torch.equal(d["p1"], r[0]["p1"])
 
 
