@@ -21,7 +21,13 @@ struct RegionLayout {
   size_t flags, t1, t2, f1, f2, fg, fr, fe, bytes;
 };
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
-static int64_t fused_cap(int64_t cap) { return cap > XgmiAllReduce::kFusedGranules ? cap : XgmiAllReduce::kFusedGranules; }
+// granules per parity half of the fused step's region, a multiple of 32 (256 B): the halves and the
+// two-phase reduced array then sit back to back with no align256 padding between them, the layout
+// fused_view() hands to the kernels (fr = fg + 2 cap)
+static int64_t fused_cap(int64_t cap) {
+  const int64_t c = cap > XgmiAllReduce::kFusedGranules ? cap : XgmiAllReduce::kFusedGranules;
+  return (c + 31) & ~(int64_t)31;
+}
 static RegionLayout region_layout(int64_t cap, int world, int blocks, int64_t slot) {
   RegionLayout L;
   const size_t fl = (size_t)2 * blocks * world * sizeof(uint64_t), tb = (size_t)2 * world * slot * sizeof(float);

@@ -121,9 +121,12 @@ class DistributedDataParallel(nn.Module):
         by the alpha-beta model (:func:`plan_buckets`). ``auto_plan`` (default: on when neither
         caps nor a hint are given, W > 1, overlap mode; MLT_DDP_AUTOPLAN=0 turns it off): the
         second synchronised backward is timed (first gradient hook -> last gradient; device
-        events on GPU), the MAX over ranks is agreed at the next forward, and the buckets are
-        rebuilt ONCE from the alpha-beta model with that time (``bucket_plan["source"]`` =
-        "alpha-beta", ``"bwd_ms"`` the agreed time)."""
+        events on GPU); at the end of that backward, once its collectives are waited for, the
+        MAX over ranks is agreed and the buckets are rebuilt ONCE from the alpha-beta model with
+        that time (``bucket_plan["source"]`` = "alpha-beta", ``"bwd_ms"`` the agreed time). The
+        re-plan is COLLECTIVE (a MAX all-reduce + the alpha-beta fit's timed all-reduces): it runs
+        at the end of the second synchronised backward, which every rank reaches in the same order
+        (``replan()`` runs it explicitly)."""
         super().__init__()
         if mode not in ("overlap", "manual"):
             raise ValueError("mode must be 'overlap' or 'manual'")
@@ -367,9 +370,15 @@ class DistributedDataParallel(nn.Module):
         alpha = max(ts - slope * small, 0.5 * ts)
         return alpha, bus
 
+    def replan(self) -> None:
+        """Collective: the one-time alpha-beta re-plan of the buckets, if the timed backward is done
+        and it has not run yet (every rank must call it at the same point)."""
+        self._maybe_replan()
+
     def _maybe_replan(self) -> None:
-        """At the forward after the timed backward: agree the backward time (MAX over ranks, so
-        every rank computes the same plan), then rebuild the buckets once from the alpha-beta model."""
+        """After the timed backward (collective, see __init__): agree the backward time (MAX over
+        ranks, so every rank computes the same plan), then rebuild the buckets once from the
+        alpha-beta model."""
         if not self._auto_plan or self._bwd_t is None or self._bwd_t[1] is None:
             return
         t0, t1 = self._bwd_t
@@ -398,13 +407,11 @@ class DistributedDataParallel(nn.Module):
                             "alpha_us": round(alpha if alpha is not None else allreduce_us(0, self.world_size), 3),
                             "bus_gbps": round(bus if bus is not None else float(
                                 os.environ.get("MLT_DDP_BUS_GBPS", XGMI_BUS_GBPS)), 3)}
-        old = list(self._buckets)
         self._bucket_cap = int(cap * 2 ** 20)
         self._first_cap = int(first * 2 ** 20)
         self._build_buckets()
-        if self._buckets != old:
-            self._pending = list(self._bucket_counts)
-            self._launched = [False] * len(self._buckets)
+        self._pending = list(self._bucket_counts)
+        self._launched = [False] * len(self._buckets)
 
     def _finish(self) -> None:
         if self._bwd_t is not None and self._bwd_t[1] is None:
@@ -426,6 +433,8 @@ class DistributedDataParallel(nn.Module):
                 del self._records[:-256]  # bounded history
                 self._step_rec = None
         self._wait_all()
+        if self._auto_plan and self._bwd_t is not None and self._bwd_t[1] is not None:
+            self._maybe_replan()  # collective: every rank finishes this synced backward in order
 
     def _wait_all(self) -> None:
         for w in self._works:
@@ -505,8 +514,6 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         if self.flat.rebind_params():
             pass  # something replaced p.data (e.g. .to()); views restored
-        if self._auto_plan and self._bwd_t is not None and self._bwd_t[1] is not None and torch.is_grad_enabled():
-            self._maybe_replan()
         if self.timing and self._comm_stream is not None and self.require_sync and torch.is_grad_enabled():
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()

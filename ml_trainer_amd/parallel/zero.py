@@ -180,9 +180,11 @@ class ZeroDataParallel(DistributedDataParallel):
             world, rank = int(comm.size), int(comm.rank)
         dev = next((p.device for p in module.parameters()), torch.device("cpu"))
         flat = FlatParams(module.parameters(), device=dev, reverse=True, align=16 * max(world, 1))
+        # auto_plan=False: the shard layout (chunks, sharded optimizer state) is fixed by the
+        # buckets built here, so the buckets must never be re-planned after construction
         super().__init__(module, process_group=process_group, bucket_cap_mb=bucket_cap_mb,
                          first_bucket_mb=first_bucket_mb, broadcast_parameters=broadcast_parameters,
-                         mode=mode, flat=flat, comm=comm)
+                         mode=mode, flat=flat, comm=comm, auto_plan=False)
         chunks, so = [], 0
         for s, e in self._buckets:
             assert (e - s) % world == 0, "bucket not divisible by the world size"
@@ -193,6 +195,11 @@ class ZeroDataParallel(DistributedDataParallel):
         self.shard.ncomm = self._ncomm
         self.shard.comm_stream = self._comm_stream
         self._gather_works: List = []
+
+    def _maybe_replan(self) -> None:
+        """Never: the shard chunks and the optimizer's sharded state follow the construction-time
+        buckets (a re-plan would reduce-scatter wrong ranges)."""
+        self._auto_plan = False
 
     # ---- gradients: reduce-scatter instead of all-reduce ------------------------------------
     def _reduce_bucket(self, bi: int, async_op: bool = True):

@@ -675,11 +675,15 @@ class Trainer:
     def _determinism_check(self) -> None:
         if not (self.opts.determinism_check and mdist.is_dist() and self.flat is not None):
             return
-        h = float(self.flat.data.double().sum().item())
-        lo = mdist.all_reduce_scalars([h], "min")[0]
-        hi = mdist.all_reduce_scalars([h], "max")[0]
+        # bitwise digest of the raw parameter words (two 31-bit position-weighted sums mod primes,
+        # utils/flat.py): a flipped bit or two swapped values on one rank changes it, where a float
+        # sum can miss both. Exact integers (< 2^31) compare exactly as the collective's float64.
+        from ml_trainer_amd.utils.flat import bitwise_digest
+        d = [float(v) for v in bitwise_digest(self.flat.data)]
+        lo = mdist.all_reduce_scalars(d, "min")
+        hi = mdist.all_reduce_scalars(d, "max")
         if lo != hi:
-            raise RuntimeError(f"parameters diverged across ranks (hash min {lo} != max {hi})")
+            raise RuntimeError(f"parameters diverged across ranks (digest min {lo} != max {hi})")
 
     def fit(self):
         logger.info("Start training..")

@@ -156,3 +156,34 @@ class FlatParams:
 
     def state_dict_views(self) -> List[torch.Tensor]:
         return [self.data[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
+
+
+_DIGEST_PRIMES = ((2 ** 31 - 1, 0x5BD1E995, 0x27D4EB2F), (2 ** 31 - 19, 0x9E3779B1, 0x165667B1))
+
+
+@torch.no_grad()
+def bitwise_digest(t: torch.Tensor, chunk: int = 1 << 24) -> Tuple[int, int]:
+    """Order- and bit-sensitive digest of a tensor's raw 32-bit words (SURVEY.md §5.2's cross-rank
+    parameter hash), computed on the tensor's own device: for each of two primes p,
+    ``sum_i (u_i + 1) * r_i mod p`` with u_i the i-th word as an unsigned 32-bit integer and
+    r_i = (A i + C) mod p distinct for every index. Flipping any bit of any word, or swapping two
+    different words, changes each digest (the difference is (u_i - u_j) * A * (j - i) != 0 mod p),
+    where a floating-point sum can miss both. Fixed order, integer arithmetic: bitwise
+    reproducible. Returns two integers < 2^31."""
+    flat = t.detach().reshape(-1)
+    if flat.element_size() != 4:
+        flat = flat.contiguous().view(torch.uint8)
+        pad = (-flat.numel()) % 4
+        if pad:
+            flat = torch.cat([flat, flat.new_zeros(pad)])
+    words = flat.contiguous().view(torch.int32)
+    out = []
+    for p, a, c in _DIGEST_PRIMES:
+        acc = 0
+        for s in range(0, words.numel(), chunk):
+            u = words[s:s + chunk].to(torch.int64) & 0xFFFFFFFF
+            idx = torch.arange(s, s + u.numel(), dtype=torch.int64, device=u.device)
+            r = (idx % p * a + c) % p                      # < 2^31
+            acc = (acc + int((((u % p) + 1) * r % p).sum().item())) % p  # products < 2^62, sums < 2^55
+        out.append(acc)
+    return out[0], out[1]

@@ -286,8 +286,9 @@ def _autoplan_worker(rank, world, port, out_dir, auto, cap, first):
 
 def test_ddp_autoplan_rebuckets_once_bitwise():
     """DDP without explicit caps times its second synchronised backward, agrees the MAX over ranks at
-    the next forward and rebuilds its buckets ONCE from the alpha-beta model (bucket_plan source
-    'alpha-beta'); training is bitwise equal to fixed caps of the same layout, on every rank."""
+    the end of that backward (collective, after its buckets were waited for) and rebuilds its buckets
+    ONCE from the alpha-beta model (bucket_plan source 'alpha-beta'); training is bitwise equal to
+    fixed caps of the same layout, on every rank."""
     world = 2
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_autoplan_worker, args=(world, free_port(), d, True, None, None), nprocs=world, join=True)
@@ -296,12 +297,12 @@ def test_ddp_autoplan_rebuckets_once_bitwise():
         assert plan["source"] == "alpha-beta" and plan["replans"] == 1 and plan["bwd_ms"] > 0
         assert a[1]["plan"] == plan  # agreed: the same plan on every rank
         lay = a[0]["layouts"]
-        assert lay[0] == lay[1] and lay[2] == lay[3] == lay[4]  # rebuilt once, before the 3rd step
-        assert lay[2] != lay[0] and len(lay[2]) > 1
+        assert lay[1] == lay[2] == lay[3] == lay[4]  # rebuilt once, at the end of the 2nd backward
+        assert lay[1] != lay[0] and len(lay[1]) > 1
         mp.spawn(_autoplan_worker, args=(world, free_port(), d, False, plan["cap_mb"], plan["first_mb"]),
                  nprocs=world, join=True)
         f = [torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True) for r in range(world)]
-        assert f[0]["layouts"][0] == lay[2]
+        assert f[0]["layouts"][0] == lay[1]
         for r in range(world):
             assert torch.equal(a[r]["params"], f[r]["params"])
 

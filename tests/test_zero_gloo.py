@@ -107,3 +107,66 @@ def test_trainer_zero1_tracks_ddp():
         for k in sd0:
             torch.testing.assert_close(sd1[k], sd0[k], rtol=1e-4, atol=1e-5)
         assert os.path.exists(os.path.join(d, "zero1", "trainer_state.pt"))
+
+
+def _zero_default_caps_worker(rank, world, port, out_dir):
+    """ZeroDataParallel(module) with NO bucket caps (as bench.py builds it) next to plain DDP with no
+    caps: DDP re-plans its buckets after the second backward (a cheap-wire model that changes the
+    layout), ZeRO must not -- its shard chunks and sharded optimizer state follow its construction-time
+    buckets."""
+    dist_env(rank, world, port)
+    os.environ["MLT_DDP_MIN_BUCKET_MB"] = "0.0001"
+    os.environ["MLT_DDP_ALPHA_US"] = "0.05"
+    os.environ["MLT_DDP_BUS_GBPS"] = "1000"
+    dist.init_process_group("gloo")
+    from ml_trainer_amd.ops.optim import FusedAdamW
+    from ml_trainer_amd.parallel.ddp import DistributedDataParallel
+    from ml_trainer_amd.parallel.zero import ZeroDataParallel
+    out = {}
+    for kind in ("ddp", "zero"):
+        torch.manual_seed(5)
+        m = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(6)])
+        if kind == "zero":
+            w = ZeroDataParallel(m)
+            opt = w.make_optimizer(FusedAdamW, lr=1e-2, weight_decay=0.01)
+            chunks0 = list(w.shard.chunks)
+        else:
+            w = DistributedDataParallel(m)
+            opt = FusedAdamW(m.parameters(), lr=1e-2, weight_decay=0.01, flat=w.flat)
+        layouts = []
+        g = torch.Generator().manual_seed(11 + rank)
+        for _ in range(5):
+            opt.zero_grad()
+            w(torch.randn(16, 64, generator=g)).pow(2).mean().backward()
+            opt.step()
+            layouts.append(list(w._buckets))
+        if kind == "zero":
+            w.wait_parameters()
+            out["zero_chunks_same"] = list(w.shard.chunks) == chunks0
+        out[kind] = w.flat.data.clone() if kind == "zero" else None
+        out[kind + "_layouts"] = layouts
+        out[kind + "_plan"] = dict(w.bucket_plan)
+        if kind == "ddp":
+            out["ddp_params"] = {n: p.detach().clone() for n, p in m.named_parameters()}
+        else:
+            out["zero_params"] = {n: p.detach().clone() for n, p in m.named_parameters()}
+    torch.save(out, os.path.join(out_dir, f"d{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_zero1_default_caps_never_replans():
+    """ZeroDataParallel without caps inherited DDP's one-time bucket re-plan, which
+    rebuilt the buckets under a fixed shard layout. It must keep its buckets, and train like DDP."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_zero_default_caps_worker, args=(world, free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"d{i}.pt"), weights_only=True) for i in range(world)]
+    for q in range(world):
+        lay = r[q]["ddp_layouts"]
+        assert r[q]["ddp_plan"]["replans"] == 1 and lay[1] != lay[0]  # DDP did re-plan (the test bites)
+        zl = r[q]["zero_layouts"]
+        assert all(x == zl[0] for x in zl) and r[q]["zero_chunks_same"]
+        assert r[q]["zero_plan"]["replans"] == 0
+        for n, p in r[q]["ddp_params"].items():
+            torch.testing.assert_close(r[q]["zero_params"][n], p, rtol=1e-5, atol=1e-6)
+    assert torch.equal(r[0]["zero"], r[1]["zero"])
