@@ -22,7 +22,7 @@ m = MLModel().to(dev)
 flat = FlatParams(m.parameters())
 opt = build_optimizer("sgd", m.parameters(), lr=1e-3, momentum=0.9, flat=flat)
 eng = LeNetStepEngine(m, flat, max_batch=B, optimizer=opt, precision="bf16")
-trace = torch.zeros(2048, dtype=torch.float32, device=dev)
+trace = torch.zeros(4096, dtype=torch.float32, device=dev)  # (slots 1024+: per-wave stamps)
 eng.bufs["trace"] = trace
 eng.eng = eng.C.LeNetEngine(m.cfg_id, B, eng.bufs)  # rebuild with the trace buffer bound
 eng.eng.set_ctrl(eng.ctrl)
@@ -39,8 +39,9 @@ C = eng.C
 idx = [0, 16, 17, 1, 2, 3, 18, 19, 4, 20, 21, 22, 5, 6, 7, 23, 24, 13]
 names = ["P0 loads issued (+ctrl/meta scalar wait)", "P1 zero fill + raw image to LDS", "P1 augment -> xh/xc",
          "P2 conv1", "P3 conv2", "P4 fc1 fwd", "P4 fc2 fwd", "P4 fc3 fwd + softmax-CE", "P6 fc3 dgrad",
-         "P7 fc2 dgrad", "-", "P8 fc1 dgrad", "P10 unpool", "P11 conv2 dgrad/wgrad", "P13 conv1 wgrad MFMAs",
-         "P13 partial sums + slab stores", "end-of-kernel stores"]
+         "P7 fc2 dgrad", "-", "P8 fc1 dgrad + unpool", "P10 w2d + dflat/dh1 stores", "P11 conv2 dgrad/wgrad",
+         "P13 conv1 wgrad MFMAs",
+         "P13 partial sums + slab stores", "end of kernel"]
 rows = []
 for rep in range(9):
     trace.zero_()  # a stamp the kernel skips this step (e.g. 17: no augmentation on a prep hit) stays 0
@@ -68,6 +69,17 @@ for k, n in enumerate(names):
     rec["phases_us"][n] = round(dm / ghz / 1e3, 3)
     assert dm >= 0, (n, d)
     print(f"  {n:28s} {dm:8d} cycles  {dm / ghz / 1e3:7.2f} us")
+# per-wave work-done stamps (slots 1024 + 16 k + w): cycles after the phase's opening stamp, median over reps
+wph = [("P2 conv1", 1, 0), ("P3 conv2 / fc3-fc2 dgrad fetch", 2, 1), ("P8 fc1 dgrad + unpool", 22, 2),
+       ("P11 conv2 dgrad/wgrad", 6, 3), ("P11 conv2 dgrad MFMAs (waves 0-6)", 6, 5), ("P13 conv1 wgrad", 7, 4)]
+rec["wave_done_cycles"] = {}
+for name, open_slot, k in wph:
+    per = []
+    for wv in range(16):
+        d = sorted(r[1024 + 16 * k + wv] - r[open_slot] for r in rows if r[1024 + 16 * k + wv] and r[open_slot])
+        per.append(d[len(d) // 2] if d else None)
+    rec["wave_done_cycles"][name] = per
+    print(f"  {name:32s} wave done (cycles after phase start): {per}")
 # per-block wall clock (100 MHz): KS blocks (slots 600 + 2b), KW blocks (64 + 5 blk: start, 4 wave ends)
 tr = rows[-1]
 ks = [(tr[600 + 2 * i], tr[601 + 2 * i]) for i in range(min(B, 200))]

@@ -1043,7 +1043,7 @@ class LeNetEngine {
       P_.wimg = reinterpret_cast<uint16_t*>(get("wimg", at::kShort, lenet_mfma_wimg_elems()).data_ptr<int16_t>());
       TORCH_CHECK(P_.slab1 != nullptr && (int64_t)C1 * 640 >= lenet_mfma_slab_floats(cfg), "slab1 too small");
     }
-    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 2048).data_ptr<float>();
+    if (bufs.contains("trace")) P_.trace = get("trace", at::kFloat, 4096).data_ptr<float>();
     // next-step input prep in the batch-reduction kernel (MLT_LENET_PREP=0: off, for A/B)
     const char* pe = std::getenv("MLT_LENET_PREP");
     if (bufs.contains("prep") && bufs.contains("pmeta") && !(pe && std::string(pe) == "0")) {
