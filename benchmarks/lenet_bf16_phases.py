@@ -1,6 +1,7 @@
 """Per-phase timing of the bf16 per-sample LeNet kernel (lenet_mfma.hip, LENET_TRACE): block 0
 stores s_memtime stamps at every phase boundary (each stamp adds a barrier, so the sum runs a
-little over the untraced kernel). Usage: python benchmarks/lenet_bf16_phases.py [batch] [--jsonl F]"""
+little over the untraced kernel). Needs a trace build (-DMLT_LENET_TRACE_BUILD=1: the stamps are
+compiled out of the shipped kernel). Usage: python benchmarks/lenet_bf16_phases.py [batch] [--jsonl F]"""
 import json
 import os
 import sys
@@ -17,6 +18,10 @@ args = [a for a in sys.argv[1:] if not a.startswith("--")]
 B = int(args[0]) if args else 32
 out = sys.argv[sys.argv.index("--jsonl") + 1] if "--jsonl" in sys.argv else None
 dev = torch.device("cuda", 0)
+from ml_trainer_amd.ops._ext import require_native  # noqa: E402
+if not require_native().lenet_mfma_trace_build():
+    sys.exit("lenet_bf16_phases.py needs a trace build of the extension: python -c \"from ml_trainer_amd.build "
+             "import build; build(extra_flags={'lenet_mfma.hip': ['-DMLT_LENET_TRACE_BUILD=1']})\"")
 torch.manual_seed(0)
 m = MLModel().to(dev)
 flat = FlatParams(m.parameters())
@@ -80,12 +85,14 @@ for name, open_slot, k in wph:
         per.append(d[len(d) // 2] if d else None)
     rec["wave_done_cycles"][name] = per
     print(f"  {name:32s} wave done (cycles after phase start): {per}")
-# per-block wall clock (100 MHz): KS blocks (slots 600 + 2b), KW blocks (64 + 5 blk: start, 4 wave ends)
+# per-block wall clock (100 MHz): KS blocks (slots 600 + 2b), KW blocks (1200 + 5 blk: start, 4 wave ends;
+# the B prep blocks follow the reduction blocks)
 tr = rows[-1]
 ks = [(tr[600 + 2 * i], tr[601 + 2 * i]) for i in range(min(B, 200))]
 C = eng.C
 nkw = C.lenet_mfma_kw_blocks(m.cfg_id)
-kw = [(tr[64 + 5 * i], max(tr[65 + 5 * i:69 + 5 * i])) for i in range(min(nkw, 100))]
+kw = [(tr[1200 + 5 * i], max(tr[1201 + 5 * i:1205 + 5 * i])) for i in range(min(nkw, 160))]
+kwp = [(tr[1200 + 5 * i], max(tr[1201 + 5 * i:1205 + 5 * i])) for i in range(nkw, min(nkw + B, 160))]
 t0 = min(a for a, _ in ks)
 ks_end = max(e for _, e in ks)
 print(f"KS blocks: start spread {(max(a for a, _ in ks) - t0) * 10} ns, block time "
@@ -98,6 +105,10 @@ if kw:
     slow = sorted(range(len(kw)), key=lambda i: kw[i][1])[-5:]
     print("  latest-ending KW blocks:", [(i, (kw[i][0] - k0) * 10, (kw[i][1] - k0) * 10) for i in slow])
     rec["kw_block_ns"] = [[(a - k0) * 10, (e - k0) * 10] for a, e in kw]
+    if kwp and all(a and e for a, e in kwp):
+        print(f"  prep blocks ({len(kwp)}): start {(min(a for a, _ in kwp) - k0) * 10}..{(max(a for a, _ in kwp) - k0) * 10} ns, "
+              f"end {(min(e for _, e in kwp) - k0) * 10}..{(max(e for _, e in kwp) - k0) * 10} ns after the first KW start")
+        rec["kw_prep_block_ns"] = [[(a - k0) * 10, (e - k0) * 10] for a, e in kwp]
 if out:
     with open(out, "a") as f:
         f.write(json.dumps(rec) + "\n")

@@ -1364,6 +1364,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_w4q8", &set_gemm_w4q8, py::arg("on"));
   m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
   m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
+  m.def("lenet_mfma_trace_build", &lenet_mfma_trace_build);
   m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));
   m.def("lenet_mfma_kw_blocks", &lenet_mfma_kw_blocks, py::arg("cfg"));
   m.def("lenet_mfma_xch_granules", &lenet_mfma_xch_granules, py::arg("cfg"));

@@ -119,6 +119,7 @@ struct XgmiFused;
 void launch_lenet_mfma_dp(int cfg, int mode, int B, const LeNetPtrs& P, const LeNetAug& A, const LeNetOpt& O,
                           const XgmiFused& X, hipStream_t stream);
 int lenet_mfma_wimg_elems();
+bool lenet_mfma_trace_build();  // LENET_TRACE stamps compiled in (MLT_LENET_TRACE_BUILD)
 // batch reductions (+ the exchange when X) into O.g only, no update (transport self-test / timing)
 void launch_lenet_mfma_reduce(int cfg, int B, const LeNetPtrs& P, const LeNetOpt& O, const XgmiFused* X,
                               hipStream_t stream);

@@ -24,6 +24,7 @@ void launch_lenet_mfma_reduce(int cfg, int B, const LeNetPtrs& P, const LeNetOpt
 }
 int lenet_mfma_slab_floats(int cfg) { return cfg == LENET_TINY ? lm::DmTiny::SLABN : lm::DmDefault::SLABN; }
 int lenet_mfma_wimg_elems() { return lm::kWimgTot; }
+bool lenet_mfma_trace_build() { return lm::kTraceBuild; }
 int lenet_mfma_kw_blocks(int cfg) {
   return cfg == LENET_TINY ? lm::mw_conv_blocks<lm::DmTiny>() + lm::mw_fc_blocks<lm::DmTiny>() + 1
                            : lm::mw_conv_blocks<lm::DmDefault>() + lm::mw_fc_blocks<lm::DmDefault>() + 1;
