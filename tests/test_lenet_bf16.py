@@ -173,6 +173,12 @@ def test_bf16_staging_bitwise(dev):
                 assert meta[:, 0].tolist() == [ep * 10 + 9] * 12, meta
                 assert meta[:, 1].tolist() == list(range(288, 300)), meta
                 assert meta[:, 2].tolist() == targets[perm[288:]].tolist()
+                # ... from the raw images the 9th step's per-sample kernel staged for them (meta2:
+                # step, position, dataset row, target)
+                m2 = eng.bufs["meta2"].view(-1, 4)[:12].cpu()
+                assert m2[:, 0].tolist() == [ep * 10 + 9] * 12, m2
+                assert m2[:, 2].tolist() == perm[288:].tolist(), m2
+                assert m2[:, 3].tolist() == targets[perm[288:]].tolist(), m2
             else:
                 for _ in range(9):
                     eng._reset_staging()
