@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
                     help="BERT modes, N>1: gradient all-reduce wire dtype (bf16 = cast in the bucket, reduce, "
                          "cast back into the fp32 gradient)")
+    ap.add_argument("--no-prewarm", action="store_true",
+                    help="LeNet bf16: no pre-launch of the timed graphs (steps per graph then divide the warmup)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="LeNet steps per captured hipGraph (0 = auto: min(steps, 64))")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
@@ -359,11 +361,20 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     # steps per graph: the largest d <= 64 dividing both K and W, so that the warmup replays the very
     # graph the timed steps replay (a freshly uploaded graph's first replay costs ~40 us more, measured
     # by scripts/debug/replay_cold.py); min(64, K) when they share no useful divisor
+    # With graph pre-warming (the bf16 step, single rank or the fused xGMI exchange): one graph for
+    # the whole timed run when K <= 64 (else the largest divisor of K up to 64; 250-step graphs ran
+    # ~1 us per step slower), its first-launch cost paid before t0 (engine.prewarm: one launch of
+    # each timed graph, then every tensor it wrote restored from a snapshot -- the timed steps start
+    # from bitwise the state the warmup left; profiles/r6/lenet_spg_sync_ab.jsonl: a cold graph
+    # costs ~20 us on its first launch, and each extra graph launch in the timed region ~7 us)
     spg = args.steps_per_graph
-    if not spg:
+    use_graph = not args.no_graph
+    prewarm = use_graph and not args.no_prewarm and engine.can_prewarm()
+    if not spg and prewarm:
+        spg = max(d for d in range(1, min(64, args.steps) + 1) if args.steps % d == 0)
+    elif not spg:
         common = [d for d in range(1, 65) if args.steps % d == 0 and args.warmup > 0 and args.warmup % d == 0]
         spg = max(common) if common and max(common) >= 4 else max(1, min(64, args.steps))
-    use_graph = not args.no_graph
 
     state = {"epoch": 0, "shard_len": 0, "step_in_epoch": 0, "steps_per_epoch": 0}
 
@@ -390,6 +401,13 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     # region on this stack (21.1-21.9 vs 19.6-19.7 us/step at K=20,
     # profiles/r4/lenet_timed_region_events_ab.jsonl); per-kernel device times come from rocprofv3
     run(args.warmup)
+    prewarmed = 0
+    if prewarm:  # one launch of every graph the timed steps replay, state restored bitwise
+        seen = set()
+        for ev in lenet_plan(args.steps, dict(state), N, world, rank, per_gpu, spg, shard_indices):
+            if ev[0] == "steps" and ev[1:] not in seen:
+                seen.add(ev[1:])
+                prewarmed += engine.prewarm(ev[1], ev[2], steps_per_graph=ev[3])
     captures_before = engine.captures
     torch.cuda.synchronize()
     if world > 1:
@@ -452,6 +470,7 @@ def bench_lenet(args, world, rank, dev, backend, precision):
                    "global_batch": per_gpu * world, "per_gpu_batch": per_gpu, "seq_len": None,
                    "parallelism": f"dp{world}", "optimizer": f"{args.optimizer} lr=1e-3 momentum=0.9",
                    "hipgraph_steps": 0 if args.no_graph else spg,
+                   "graph_prewarm": prewarmed,
                    "kernels_per_step": round(nodes / spg, 2) if nodes else None,
                    "update": ("pipelined: step k's batch reductions / exchange / optimizer update run in "
                               "step k+1's launch beside its sample blocks' input phase"
@@ -492,6 +511,13 @@ def main():
         # profiles/r5/bert_base_batch_1024_1536.jsonl)
         args.batch = {"bert-base": 1536, "bert-large": 256, "large": 512, "bert-tiny": 32}.get(args.model, 32)
 
+    # host waits spin instead of yield (before anything creates the device's context; MLT_SYNC_SPIN=0
+    # keeps ROCm's default): the timed region ends in one synchronize
+    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
+    spin = False
+    if args.device != "cpu" and torch.cuda.device_count() > 0:
+        from ml_trainer_amd.parallel.dist import set_sync_spin
+        spin = set_sync_spin(0 if same_dev else local_rank)
     if args.device == "cpu" or not torch.cuda.is_available():
         if world > 1:
             dist.init_process_group("gloo")
@@ -504,7 +530,6 @@ def main():
         return
 
     # rehearsal knob for a 1-GPU box (not for real runs): all ranks on GPU 0 over gloo
-    same_dev = os.environ.get("MLT_BENCH_SAME_DEVICE") == "1"
     dev = torch.device("cuda", 0 if same_dev else local_rank)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -517,13 +542,16 @@ def main():
     if args.model in ("bert-base", "bert-tiny", "bert-large", "large"):
         if args.steps == 3000 and args.warmup == 300:  # LeNet-sized defaults -> BERT-sized
             args.steps, args.warmup = 20, 5
-        _emit(bench_bert(args, world, rank, dev), rank, args)
+        r = bench_bert(args, world, rank, dev)
+        r["config"]["host_sync"] = "spin" if spin else "default"
+        _emit(r, rank, args)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
 
     out = bench_lenet(args, world, rank, dev, backend, args.precision)
+    out["config"]["host_sync"] = "spin" if spin else "default"
     if args.precision == "bf16" and not args.no_fp32_companion:
         # same-dtype comparison with the reference (fp32), same protocol, after the headline run
         comp = bench_lenet(args, world, rank, dev, backend, "fp32")

@@ -1365,6 +1365,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_lenet_variant", &set_lenet_variant, py::arg("variant"));
   m.def("lenet_mfma_wimg_elems", &lenet_mfma_wimg_elems);
   m.def("lenet_mfma_trace_build", &lenet_mfma_trace_build);
+  // host-side completion waits of a device: spin (lowest latency; the launch-bound LeNet step
+  // syncs per epoch / per timed region) instead of ROCm's default yield. Call before the device's
+  // context is active; returns the hipError_t (hipErrorSetOnActiveProcess: too late, unchanged).
+  m.def("set_device_sync_spin", [](int device) {
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipSetDeviceFlags(hipDeviceScheduleSpin);
+    return (int)e;
+  });
   m.def("lenet_mfma_slab_floats", &lenet_mfma_slab_floats, py::arg("cfg"));
   m.def("lenet_mfma_kw_blocks", &lenet_mfma_kw_blocks, py::arg("cfg"));
   m.def("lenet_mfma_xch_granules", &lenet_mfma_xch_granules, py::arg("cfg"));

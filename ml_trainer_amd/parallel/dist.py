@@ -42,6 +42,26 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", os.environ.get("SLURM_LOCALID", "0")))
 
 
+def set_sync_spin(device_index: int) -> bool:
+    """Make host waits on ``device_index`` spin instead of yield (``hipDeviceScheduleSpin``; ROCm's
+    default heuristic yields when the host has more cores than HIP contexts). Must run before the
+    device's context is active -- i.e. before the first tensor / stream / graph on it. Opt out with
+    MLT_SYNC_SPIN=0. Returns whether the flag took effect."""
+    if os.environ.get("MLT_SYNC_SPIN", "1") == "0":
+        return False
+    try:
+        from ml_trainer_amd.ops._ext import native_available, require_native
+        if not native_available():
+            return False
+        err = require_native().set_device_sync_spin(int(device_index))
+    except Exception as e:  # pragma: no cover - best effort, never fatal
+        logger.warning(f"spin sync not set: {e!r}")
+        return False
+    if err != 0:
+        logger.warning(f"spin sync not set on device {device_index}: hipError {err}")
+    return err == 0
+
+
 def bind_device(prefer_gpu: bool = True) -> torch.device:
     """Select the device for this process (LOCAL_RANK-th GPU) before anything touches it."""
     if prefer_gpu and torch.cuda.is_available():
@@ -51,6 +71,7 @@ def bind_device(prefer_gpu: bool = True) -> torch.device:
         n = torch.cuda.device_count()
         if lr >= n:
             raise RuntimeError(f"LOCAL_RANK={lr} but only {n} GPUs are visible")
+        set_sync_spin(lr)
         torch.cuda.set_device(lr)
         return torch.device("cuda", lr)
     return torch.device("cpu")

@@ -150,6 +150,38 @@ def test_bf16_graph_equals_eager_bitwise(dev):
 
 
 @pytest.mark.gpu
+def test_bf16_prewarm_is_a_bitwise_noop(dev):
+    """engine.prewarm launches the graphs of the next steps once and restores every tensor they
+    wrote: all engine buffers, weights, gradients, optimizer state and counters are bitwise what
+    they were, and training after it == training without it, bit for bit (adam: state + step)."""
+    data, targets = _toy_data(300, 5)
+    runs = []
+    for pre in (False, True):
+        m = _mk("default", 4).to(dev)
+        eng, flat = _engine(m, "adam", max_batch=32, lr=1e-3)
+        eng.set_dataset(data, targets, batch_size=32)
+        eng.start_epoch(torch.randperm(300, generator=torch.Generator().manual_seed(3)))
+        eng.train_steps(32, 2, use_graph=True, steps_per_graph=2)
+        if pre:
+            torch.cuda.synchronize()
+            state = eng._state_tensors()
+            assert any(t.data_ptr() == flat.data.data_ptr() for t in state)
+            assert len([t for t in state if t.dtype == torch.float32]) >= 4  # (+ adam's two moments)
+            before = [t.clone() for t in state]
+            assert eng.can_prewarm()
+            assert eng.prewarm(32, 6, steps_per_graph=3) == 1
+            torch.cuda.synchronize()
+            for i, (a, b) in enumerate(zip(state, before)):  # bitwise (scratch may hold NaN patterns)
+                assert torch.equal(a.reshape(-1).view(torch.uint8), b.reshape(-1).view(torch.uint8)), i
+        eng.train_steps(32, 6, use_graph=True, steps_per_graph=3)
+        torch.cuda.synchronize()
+        runs.append((flat.data.clone(), eng.stats.clone(), eng.ctrl.clone()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert runs[1][2].tolist() == [8, 8]
+
+
+@pytest.mark.gpu
 def test_bf16_staging_bitwise(dev):
     """The batch-reduction kernel's prep blocks augment the next step's inputs (pixels + tags);
     a step uses them only on a tag match. Training with prepared inputs (graphs, two epochs, a
