@@ -78,7 +78,7 @@ def parse():
                     help="BERT modes, N>1: gradient all-reduce wire dtype (bf16 = cast in the bucket, reduce, "
                          "cast back into the fp32 gradient)")
     ap.add_argument("--no-prewarm", action="store_true",
-                    help="LeNet bf16: no pre-launch of the timed graphs (steps per graph then divide the warmup)")
+                    help="LeNet: no pre-launch of the timed graphs (steps per graph then divide the warmup)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="LeNet steps per captured hipGraph (0 = auto: min(steps, 64))")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
@@ -361,7 +361,7 @@ def bench_lenet(args, world, rank, dev, backend, precision):
     # steps per graph: the largest d <= 64 dividing both K and W, so that the warmup replays the very
     # graph the timed steps replay (a freshly uploaded graph's first replay costs ~40 us more, measured
     # by scripts/debug/replay_cold.py); min(64, K) when they share no useful divisor
-    # With graph pre-warming (the bf16 step, single rank or the fused xGMI exchange): one graph for
+    # With graph pre-warming (single rank, or the bf16 step's fused xGMI exchange): one graph for
     # the whole timed run when K <= 64 (else the largest divisor of K up to 64; 250-step graphs ran
     # ~1 us per step slower), its first-launch cost paid before t0 (engine.prewarm: one launch of
     # each timed graph, then every tensor it wrote restored from a snapshot -- the timed steps start

@@ -468,11 +468,11 @@ class LeNetStepEngine:
         return new
 
     def can_prewarm(self) -> bool:
-        """Whether prewarm() applies: the bf16 step replayed from graphs, single rank or the fused
-        xGMI exchange (every buffer those graphs write is engine / optimizer state it can snapshot;
-        the exchange's own launch counters are not restored: they advance on every rank alike)."""
-        return self.precision == "bf16" and (self.fused or self.in_graph_collective) and \
-            self.dp_transport in ("none", "xgmi-fused")
+        """Whether prewarm() applies: the step replayed from graphs on a single rank (bf16 or fp32)
+        or through the fused xGMI exchange (every buffer those graphs write is engine / optimizer
+        state it can snapshot; the exchange's own launch counters are not restored: they advance on
+        every rank alike)."""
+        return (self.fused or self.in_graph_collective) and self.dp_transport in ("none", "xgmi-fused")
 
     def _state_tensors(self):
         """Every device tensor the step graphs write: engine buffers (activations, slabs, staging,

@@ -150,7 +150,8 @@ def test_bf16_graph_equals_eager_bitwise(dev):
 
 
 @pytest.mark.gpu
-def test_bf16_prewarm_is_a_bitwise_noop(dev):
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_bf16_prewarm_is_a_bitwise_noop(dev, precision):
     """engine.prewarm launches the graphs of the next steps once and restores every tensor they
     wrote: all engine buffers, weights, gradients, optimizer state and counters are bitwise what
     they were, and training after it == training without it, bit for bit (adam: state + step)."""
@@ -158,7 +159,7 @@ def test_bf16_prewarm_is_a_bitwise_noop(dev):
     runs = []
     for pre in (False, True):
         m = _mk("default", 4).to(dev)
-        eng, flat = _engine(m, "adam", max_batch=32, lr=1e-3)
+        eng, flat = _engine(m, "adam", max_batch=32, lr=1e-3, precision=precision)
         eng.set_dataset(data, targets, batch_size=32)
         eng.start_epoch(torch.randperm(300, generator=torch.Generator().manual_seed(3)))
         eng.train_steps(32, 2, use_graph=True, steps_per_graph=2)
