@@ -786,7 +786,8 @@ void attn_fwd(Tensor qkv, Tensor out, Tensor lse, c10::optional<Tensor> lens, in
 
 void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10::optional<Tensor> lens, Tensor dqkv,
               int64_t B, int64_t S, int64_t H, double scale, c10::optional<Tensor> colsum_out,
-              bool colsum_accumulate) {
+              bool colsum_accumulate, c10::optional<Tensor> q8_y, c10::optional<Tensor> q8_yt,
+              c10::optional<Tensor> q8_scale, c10::optional<Tensor> q8_amax) {
   const int64_t D = H * 64;
   check_bf16_2d(qkv, "qkv", B * S, 3 * D);
   check_bf16_2d(out, "out", B * S, D);
@@ -802,12 +803,32 @@ void attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, c10
     pq = at::empty({rows * D}, qkv.options().dtype(at::kFloat));
     pkv = at::empty({rows * 2 * D}, qkv.options().dtype(at::kFloat));
   }
+  AttnQ8 q8;
+  if (q8_y.has_value()) {  // fp8 training: e5m2 dQKV + transpose + amax instead of the bf16 dQKV
+    TORCH_CHECK(q8_yt.has_value() && q8_scale.has_value() && q8_amax.has_value(), "attn_bwd q8: y, yt, scale, amax");
+    TORCH_CHECK(q8_y->scalar_type() == at::kFloat8_e5m2 && q8_yt->scalar_type() == at::kFloat8_e5m2,
+                "attn_bwd q8: e5m2 outputs");
+    TORCH_CHECK(q8_y->is_cuda() && q8_y->is_contiguous() && q8_y->dim() == 2 && q8_y->size(0) == B * S &&
+                    q8_y->size(1) == 3 * D, "attn_bwd q8: y must be [B*S, 3D] contiguous");
+    TORCH_CHECK(q8_yt->is_cuda() && q8_yt->is_contiguous() && q8_yt->dim() == 2 && q8_yt->size(0) == 3 * D &&
+                    q8_yt->size(1) == B * S, "attn_bwd q8: yt must be [3D, B*S] contiguous");
+    TORCH_CHECK(S % 16 == 0 && reinterpret_cast<uintptr_t>(q8_yt->data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(q8_y->data_ptr()) % 4 == 0, "attn_bwd q8: S % 16 == 0, aligned outputs");
+    check_dev(*q8_scale, "q8_scale", at::kFloat, 1, 4);
+    check_dev(*q8_amax, "q8_amax", at::kFloat, (int64_t)kAmaxSlots * kAmaxStride, 4);
+    q8.y = (uint8_t*)q8_y->data_ptr();
+    q8.yt = (uint8_t*)q8_yt->data_ptr();
+    q8.scale = q8_scale->data_ptr<float>();
+    q8.amax = q8_amax->data_ptr<float>();
+    q8.ldt = B * S;
+  }
   int rq = 0, rkv = 0;
   const bool fused = launch_attn_bwd(bf16_ptr(qkv), bf16_ptr(out), bf16_ptr(dout), lse.data_ptr<float>(),
                                      delta.data_ptr<float>(), lens_ptr(lens, B), (uint16_t*)dqkv.data_ptr(), (int)B,
                                      (int)S, (int)H, (float)scale, cur_stream(),
                                      pq.defined() ? pq.data_ptr<float>() : nullptr,
-                                     pkv.defined() ? pkv.data_ptr<float>() : nullptr, &rq, &rkv);
+                                     pkv.defined() ? pkv.data_ptr<float>() : nullptr, &rq, &rkv, q8);
+  TORCH_CHECK(!q8.y || !colsum_out.has_value() || fused, "attn_bwd q8: column sums need the ring kernels");
   if (!colsum_out.has_value()) return;
   float* cs = colsum_out->data_ptr<float>();
   const int acc = colsum_accumulate ? 1 : 0;
@@ -1403,7 +1424,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("delta"),
         py::arg("lens"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"),
-        py::arg("colsum_out") = py::none(), py::arg("colsum_accumulate") = false);
+        py::arg("colsum_out") = py::none(), py::arg("colsum_accumulate") = false, py::arg("q8_y") = py::none(),
+        py::arg("q8_yt") = py::none(), py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none());
   py::class_<PyComm>(m, "Communicator")
       .def(py::init<py::bytes, int, int, int>(), py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
            py::arg("device"))

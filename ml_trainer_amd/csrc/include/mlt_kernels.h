@@ -301,9 +301,20 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* 
 // colpart_q [B * ceil(S/64)][D] and colpart_kv [B * ceil(S/64)][2D] (or nullptr): bias-gradient
 // column partials of dQ and dK|dV; returns whether they were written (ring kernels) and the
 // number of partial rows in rows_q / rows_kv
+// q8 (fp8 training, y != nullptr): instead of the bf16 dQKV, the backward kernels write its e5m2
+// copy y [B*S][3D] and transpose yt [3D][B*S] -- each value the bf16 one rounded first, then scaled
+// by *scale and quantised exactly as fp8_cast_transpose would -- and record amax(|dQKV|) into the
+// kAmaxSlots sub-slots at amax (the ring kernels only; S % 16 == 0)
+struct AttnQ8 {
+  uint8_t* y = nullptr;
+  uint8_t* yt = nullptr;
+  const float* scale = nullptr;
+  float* amax = nullptr;
+  int64_t ldt = 0;  // yt row stride (B * S)
+};
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
                      const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st,
                      float* colpart_q = nullptr, float* colpart_kv = nullptr, int* rows_q = nullptr,
-                     int* rows_kv = nullptr);
+                     int* rows_kv = nullptr, const AttnQ8& q8 = AttnQ8{});
 
 }  // namespace mlt

@@ -23,9 +23,11 @@
 // Global->LDS staging of the next tile is register-staged (loads issued before the MFMA work
 // of the current tile, LDS writes after it), so HBM latency overlaps the math.
 #include <cstdlib>
+#include <stdexcept>
 #include <type_traits>
 
 #include "mlt_common.h"
+#include "mlt_fp8.h"
 #include "mlt_kernels.h"
 
 namespace mlt {
@@ -786,6 +788,59 @@ __device__ __forceinline__ void block_colsum64(float (&v)[4][4], float* red, flo
     out[threadIdx.x] = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
 }
 
+// q8 epilogue of a ring backward kernel (AttnQ8): NT tensors (dK, dV: 2; dQ: 1) of this block's
+// NR = 64 * groups rows x 64 head dims. v[t][n][d][r] is the fp32 value of row n * 64 + wid * 16 + i,
+// dim d * 16 + 4 g + r. Each value is rounded to bf16 first (what the bf16 store would hold), so y,
+// yt and amax are bitwise those of fp8_cast_transpose over the bf16 dQKV. Row-major bytes go
+// straight out (4 dims per lane, one dword); the transpose is staged through LDS (the ring's
+// space, free after the loop) so that each thread stores 16-byte runs of rows.
+// col0[t]: first column of tensor t in the packed 3D layout (+ h * 64); rows beyond S are skipped.
+template <int NT, int NG>
+__device__ __forceinline__ void attn_q8_epilogue(const AttnQ8& q8, const float (&v)[NT][NG][4][4], uint8_t* smem,
+                                                 int64_t base, int row0, int S, int D, const int (&col0)[NT]) {
+  constexpr int NR = 64 * NG, TP = NR + 16;  // rows per block; LDS pitch of a transposed row
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const float sc = *q8.scale;
+  const int64_t ld3 = 3 * (int64_t)D;
+  float mx = 0.f;
+  __syncthreads();  // every wave is past its last ring-stage read
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int n = 0; n < NG; ++n) {
+      const int rl = n * 64 + wid * 16 + i, row = row0 + rl;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = __uint_as_float((unsigned)f32_to_bf16(v[t][n][d][r]) << 16);
+          mx = row < S ? fmaxf(mx, fabsf(f[r])) : mx;
+        }
+        const uint32_t q = pack4_fp8<1>(f[0] * sc, f[1] * sc, f[2] * sc, f[3] * sc);
+        if (row < S) *reinterpret_cast<uint32_t*>(q8.y + (base + row) * ld3 + col0[t] + d * 16 + 4 * g) = q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) smem[(t * 64 + d * 16 + 4 * g + r) * TP + rl] = (uint8_t)(q >> (8 * r));
+      }
+    }
+  __syncthreads();
+  // NT x 64 transposed rows of NR bytes: 16-byte runs
+  constexpr int RUNS = NR / 16;
+  for (int e = threadIdx.x; e < NT * 64 * RUNS; e += blockDim.x) {
+    const int tr = e / RUNS, c = e - tr * RUNS, t = tr >> 6, dim = tr & 63;
+    if (row0 + 16 * c < S) {
+      const uint4 w = *reinterpret_cast<const uint4*>(smem + tr * TP + 16 * c);
+      *reinterpret_cast<uint4*>(q8.yt + (int64_t)(col0[t] + dim) * q8.ldt + base + row0 + 16 * c) = w;
+    }
+  }
+  mx = wave_max(mx);
+  float* red = reinterpret_cast<float*>(smem + NT * 64 * TP);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_pos(q8.amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  __syncthreads();  // (the caller's column-sum pass reuses the LDS)
+}
+
 // FULLT: S % 64 == 0 (every ring stage a whole tile: the clamped-row copy path is compiled out, which
 // keeps the 2-group kernel within 256 VGPRs)
 template <int NK, int kRing, bool FULLT>
@@ -795,7 +850,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
                                                                  const float* __restrict__ delta,
                                                                  const int* __restrict__ lens,
                                                                  uint16_t* __restrict__ dqkv, int S, int H,
-                                                                 float scale, float* __restrict__ colpart) {
+                                                                 float scale, float* __restrict__ colpart, AttnQ8 q8) {
   constexpr int STAGE = 2 * kTile + 2 * AB * 4;  // Q tile, dO tile, lse[64], delta[64]
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
   int kbk, h, b;
@@ -812,8 +867,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
     for (int e = threadIdx.x; e < 64 * NK * AH; e += 256) {
       const int kk = k0b + e / AH, d = e % AH;
       if (kk < S) {
-        dqkv[(base + kk) * ld + D + h * AH + d] = 0;
-        dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
+        if (q8.y) {
+          q8.y[(base + kk) * ld + D + h * AH + d] = 0;
+          q8.y[(base + kk) * ld + 2 * D + h * AH + d] = 0;
+          q8.yt[(int64_t)(D + h * AH + d) * q8.ldt + base + kk] = 0;
+          q8.yt[(int64_t)(2 * D + h * AH + d) * q8.ldt + base + kk] = 0;
+        } else {
+          dqkv[(base + kk) * ld + D + h * AH + d] = 0;
+          dqkv[(base + kk) * ld + 2 * D + h * AH + d] = 0;
+        }
       }
     }
     if (cp && threadIdx.x < 64) {
@@ -995,6 +1057,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
       }
     }
   }
+  if (q8.y) {  // fp8 training: e5m2 dK | dV and their transposes instead of the bf16 dQKV
+    float v[2][NK][4][4];
+#pragma unroll
+    for (int n = 0; n < NK; ++n)
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[0][n][d][r] = dk[n][d][r] * scale;
+          v[1][n][d][r] = dv[n][d][r];
+        }
+    const int col0[2] = {D + h * AH, 2 * D + h * AH};
+    attn_q8_epilogue<2, NK>(q8, v, smem, base, k0b, S, D, col0);
+  } else {
 #pragma unroll
   for (int n = 0; n < NK; ++n) {
     if (key[n] < S) {
@@ -1015,6 +1091,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_ring_kernel(const uint16
         *reinterpret_cast<ushort4*>(vp) = uv;
       }
     }
+  }
   }
   if (cp) {  // bias-gradient partials of dK and dV over this block's keys
     float vk[4][4], vv[4][4];
@@ -1048,7 +1125,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
                                                                float* __restrict__ delta,
                                                                const int* __restrict__ lens,
                                                                uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                               float* __restrict__ colpart) {
+                                                               float* __restrict__ colpart, AttnQ8 q8) {
   constexpr int STAGE = 2 * kTile;  // K tile, V tile
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * STAGE];
   int qb, h, b;
@@ -1199,6 +1276,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
       }
     }
   }
+  if (q8.y) {  // fp8 training: e5m2 dQ and its transpose instead of the bf16 dQKV
+    float v[1][NQ][4][4];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[0][n][d][r] = acc[n][d][r] * scale;
+    const int col0[1] = {h * AH};
+    attn_q8_epilogue<1, NQ>(q8, v, smem, base, qb * (64 * NQ), S, D, col0);
+  } else {
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     if (q[n] < S) {
@@ -1213,6 +1301,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ring_kernel(const uint16_t* _
         *reinterpret_cast<ushort4*>(qp + d * 16 + 4 * g) = u;
       }
     }
+  }
   }
   if (colpart) {  // bias-gradient partials of dQ over this block's queries: [B * query blocks][D]
     float vq[4][4];
@@ -1254,7 +1343,7 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, const int* 
 
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
                      const int* lens, uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st,
-                     float* colpart_q, float* colpart_kv, int* rows_q, int* rows_kv) {
+                     float* colpart_q, float* colpart_kv, int* rows_q, int* rows_kv, const AttnQ8& q8) {
   if (B <= 0 || S <= 0) return false;
   const int64_t pairs = (int64_t)B * S * H;
   const dim3 g2((S + 127) / 128 * H * B), g1((S + 63) / 64 * H * B);
@@ -1267,16 +1356,16 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   {                                                                                                                   \
     if (q2)                                                                                                           \
       hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<2, RD, FL>), g2, dim3(256), 0, st, qkv, dout, out, lse, delta, lens, \
-                         dqkv, S, H, scale, colpart_q);                                                               \
+                         dqkv, S, H, scale, colpart_q, q8);                                                           \
     else                                                                                                              \
       hipLaunchKernelGGL((attn_bwd_dq_ring_kernel<1, RD, FL>), g1, dim3(256), 0, st, qkv, dout, out, lse, delta, lens, \
-                         dqkv, S, H, scale, colpart_q);                                                               \
+                         dqkv, S, H, scale, colpart_q, q8);                                                           \
     if (k2)                                                                                                           \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<2, RD, FL>), g2, dim3(256), 0, st, qkv, dout, lse, delta, lens,   \
-                         dqkv, S, H, scale, colpart_kv);                                                              \
+                         dqkv, S, H, scale, colpart_kv, q8);                                                          \
     else                                                                                                              \
       hipLaunchKernelGGL((attn_bwd_dkdv_ring_kernel<1, RD, FL>), g1, dim3(256), 0, st, qkv, dout, lse, delta, lens,   \
-                         dqkv, S, H, scale, colpart_kv);                                                              \
+                         dqkv, S, H, scale, colpart_kv, q8);                                                          \
   }
     const bool full = S % AB == 0;
     if (ring == 3) {
@@ -1290,6 +1379,7 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     if (rows_q) *rows_q = B * ((S + (q2 ? 127 : 63)) / (q2 ? 128 : 64));
     return colpart_q != nullptr && colpart_kv != nullptr;
   }
+  if (q8.y) throw std::runtime_error("attn_bwd: the fp8 (q8) outputs need the ring kernels (MLT_ATTN_RING=3|4)");
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, st, dout, out, delta,
                      (int64_t)B * S, H);
   if (attn_groups("MLT_ATTN_DKDV_GROUPS", S, 1) == 2)

@@ -238,6 +238,36 @@ class Fp8Linear:
         return out
 
 
+    # ---- attention backward quantises the QKV projection's dY ------------------------------------
+    # The dQ and dK/dV kernels write dQKV as e5m2 with its transpose and amax (attn_bwd q8_*), from
+    # the bf16-rounded values, bitwise what fp8_cast_transpose of the bf16 dQKV gives: the widest
+    # cast of the layer (3 x hidden columns) and the bf16 dQKV itself disappear.
+    fuse_attn = os.environ.get("MLT_FP8_ATTN_Q", "1") != "0"
+
+    @staticmethod
+    def attn_dy_q(wqkv, x, rows: int):
+        """(dqkv8, dqkv8^T, scale, amax) buffers for attn_bwd's q8 outputs when Wqkv's e5m2 dY scale
+        exists and the forward left X^T for its fp8 weight gradient; else None."""
+        if not Fp8Linear.fuse_attn:
+            return None
+        st = getattr(wqkv, "_mlt_f8", None)
+        if st is None or st.xt is None or st.xt[0] != x.data_ptr() or not _fp8_wgrad_ok(x, wqkv):
+            return None
+        ctx = context(x.device)
+        if not ctx._ready[st.mdy] or rows % 16:
+            return None
+        n = wqkv.shape[0]
+        d8 = torch.empty(rows, n, dtype=_DT[E5M2], device=x.device)
+        d8t = torch.empty(n, rows, dtype=_DT[E5M2], device=x.device)
+        return d8, d8t, ctx.scale[st.mdy:st.mdy + 1], ctx.amax[st.mdy]
+
+    @staticmethod
+    def attn_dy_q_done(wqkv, d8, d8t):
+        """Hand the attention backward's e5m2 dY (and transpose) to Wqkv's wgrad / dgrad."""
+        st = _state(wqkv, context(d8.device))
+        st.dy8 = (d8.data_ptr(), d8)
+        st.dyt = d8t
+
     # ---- LayerNorm backward quantises the out-proj / FFN2 dY ------------------------------------
     # In the post-LN blocks the LayerNorm backward's dx is the dY of the out-projection (attention
     # block) and of FFN2: C.ln_bwd_q8 writes its e5m2 copy and transpose with that weight's dY scale

@@ -214,6 +214,23 @@ def _attn_bwd(saved, params, lens, B, S, H, dy, G, dbo="colsum", impl=BF16):
     dattn = impl.dgrad(dy, wo, torch.empty_like(attn))
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B * S * H, dtype=torch.float32, device=dy.device)
+    q8 = impl.attn_dy_q(wqkv, x, qkv.shape[0]) if (impl is not BF16 and hasattr(impl, "attn_dy_q")) else None
+    if q8 is not None:
+        # fp8: the backward kernels write dQKV as e5m2 + transpose + amax (no bf16 dQKV, no cast
+        # pass) and the QKV bias gradient as their column sums
+        d8, d8t, qs, qa = q8
+        db = None
+        if bqkv is not None:
+            gb = G.sink(bqkv)
+            db = gb if gb is not None else torch.empty(qkv.shape[1], dtype=torch.float32, device=dy.device)
+        C.attn_bwd(qkv, attn, dattn, lse, delta, lens, dqkv, B, S, H, _ATTN_SCALE, colsum_out=db,
+                   colsum_accumulate=bqkv is not None and gb is not None, q8_y=d8, q8_yt=d8t, q8_scale=qs,
+                   q8_amax=qa)
+        impl.attn_dy_q_done(wqkv, d8, d8t)
+        dwqkv = G.wgrad(wqkv, d8, x, impl)
+        dbqkv = None if (bqkv is None or gb is not None) else db
+        dx = impl.dgrad(d8, wqkv, torch.empty_like(x), res=dy)  # dx = dqkv . Wqkv + dy (residual)
+        return dx, dwqkv, dbqkv, dwo, dbo
     if impl is BF16 and bqkv is not None and _ATTN_COLSUM:
         # the QKV bias gradient (column sums of dQKV) from the backward kernels themselves
         gb = G.sink(bqkv)
