@@ -793,7 +793,9 @@ __device__ __forceinline__ void block_colsum64(float (&v)[4][4], float* red, flo
 // dim d * 16 + 4 g + r. Each value is rounded to bf16 first (what the bf16 store would hold), so y,
 // yt and amax are bitwise those of fp8_cast_transpose over the bf16 dQKV. Row-major bytes go
 // straight out (4 dims per lane, one dword); the transpose is staged through LDS (the ring's
-// space, free after the loop) so that each thread stores 16-byte runs of rows.
+// space, free after the loop) so that each thread stores 16-byte runs of rows. (Staging dwords after
+// a 4 x 4 byte transpose inside each lane quad, DPP, instead of the byte writes measured slower:
+// profiles/r6/fp8_attn_q8_dpp_ab.jsonl.)
 // col0[t]: first column of tensor t in the packed 3D layout (+ h * 64); rows beyond S are skipped.
 template <int NT, int NG>
 __device__ __forceinline__ void attn_q8_epilogue(const AttnQ8& q8, const float (&v)[NT][NG][4][4], uint8_t* smem,
