@@ -801,6 +801,7 @@ template <int NT, int NG>
 __device__ __forceinline__ void attn_q8_epilogue(const AttnQ8& q8, const float (&v)[NT][NG][4][4], uint8_t* smem,
                                                  int64_t base, int row0, int S, int D, const int (&col0)[NT]) {
   constexpr int NR = 64 * NG, TP = NR + 16;  // rows per block; LDS pitch of a transposed row
+  constexpr int YP = 64 + 16, YOFF = NT * 64 * TP;  // row-major image: pitch, offset (both 16-B multiples)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
   const float sc = *q8.scale;
   const int64_t ld3 = 3 * (int64_t)D;
@@ -820,12 +821,19 @@ __device__ __forceinline__ void attn_q8_epilogue(const AttnQ8& q8, const float (
           mx = row < S ? fmaxf(mx, fabsf(f[r])) : mx;
         }
         const uint32_t q = pack4_fp8<1>(f[0] * sc, f[1] * sc, f[2] * sc, f[3] * sc);
-        if (row < S) *reinterpret_cast<uint32_t*>(q8.y + (base + row) * ld3 + col0[t] + d * 16 + 4 * g) = q;
+        *reinterpret_cast<uint32_t*>(smem + YOFF + (t * NR + rl) * YP + d * 16 + 4 * g) = q;
 #pragma unroll
         for (int r = 0; r < 4; ++r) smem[(t * 64 + d * 16 + 4 * g + r) * TP + rl] = (uint8_t)(q >> (8 * r));
       }
     }
   __syncthreads();
+  // the row-major bytes: each row's 64 head dims as four 16-byte pieces
+  for (int e = threadIdx.x; e < NT * NR * 4; e += blockDim.x) {
+    const int tr = e >> 2, c = e & 3, t = tr / NR, rl = tr - t * NR;
+    if (row0 + rl < S)
+      *reinterpret_cast<uint4*>(q8.y + (base + row0 + rl) * ld3 + col0[t] + 16 * c) =
+          *reinterpret_cast<const uint4*>(smem + YOFF + tr * YP + 16 * c);
+  }
   // NT x 64 transposed rows of NR bytes: 16-byte runs
   constexpr int RUNS = NR / 16;
   for (int e = threadIdx.x; e < NT * 64 * RUNS; e += blockDim.x) {
@@ -836,7 +844,7 @@ __device__ __forceinline__ void attn_q8_epilogue(const AttnQ8& q8, const float (
     }
   }
   mx = wave_max(mx);
-  float* red = reinterpret_cast<float*>(smem + NT * 64 * TP);
+  float* red = reinterpret_cast<float*>(smem + YOFF + NT * NR * YP);
   if (lane == 0) red[wid] = mx;
   __syncthreads();
   if (threadIdx.x == 0) atomic_max_pos(q8.amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
